@@ -1,0 +1,161 @@
+"""Headline benchmark: ResNet-50 bf16 AMP data-parallel training throughput (images/s, whole job).
+
+    python bench.py [--gpus N --steps K --warmup W]                       # N = 1
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+Metric/config from BASELINE.json: "images/sec (whole node) ResNet-50 bf16 at 1/2/4/8
+MI355X; % step in all-reduce".  Synthetic ImageNet-shape data (3x224x224, 1000 classes),
+random-init weights, the full training step inside the timed window: forward (bf16
+autocast, channels_last), loss, loss scaling, backward with the bucketed RCCL all-reduce,
+fused SGD (lr 0.1, momentum 0.9, wd 5e-4) with the device-resident scaler, device metrics.
+W untimed warmup steps, then EXACTLY K steps bracketed by barrier + device synchronize on
+both sides; the MAX step time over ranks is reported.  Per-GPU batch is fixed as N grows
+(weak scaling).  ``vs_baseline`` divides by N x the stock-PyTorch-ROCm single-GPU number
+measured on MI355X with the same harness (``--impl torch``), since the
+reference publishes no numbers.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+# Stock PyTorch-ROCm (torch DDP defaults, foreach SGD, torch.amp.GradScaler, bf16 autocast,
+# channels_last) on one MI355X, ResNet-50, 224px: images/s per GPU at the per-GPU batch.
+STOCK_TORCH_1GPU = {128: 5736.1, 256: 6381.7}
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch-size", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--num-classes", type=int, default=1000)
+    ap.add_argument("--impl", default="native", choices=["native", "torch"])
+    ap.add_argument("--amp-dtype", default="bf16", choices=["bf16", "fp16"])
+    ap.add_argument("--no-amp", action="store_true", help="fp32 (AMP-vs-FP32 table)")
+    ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adam", "adamw"])
+    ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
+    ap.add_argument("--first-bucket-mb", type=float, default=1.0)
+    ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--profile-steps", type=int, default=0,
+                    help="extra steps after the timed window with the hipEvent sync timeline")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args(argv)
+
+
+def train_args(a):
+    from distributed_pytorch_training_amd.config import parse_args
+
+    argv = ["--model", a.model, "--dataset", "synthetic", "--batch-size", str(a.batch_size),
+            "--image-size", str(a.image_size), "--num-classes", str(a.num_classes),
+            "--impl", a.impl, "--amp-dtype", a.amp_dtype, "--optimizer", a.optimizer,
+            "--bucket-cap-mb", str(a.bucket_cap_mb), "--first-bucket-mb", str(a.first_bucket_mb),
+            "--grad-dtype", a.grad_dtype, "--lr", "0.1", "--momentum", "0.9", "--weight-decay", "5e-4"]
+    if not a.no_amp:
+        argv.append("--amp")
+    if not a.no_channels_last:
+        argv.append("--channels-last")
+    return parse_args(argv)
+
+
+def main(argv=None) -> int:
+    a = parse(argv)
+    from distributed_pytorch_training_amd.data import SyntheticLoader
+    from distributed_pytorch_training_amd.engine.trainer import Trainer
+    from distributed_pytorch_training_amd.models import build_model
+    from distributed_pytorch_training_amd.utils.dist import init_distributed, set_seed
+    from distributed_pytorch_training_amd.utils.env import setup_miopen_env
+
+    setup_miopen_env()
+    args = train_args(a)
+    info = init_distributed("auto")
+    rank, ws, device = info.rank, info.world_size, info.device
+    if ws != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={ws}; reporting WORLD_SIZE", file=sys.stderr)
+    set_seed(0, rank)
+    torch.backends.cudnn.benchmark = True
+
+    model = build_model(args.model, args.num_classes, device, image_size=args.image_size,
+                        channels_last=args.channels_last)
+    trainer = Trainer(model, args, rank, ws, device, log=lambda s: None)
+    trainer.model.train()
+    loader = SyntheticLoader(a.batch_size * 4, a.batch_size, args.image_size, args.num_classes, device,
+                             channels_last=args.channels_last, pool=4, seed=rank)
+    batches = list(iter(loader))
+
+    def run(n):
+        for i in range(n):
+            x, y = batches[i % len(batches)]
+            trainer.train_step(x, y)
+
+    def fence():
+        if ws > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device) if device.type == "cuda" else None
+
+    t_w = time.time()
+    run(a.warmup)
+    fence()
+    warm_s = time.time() - t_w
+    t0 = time.time()
+    run(a.steps)
+    fence()
+    dt = time.time() - t0
+    if ws > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms = 1e3 * dt / max(a.steps, 1)
+    value = a.batch_size * ws * a.steps / dt
+
+    prof = {}
+    if a.profile_steps > 0 and a.impl == "native":
+        trainer.timeline.enabled = device.type == "cuda"
+        run(a.profile_steps)
+        fence()
+        prof = trainer.timeline.summary(skip=1)
+
+    base = STOCK_TORCH_1GPU.get(a.batch_size) if (args.model == "resnet50" and args.amp and
+                                                  args.amp_dtype == "bf16" and args.image_size == 224) else None
+    rec = {
+        "metric": "images/sec (whole node) ResNet-50 bf16 training" if args.model == "resnet50"
+                  else f"images/sec (whole node) {args.model} training",
+        "value": round(value, 2), "unit": "images/s", "n_gpus": ws, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / (base * ws), 4) if base else None,
+        "dtype": (args.amp_dtype if args.amp else "fp32"), "data": "synthetic",
+        "config": {"model": args.model, "global_batch": a.batch_size * ws, "per_gpu_batch": a.batch_size,
+                   "seq_len": None, "image_size": args.image_size, "parallelism": f"dp{ws}",
+                   "impl": a.impl, "optimizer": a.optimizer, "channels_last": bool(args.channels_last),
+                   "bucket_cap_mb": a.bucket_cap_mb, "grad_dtype": a.grad_dtype},
+        "baseline": {"stock_torch_1gpu_img_s": base, "source": "BASELINE.md (MI355X, --impl torch)"},
+        "warmup_seconds": round(warm_s, 1),
+    }
+    if prof:
+        rec["sync_profile"] = {k: round(v, 4) if isinstance(v, float) else v for k, v in prof.items()}
+    if rank == 0:
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "a") as f:
+                f.write(line + "\n")
+    if ws > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,250 @@
+// Python bindings of the native runtime: kernel launchers (tensor-checked), the RCCL
+// communicator and the C++ reducer.  Kernels launch on the caller's current HIP stream.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include "kernels/kernels.h"
+#include "rccl_comm.h"
+#include "reducer.h"
+
+namespace py = pybind11;
+using at::Tensor;
+
+namespace {
+
+hipStream_t cur_stream(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_flat_f32(const Tensor& t, const char* name, int64_t align = 4) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor (HIP kernel path)");
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.numel() % align == 0, name, " numel must be a multiple of ", align);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+const float* opt_f32(const c10::optional<Tensor>& t, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() >= 1, name,
+              " must be a float32 GPU tensor");
+  return t->data_ptr<float>();
+}
+
+void grad_check(Tensor g, c10::optional<Tensor> scale, double host_factor, Tensor found_inf) {
+  check_flat_f32(g, "grad");
+  check_flat_f32(found_inf, "found_inf", 1);
+  c10::hip::HIPGuard guard(g.device());
+  dpt::launch_grad_check(g.data_ptr<float>(), g.numel(), opt_f32(scale, "scale"), (float)host_factor,
+                         found_inf.data_ptr<float>(), cur_stream(g));
+}
+
+void sgd_step(Tensor p, Tensor g, Tensor buf, double lr, double momentum, double dampening,
+              double wd, bool nesterov, c10::optional<Tensor> scale, double host_factor,
+              c10::optional<Tensor> found_inf, c10::optional<Tensor> step, bool zero_grad) {
+  check_flat_f32(p, "param");
+  check_flat_f32(g, "grad");
+  TORCH_CHECK(g.numel() == p.numel(), "grad/param size mismatch");
+  if (momentum != 0.0) {
+    check_flat_f32(buf, "momentum_buffer");
+    TORCH_CHECK(buf.numel() == p.numel(), "momentum buffer size mismatch");
+  }
+  c10::hip::HIPGuard guard(p.device());
+  dpt::launch_sgd(p.data_ptr<float>(), g.data_ptr<float>(),
+                  momentum != 0.0 ? buf.data_ptr<float>() : nullptr, p.numel(), (float)lr,
+                  (float)momentum, (float)dampening, (float)wd, nesterov, opt_f32(scale, "scale"),
+                  (float)host_factor, opt_f32(found_inf, "found_inf"), opt_f32(step, "step"),
+                  zero_grad, cur_stream(p));
+}
+
+void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, double lr, double beta1, double beta2,
+               double eps, double wd, bool adamw, c10::optional<Tensor> scale, double host_factor,
+               c10::optional<Tensor> found_inf, c10::optional<Tensor> step, bool zero_grad) {
+  check_flat_f32(p, "param");
+  check_flat_f32(g, "grad");
+  check_flat_f32(m, "exp_avg");
+  check_flat_f32(v, "exp_avg_sq");
+  TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(),
+              "adam arena size mismatch");
+  c10::hip::HIPGuard guard(p.device());
+  dpt::launch_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                   p.numel(), (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, adamw,
+                   opt_f32(scale, "scale"), (float)host_factor, opt_f32(found_inf, "found_inf"),
+                   opt_f32(step, "step"), zero_grad, cur_stream(p));
+}
+
+void optim_tail(c10::optional<Tensor> scale, c10::optional<Tensor> growth_tracker, Tensor found_inf,
+                c10::optional<Tensor> step, double growth_factor, double backoff_factor,
+                int64_t growth_interval) {
+  check_flat_f32(found_inf, "found_inf", 1);
+  int* gt = nullptr;
+  if (growth_tracker.has_value() && growth_tracker->defined()) {
+    TORCH_CHECK(growth_tracker->is_cuda() && growth_tracker->scalar_type() == at::kInt,
+                "growth_tracker must be an int32 GPU tensor");
+    gt = growth_tracker->data_ptr<int>();
+  }
+  float* sc = const_cast<float*>(opt_f32(scale, "scale"));
+  TORCH_CHECK(sc == nullptr || gt != nullptr, "scale needs a growth_tracker");
+  c10::hip::HIPGuard guard(found_inf.device());
+  dpt::launch_optim_tail(sc, gt, found_inf.data_ptr<float>(), const_cast<float*>(opt_f32(step, "step")),
+                         (float)growth_factor, (float)backoff_factor, (int)growth_interval,
+                         cur_stream(found_inf));
+}
+
+void pack_bf16(Tensor src, Tensor dst) {
+  check_flat_f32(src, "src", 8);
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kBFloat16 && dst.is_contiguous() &&
+                  dst.numel() == src.numel(), "dst must be a contiguous bf16 GPU tensor of src's size");
+  c10::hip::HIPGuard guard(src.device());
+  dpt::launch_pack_bf16(src.data_ptr<float>(), reinterpret_cast<uint16_t*>(dst.data_ptr()), src.numel(),
+                        cur_stream(src));
+}
+
+void unpack_bf16(Tensor src, Tensor dst, c10::optional<Tensor> scale, double host_factor,
+                 c10::optional<Tensor> found_inf) {
+  check_flat_f32(dst, "dst", 8);
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kBFloat16 && src.is_contiguous() &&
+                  dst.numel() == src.numel(), "src must be a contiguous bf16 GPU tensor of dst's size");
+  c10::hip::HIPGuard guard(dst.device());
+  dpt::launch_unpack_bf16(reinterpret_cast<const uint16_t*>(src.data_ptr()), dst.data_ptr<float>(),
+                          dst.numel(), opt_f32(scale, "scale"), (float)host_factor,
+                          const_cast<float*>(opt_f32(found_inf, "found_inf")), cur_stream(dst));
+}
+
+void accumulate_metrics(Tensor logits, Tensor targets, c10::optional<Tensor> loss, Tensor acc) {
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2, "logits must be a 2-D GPU tensor");
+  TORCH_CHECK(logits.stride(1) == 1, "logits rows must be contiguous");
+  TORCH_CHECK(targets.is_cuda() && targets.scalar_type() == at::kLong && targets.is_contiguous() &&
+                  targets.numel() == logits.size(0), "targets must be contiguous int64 [rows]");
+  TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kDouble && acc.numel() >= 3 && acc.is_contiguous(),
+              "acc must be a float64 GPU tensor with >= 3 elements");
+  int dt;
+  switch (logits.scalar_type()) {
+    case at::kFloat: dt = 0; break;
+    case at::kBFloat16: dt = 1; break;
+    case at::kHalf: dt = 2; break;
+    default: TORCH_CHECK(false, "logits dtype must be f32/bf16/f16");
+  }
+  const float* lp = nullptr;
+  Tensor lf;
+  if (loss.has_value() && loss->defined()) {
+    lf = loss->detach().to(at::kFloat).reshape({1});
+    lp = lf.data_ptr<float>();
+  }
+  c10::hip::HIPGuard guard(logits.device());
+  dpt::launch_metrics(logits.data_ptr(), dt, logits.size(0), logits.size(1), logits.stride(0),
+                      targets.data_ptr<int64_t>(), lp, acc.data_ptr<double>(), cur_stream(logits));
+}
+
+void augment(Tensor data, Tensor idx, c10::optional<Tensor> offs, c10::optional<Tensor> flips, Tensor out,
+             bool nhwc, int64_t pad, std::vector<double> mean, std::vector<double> std) {
+  TORCH_CHECK(data.is_cuda() && data.scalar_type() == at::kByte && data.dim() == 4 && data.is_contiguous(),
+              "data must be contiguous uint8 [N,C,H,W] on the GPU");
+  const int64_t C = data.size(1), H = data.size(2), W = data.size(3), B = idx.numel();
+  TORCH_CHECK(C <= 4 && (int64_t)mean.size() == C && (int64_t)std.size() == C, "mean/std must have C<=4 entries");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kLong && idx.is_contiguous(), "idx must be int64 GPU");
+  const int32_t* op = nullptr;
+  const uint8_t* fp = nullptr;
+  if (offs.has_value() && offs->defined()) {
+    TORCH_CHECK(offs->is_cuda() && offs->scalar_type() == at::kInt && offs->is_contiguous() && offs->numel() == 2 * B,
+                "offs must be int32 [B,2]");
+    op = offs->data_ptr<int32_t>();
+  }
+  if (flips.has_value() && flips->defined()) {
+    TORCH_CHECK(flips->is_cuda() && flips->scalar_type() == at::kByte && flips->numel() == B, "flips must be uint8 [B]");
+    fp = flips->data_ptr<uint8_t>();
+  }
+  TORCH_CHECK(out.is_cuda() && out.numel() == B * C * H * W, "out size mismatch");
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "out must be f32/bf16");
+  if (nhwc) {
+    TORCH_CHECK(out.is_contiguous(at::MemoryFormat::ChannelsLast), "out must be channels_last");
+  } else {
+    TORCH_CHECK(out.is_contiguous(), "out must be contiguous NCHW");
+  }
+  dpt::AugNorm n{};
+  for (int c = 0; c < C; ++c) { n.mean[c] = (float)mean[c]; n.inv_std[c] = (float)(1.0 / std[c]); }
+  c10::hip::HIPGuard guard(data.device());
+  dpt::launch_augment(data.data_ptr<uint8_t>(), idx.data_ptr<int64_t>(), op, fp, out.data_ptr(),
+                      out.scalar_type() == at::kBFloat16, nhwc, B, (int)C, (int)H, (int)W, (int)pad, n,
+                      cur_stream(data));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X-native runtime: gfx950 kernels, RCCL communicator, C++ gradient reducer";
+  m.def("grad_check", &grad_check, py::arg("grad"), py::arg("scale"), py::arg("host_factor"), py::arg("found_inf"));
+  m.def("sgd_step", &sgd_step, py::arg("param"), py::arg("grad"), py::arg("momentum_buffer"), py::arg("lr"),
+        py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"), py::arg("scale"),
+        py::arg("host_factor"), py::arg("found_inf"), py::arg("step"), py::arg("zero_grad"));
+  m.def("adam_step", &adam_step, py::arg("param"), py::arg("grad"), py::arg("exp_avg"), py::arg("exp_avg_sq"),
+        py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("adamw"),
+        py::arg("scale"), py::arg("host_factor"), py::arg("found_inf"), py::arg("step"), py::arg("zero_grad"));
+  m.def("optim_tail", &optim_tail, py::arg("scale"), py::arg("growth_tracker"), py::arg("found_inf"),
+        py::arg("step"), py::arg("growth_factor"), py::arg("backoff_factor"), py::arg("growth_interval"));
+  m.def("pack_bf16", &pack_bf16);
+  m.def("unpack_bf16", &unpack_bf16);
+  m.def("accumulate_metrics", &accumulate_metrics, py::arg("logits"), py::arg("targets"), py::arg("loss"), py::arg("acc"));
+  m.def("augment", &augment, py::arg("data"), py::arg("idx"), py::arg("offs"), py::arg("flips"), py::arg("out"),
+        py::arg("nhwc"), py::arg("pad"), py::arg("mean"), py::arg("std"));
+  m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
+
+  py::class_<dpt::RcclComm, std::shared_ptr<dpt::RcclComm>>(m, "RcclComm")
+      .def(py::init<const std::string&, int, int, int>(), py::arg("unique_id"), py::arg("rank"),
+           py::arg("world_size"), py::arg("device"))
+      .def_static("new_unique_id", []() { return py::bytes(dpt::RcclComm::new_unique_id()); })
+      .def("all_reduce", [](dpt::RcclComm& c, Tensor t, bool on_current_stream) {
+             TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "all_reduce needs a contiguous GPU tensor");
+             dpt::WireType w;
+             switch (t.scalar_type()) {
+               case at::kFloat: w = dpt::WireType::kF32; break;
+               case at::kBFloat16: w = dpt::WireType::kBF16; break;
+               case at::kHalf: w = dpt::WireType::kF16; break;
+               case at::kLong: w = dpt::WireType::kI64; break;
+               default: TORCH_CHECK(false, "unsupported all_reduce dtype");
+             }
+             c10::hip::HIPGuard guard(t.device());
+             hipStream_t s = cur_stream(t);
+             c.all_reduce(t.data_ptr(), (size_t)t.numel(), w, on_current_stream ? s : c.stream());
+           }, py::arg("tensor"), py::arg("on_current_stream") = true)
+      .def("broadcast", [](dpt::RcclComm& c, Tensor t, int root) {
+             TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "broadcast needs a contiguous GPU tensor");
+             dpt::WireType w;
+             switch (t.scalar_type()) {
+               case at::kFloat: w = dpt::WireType::kF32; break;
+               case at::kBFloat16: w = dpt::WireType::kBF16; break;
+               case at::kHalf: w = dpt::WireType::kF16; break;
+               case at::kLong: w = dpt::WireType::kI64; break;
+               default: TORCH_CHECK(false, "unsupported broadcast dtype");
+             }
+             c10::hip::HIPGuard guard(t.device());
+             c.broadcast(t.data_ptr(), (size_t)t.numel(), w, root, cur_stream(t));
+           }, py::arg("tensor"), py::arg("root") = 0)
+      .def("abort", &dpt::RcclComm::abort)
+      .def_property_readonly("rank", &dpt::RcclComm::rank)
+      .def_property_readonly("world_size", &dpt::RcclComm::world_size)
+      .def_property_readonly("device", &dpt::RcclComm::device);
+
+  py::class_<dpt::Reducer, std::shared_ptr<dpt::Reducer>>(m, "Reducer")
+      .def(py::init<std::vector<Tensor>, std::vector<Tensor>, Tensor, std::vector<int64_t>, std::vector<int64_t>,
+                    std::vector<int64_t>, std::shared_ptr<dpt::RcclComm>, py::object, int, Tensor, Tensor, Tensor,
+                    double, bool, bool>(),
+           py::arg("params"), py::arg("grad_views"), py::arg("flat_grad"), py::arg("bucket_offsets"),
+           py::arg("bucket_numels"), py::arg("param_bucket"), py::arg("comm"), py::arg("py_allreduce"),
+           py::arg("wire"), py::arg("wire_buf"), py::arg("found_inf"), py::arg("scale"), py::arg("host_factor"),
+           py::arg("check_inf"), py::arg("profile"))
+      .def("prepare_for_backward", &dpt::Reducer::prepare_for_backward)
+      .def("mark_ready", &dpt::Reducer::mark_ready)
+      .def("finalize", &dpt::Reducer::finalize)
+      .def("set_require_sync", &dpt::Reducer::set_require_sync)
+      .def("set_check_inf", &dpt::Reducer::set_check_inf)
+      .def_property_readonly("require_sync", &dpt::Reducer::require_sync)
+      .def("ready_order", &dpt::Reducer::ready_order)
+      .def_property_readonly("num_buckets", &dpt::Reducer::num_buckets)
+      .def_property_readonly("backward_count", &dpt::Reducer::backward_count)
+      .def("bucket_times_ms", &dpt::Reducer::bucket_times_ms)
+      .def("step_times_ms", &dpt::Reducer::step_times_ms)
+      .def("remove_hooks", &dpt::Reducer::remove_hooks);
+}

@@ -1,0 +1,42 @@
+// Host-side launchers of the gfx950 kernel library.  Raw pointers + hipStream_t only: the
+// .hip translation units never include torch headers (bindings.cpp does the tensor checks).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dpt {
+
+struct AugNorm {
+  float mean[4];
+  float inv_std[4];
+};
+
+// optim_kernels.hip
+void launch_grad_check(const float* g, int64_t n, const float* scale, float host_factor,
+                       float* found_inf, hipStream_t s);
+void launch_sgd(float* p, float* g, float* buf, int64_t n, float lr, float momentum,
+                float dampening, float wd, bool nesterov, const float* scale, float host_factor,
+                const float* found_inf, const float* step, bool zero_grad, hipStream_t s);
+void launch_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                 float beta2, float eps, float wd, bool adamw, const float* scale, float host_factor,
+                 const float* found_inf, const float* step, bool zero_grad, hipStream_t s);
+void launch_optim_tail(float* scale, int* growth_tracker, float* found_inf, float* step,
+                       float growth_factor, float backoff_factor, int growth_interval,
+                       hipStream_t s);
+
+// comm_kernels.hip
+void launch_pack_bf16(const float* src, uint16_t* dst, int64_t n, hipStream_t s);
+void launch_unpack_bf16(const uint16_t* src, float* dst, int64_t n, const float* scale,
+                        float host_factor, float* found_inf, hipStream_t s);
+
+// metrics_kernels.hip  (dtype: 0 f32, 1 bf16, 2 f16)
+void launch_metrics(const void* logits, int dtype, int64_t rows, int64_t cols, int64_t ld,
+                    const int64_t* targets, const float* loss, double* acc, hipStream_t s);
+
+// augment_kernels.hip
+void launch_augment(const uint8_t* data, const int64_t* idx, const int32_t* offs,
+                    const uint8_t* flips, void* out, bool out_bf16, bool nhwc, int64_t B, int C,
+                    int H, int W, int pad, AugNorm norm, hipStream_t s);
+
+}  // namespace dpt

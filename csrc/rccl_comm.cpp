@@ -1,0 +1,86 @@
+#include "rccl_comm.h"
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace dpt {
+
+#define DPT_HIP_CHECK(expr)                                                                  \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess)                                                                    \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                   \
+  } while (0)
+
+#define DPT_RCCL_CHECK(expr)                                                                 \
+  do {                                                                                       \
+    ncclResult_t _r = (expr);                                                                \
+    if (_r != ncclSuccess)                                                                   \
+      throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(_r) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                   \
+  } while (0)
+
+static ncclDataType_t to_nccl(WireType t) {
+  switch (t) {
+    case WireType::kF32: return ncclFloat32;
+    case WireType::kBF16: return ncclBfloat16;
+    case WireType::kF16: return ncclFloat16;
+    case WireType::kI64: return ncclInt64;
+  }
+  return ncclFloat32;
+}
+
+std::string RcclComm::new_unique_id() {
+  ncclUniqueId id;
+  DPT_RCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+RcclComm::RcclComm(const std::string& unique_id, int rank, int world_size, int device)
+    : rank_(rank), world_size_(world_size), device_(device) {
+  if (unique_id.size() != sizeof(ncclUniqueId))
+    throw std::invalid_argument("RcclComm: unique id must be " + std::to_string(sizeof(ncclUniqueId)) + " bytes");
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id.data(), sizeof(id));
+  DPT_HIP_CHECK(hipSetDevice(device));
+  // Highest priority: bucket all-reduces should not queue behind backward kernels.
+  int lo = 0, hi = 0;
+  DPT_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  DPT_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
+  DPT_RCCL_CHECK(ncclCommInitRank(&comm_, world_size, id, rank));
+}
+
+RcclComm::~RcclComm() {
+  if (comm_ != nullptr && !aborted_) ncclCommDestroy(comm_);
+  if (stream_ != nullptr) hipStreamDestroy(stream_);
+}
+
+void RcclComm::all_reduce(void* ptr, size_t count, WireType t, hipStream_t stream) {
+  if (aborted_) throw std::runtime_error("RcclComm: communicator was aborted");
+  if (count == 0) return;
+  DPT_RCCL_CHECK(ncclAllReduce(ptr, ptr, count, to_nccl(t), ncclSum, comm_, stream ? stream : stream_));
+}
+
+void RcclComm::broadcast(void* ptr, size_t count, WireType t, int root, hipStream_t stream) {
+  if (aborted_) throw std::runtime_error("RcclComm: communicator was aborted");
+  if (count == 0) return;
+  DPT_RCCL_CHECK(ncclBroadcast(ptr, ptr, count, to_nccl(t), root, comm_, stream ? stream : stream_));
+}
+
+void RcclComm::abort() {
+  if (comm_ != nullptr && !aborted_) {
+    ncclCommAbort(comm_);
+    aborted_ = true;
+  }
+}
+
+const char* rccl_version_string() {
+  static std::string s;
+  int v = 0;
+  if (ncclGetVersion(&v) == ncclSuccess) s = std::to_string(v);
+  return s.c_str();
+}
+
+}  // namespace dpt

@@ -1,0 +1,249 @@
+#include "reducer.h"
+
+#include <c10/hip/HIPStream.h>
+#include <torch/csrc/autograd/engine.h>
+#include <torch/csrc/autograd/utils/lambda_post_hook.h>
+#include <torch/csrc/autograd/variable.h>
+
+#include <stdexcept>
+
+#include "kernels/kernels.h"
+
+namespace py = pybind11;
+
+namespace dpt {
+
+#define DPT_HIP_OK(expr)                                                                     \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess)                                                                    \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                   \
+  } while (0)
+
+Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_views,
+                 at::Tensor flat_grad, std::vector<int64_t> bucket_offsets,
+                 std::vector<int64_t> bucket_numels, std::vector<int64_t> param_bucket,
+                 std::shared_ptr<RcclComm> comm, py::object py_allreduce, int wire,
+                 at::Tensor wire_buf, at::Tensor found_inf, at::Tensor scale, double host_factor,
+                 bool check_inf, bool profile)
+    : params_(std::move(params)),
+      grad_views_(std::move(grad_views)),
+      flat_grad_(std::move(flat_grad)),
+      wire_buf_(std::move(wire_buf)),
+      found_inf_(std::move(found_inf)),
+      scale_(std::move(scale)),
+      bucket_offsets_(std::move(bucket_offsets)),
+      bucket_numels_(std::move(bucket_numels)),
+      param_bucket_(std::move(param_bucket)),
+      comm_(std::move(comm)),
+      py_allreduce_(std::move(py_allreduce)),
+      wire_(wire),
+      host_factor_((float)host_factor),
+      check_inf_(check_inf),
+      profile_(profile) {
+  const size_t P = params_.size(), B = bucket_offsets_.size();
+  if (grad_views_.size() != P || param_bucket_.size() != P || bucket_numels_.size() != B)
+    throw std::invalid_argument("Reducer: inconsistent parameter/bucket metadata");
+  gpu_ = flat_grad_.is_cuda();
+  if (gpu_ && !comm_) throw std::invalid_argument("Reducer: GPU arena needs an RcclComm");
+  if (!gpu_ && py_allreduce_.is_none())
+    throw std::invalid_argument("Reducer: CPU arena needs a Python all-reduce callback");
+  if (gpu_ && wire_ == 1 && (!wire_buf_.defined() || wire_buf_.numel() < flat_grad_.numel()))
+    throw std::invalid_argument("Reducer: bf16 wire needs a wire buffer as large as the arena");
+  for (size_t b = 0; b < B; ++b) {
+    if (bucket_offsets_[b] < 0 || bucket_offsets_[b] + bucket_numels_[b] > flat_grad_.numel())
+      throw std::invalid_argument("Reducer: bucket out of arena bounds");
+    if (gpu_ && (bucket_offsets_[b] % 8 != 0 || bucket_numels_[b] % 8 != 0))
+      throw std::invalid_argument("Reducer: GPU buckets must be 8-element aligned");
+  }
+  bucket_size_.assign(B, 0);
+  for (size_t i = 0; i < P; ++i) {
+    if (param_bucket_[i] < 0 || param_bucket_[i] >= (int64_t)B)
+      throw std::invalid_argument("Reducer: parameter mapped to a missing bucket");
+    bucket_size_[param_bucket_[i]]++;
+  }
+  pending_ = bucket_size_;
+  launched_.assign(B, 0);
+  marked_.assign(P, 0);
+
+  if (gpu_) {
+    const unsigned flags = profile_ ? hipEventDefault : hipEventDisableTiming;
+    ev_ready_.resize(B);
+    for (auto& e : ev_ready_) DPT_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (profile_) {
+      ev_start_.resize(B);
+      ev_end_.resize(B);
+      for (auto& e : ev_start_) DPT_HIP_OK(hipEventCreateWithFlags(&e, flags));
+      for (auto& e : ev_end_) DPT_HIP_OK(hipEventCreateWithFlags(&e, flags));
+    }
+    DPT_HIP_OK(hipEventCreateWithFlags(&ev_bwd_end_, flags));
+    DPT_HIP_OK(hipEventCreateWithFlags(&ev_done_, flags));
+    DPT_HIP_OK(hipEventCreateWithFlags(&ev_first_, flags));
+  }
+
+  // One post-hook per parameter on its AccumulateGrad node: fires after the gradient has
+  // been accumulated into the arena view.
+  for (size_t i = 0; i < P; ++i) {
+    auto acc = torch::autograd::impl::grad_accumulator(params_[i]);
+    if (!acc) throw std::invalid_argument("Reducer: parameter without a gradient accumulator");
+    const int64_t idx = (int64_t)i;
+    auto key = acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
+        [this, idx](const torch::autograd::variable_list& outputs,
+                    const torch::autograd::variable_list& /*inputs*/) {
+          this->mark_ready(idx);
+          return outputs;
+        }));
+    accumulators_.push_back(std::move(acc));
+    hook_keys_.push_back(key);
+  }
+}
+
+void Reducer::remove_hooks() {
+  for (size_t i = 0; i < accumulators_.size(); ++i) accumulators_[i]->del_post_hook(hook_keys_[i]);
+  accumulators_.clear();
+  hook_keys_.clear();
+}
+
+Reducer::~Reducer() {
+  remove_hooks();
+  if (gpu_) {
+    for (auto e : ev_ready_) hipEventDestroy(e);
+    for (auto e : ev_start_) hipEventDestroy(e);
+    for (auto e : ev_end_) hipEventDestroy(e);
+    if (ev_bwd_end_) hipEventDestroy(ev_bwd_end_);
+    if (ev_done_) hipEventDestroy(ev_done_);
+    if (ev_first_) hipEventDestroy(ev_first_);
+  }
+  if (!py_allreduce_.is_none()) {
+    py::gil_scoped_acquire g;
+    py_allreduce_ = py::none();
+  }
+}
+
+void Reducer::prepare_for_backward() {
+  std::lock_guard<std::mutex> lk(mu_);
+  pending_ = bucket_size_;
+  std::fill(launched_.begin(), launched_.end(), 0);
+  std::fill(marked_.begin(), marked_.end(), 0);
+  next_launch_ = 0;
+  callback_queued_ = false;
+  if (record_order_) ready_order_.clear();
+  if (gpu_) caller_stream_ = c10::hip::getCurrentHIPStream(flat_grad_.device().index()).stream();
+  // Re-attach arena views if someone replaced or cleared .grad (e.g. zero_grad(set_to_none)).
+  for (size_t i = 0; i < params_.size(); ++i) {
+    const at::Tensor& g = params_[i].grad();
+    if (!g.defined() || g.data_ptr() != grad_views_[i].data_ptr()) {
+      if (g.defined()) grad_views_[i].copy_(g);
+      else grad_views_[i].zero_();
+      params_[i].mutable_grad() = grad_views_[i];
+    }
+  }
+}
+
+void Reducer::mark_ready(int64_t index) {
+  if (!require_sync_) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  if (marked_[index]) return;  // second accumulation in one backward: already counted
+  marked_[index] = 1;
+  if (record_order_) ready_order_.push_back(index);
+  if (!callback_queued_) {
+    callback_queued_ = true;
+    if (gpu_ && profile_) DPT_HIP_OK(hipEventRecord(ev_first_, caller_stream_));
+    torch::autograd::Engine::get_default_engine().queue_callback([this] { this->finalize(); });
+  }
+  const int64_t b = param_bucket_[index];
+  if (--pending_[b] == 0) {
+    if (gpu_) {
+      // The gradient was produced on this thread's current stream.
+      hipStream_t producer = c10::hip::getCurrentHIPStream(flat_grad_.device().index()).stream();
+      DPT_HIP_OK(hipEventRecord(ev_ready_[b], producer));
+    }
+    launched_[b] = 1;  // "ready"; the launch itself happens in index order below
+    while (next_launch_ < (int64_t)launched_.size() && launched_[next_launch_] == 1) {
+      launch_bucket(next_launch_);
+      launched_[next_launch_] = 2;
+      ++next_launch_;
+    }
+  }
+}
+
+void Reducer::launch_bucket(int64_t b) {
+  const int64_t off = bucket_offsets_[b], n = bucket_numels_[b];
+  if (!gpu_) {
+    py::gil_scoped_acquire g;
+    py_allreduce_(b, off, n);
+    return;
+  }
+  hipStream_t cs = comm_->stream();
+  DPT_HIP_OK(hipStreamWaitEvent(cs, ev_ready_[b], 0));
+  if (profile_) DPT_HIP_OK(hipEventRecord(ev_start_[b], cs));
+  float* g = flat_grad_.data_ptr<float>() + off;
+  const float* scale = (scale_.defined() && scale_.numel() > 0) ? scale_.data_ptr<float>() : nullptr;
+  float* finf = check_inf_ ? found_inf_.data_ptr<float>() : nullptr;
+  if (comm_->world_size() > 1) {
+    if (wire_ == 1) {
+      uint16_t* w = reinterpret_cast<uint16_t*>(wire_buf_.data_ptr()) + off;
+      launch_pack_bf16(g, w, n, cs);
+      comm_->all_reduce(w, (size_t)n, WireType::kBF16, cs);
+      launch_unpack_bf16(w, g, n, scale, host_factor_, finf, cs);
+    } else {
+      comm_->all_reduce(g, (size_t)n, WireType::kF32, cs);
+      if (finf) launch_grad_check(g, n, scale, host_factor_, finf, cs);
+    }
+  } else if (finf) {
+    launch_grad_check(g, n, scale, host_factor_, finf, cs);
+  }
+  if (profile_) DPT_HIP_OK(hipEventRecord(ev_end_[b], cs));
+}
+
+void Reducer::finalize() {
+  std::lock_guard<std::mutex> lk(mu_);
+  // Buckets whose parameters received no gradient this backward (unused parameters) are
+  // still reduced, in order, so every rank issues the same collective sequence.
+  if (gpu_) {
+    hipStream_t producer = c10::hip::getCurrentHIPStream(flat_grad_.device().index()).stream();
+    for (size_t b = 0; b < launched_.size(); ++b)
+      if (launched_[b] == 0) DPT_HIP_OK(hipEventRecord(ev_ready_[b], producer));
+    if (profile_) DPT_HIP_OK(hipEventRecord(ev_bwd_end_, caller_stream_));
+  }
+  for (size_t b = 0; b < launched_.size(); ++b) {
+    if (launched_[b] != 2) {
+      launch_bucket((int64_t)b);
+      launched_[b] = 2;
+    }
+  }
+  next_launch_ = (int64_t)launched_.size();
+  if (gpu_) {
+    DPT_HIP_OK(hipEventRecord(ev_done_, comm_->stream()));
+    DPT_HIP_OK(hipStreamWaitEvent(caller_stream_, ev_done_, 0));
+  }
+  if (record_order_ && !ready_order_.empty()) record_order_ = false;
+  ++backward_count_;
+}
+
+std::vector<double> Reducer::bucket_times_ms() {
+  std::vector<double> out;
+  if (!gpu_ || !profile_) return out;
+  for (size_t b = 0; b < ev_start_.size(); ++b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ev_start_[b], ev_end_[b]) != hipSuccess) ms = -1.f;
+    out.push_back(ms);
+  }
+  return out;
+}
+
+std::vector<double> Reducer::step_times_ms() {
+  // {first-grad-ready -> backward end, backward end -> comm done (exposed), first bucket
+  //  start -> comm done (comm span)}
+  std::vector<double> out;
+  if (!gpu_ || !profile_ || ev_start_.empty()) return out;
+  float a = 0.f, b = 0.f, c = 0.f;
+  hipEventElapsedTime(&a, ev_first_, ev_bwd_end_);
+  hipEventElapsedTime(&b, ev_bwd_end_, ev_done_);
+  hipEventElapsedTime(&c, ev_start_[0], ev_done_);
+  out = {a, b, c};
+  return out;
+}
+
+}  // namespace dpt

@@ -1,0 +1,122 @@
+"""Command-line contract.
+
+The first eleven flags reproduce the reference's CLI exactly: names, types, defaults and
+help strings (reference ``train_ddp.py:19-46``).  Everything after them is
+additive, and every additive default reproduces the reference's behaviour
+(resnet18 / CIFAR-10 / fp16 autocast / SGD / 25 MiB buckets / BN-buffer broadcast), except
+``--impl``: the default ``native`` engine keeps the same semantics but runs the MI355X hot
+path (HIP fused optimizer + device-resident scaler + RCCL reducer).
+"""
+from __future__ import annotations
+
+import argparse
+from typing import Optional, Sequence
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="DDP training of ResNet-18 on CIFAR-10")
+
+    # ---- reference flags (train_ddp.py:22-43) -------------------------------------------
+    p.add_argument("--data-dir", default="./data", type=str,
+                   help="directory to store CIFAR-10")
+    p.add_argument("--epochs", default=10, type=int,
+                   help="number of total epochs to run")
+    p.add_argument("--batch-size", default=128, type=int,
+                   help="mini-batch size *per GPU*")
+    p.add_argument("--workers", default=4, type=int,
+                   help="number of data loading workers per process")
+    p.add_argument("--lr", default=0.1, type=float,
+                   help="initial learning rate")
+    p.add_argument("--momentum", default=0.9, type=float,
+                   help="SGD momentum")
+    p.add_argument("--weight-decay", default=5e-4, type=float,
+                   help="weight decay")
+    p.add_argument("--amp", action="store_true",
+                   help="use automatic mixed precision (AMP)")
+    p.add_argument("--print-freq", default=50, type=int,
+                   help="print frequency (in steps)")
+    p.add_argument("--output-dir", default="./experiments", type=str,
+                   help="directory to save logs")
+    p.add_argument("--seed", default=42, type=int,
+                   help="random seed")
+
+    # ---- additive flags ---------------------------------------------------
+    g = p.add_argument_group("MI355X extensions (defaults reproduce the reference)")
+    g.add_argument("--model", default="resnet18",
+                   choices=["resnet18", "resnet34", "resnet50", "resnet101", "vit_b_16"],
+                   help="model architecture")
+    g.add_argument("--dataset", default="cifar10", choices=["cifar10", "synthetic"],
+                   help="cifar10 reads local CIFAR-10 files; synthetic generates on-device data")
+    g.add_argument("--image-size", default=None, type=int,
+                   help="input resolution (default 32 for cifar10, 224 for synthetic)")
+    g.add_argument("--num-classes", default=None, type=int,
+                   help="number of classes (default 10 for cifar10, 1000 for synthetic)")
+    g.add_argument("--synthetic-train-size", default=50000, type=int,
+                   help="samples per epoch for --dataset synthetic")
+    g.add_argument("--synthetic-val-size", default=10000, type=int,
+                   help="validation samples for --dataset synthetic")
+    g.add_argument("--amp-dtype", default="fp16", choices=["fp16", "bf16"],
+                   help="autocast dtype when --amp is set (reference: fp16)")
+    g.add_argument("--optimizer", default="sgd", choices=["sgd", "adam", "adamw"],
+                   help="optimizer (reference: sgd)")
+    g.add_argument("--nesterov", action="store_true", help="Nesterov momentum (SGD)")
+    g.add_argument("--betas", default="0.9,0.999", type=str, help="Adam betas")
+    g.add_argument("--eps", default=1e-8, type=float, help="Adam epsilon")
+    g.add_argument("--impl", default="native", choices=["native", "torch"],
+                   help="native: MI355X engine (HIP kernels, RCCL reducer); torch: stock DDP/foreach SGD/GradScaler")
+    g.add_argument("--backend", default="auto", choices=["auto", "rccl", "nccl", "gloo"],
+                   help="process-group backend (auto: rccl on GPUs, gloo on CPU)")
+    g.add_argument("--bucket-cap-mb", default=25.0, type=float,
+                   help="gradient bucket size cap in MiB")
+    g.add_argument("--first-bucket-mb", default=1.0, type=float,
+                   help="first (last-layer) bucket cap in MiB")
+    g.add_argument("--no-broadcast-buffers", dest="broadcast_buffers", action="store_false",
+                   help="do not broadcast BN buffers from rank 0 before each forward")
+    g.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
+                   help="all-reduce wire dtype (bf16 = gradient compression, native only)")
+    g.add_argument("--channels-last", action="store_true",
+                   help="NHWC activations/weights (MIOpen's fast layout on gfx950)")
+    g.add_argument("--max-steps", default=0, type=int,
+                   help="stop each epoch after this many steps (0 = full epoch)")
+    g.add_argument("--warmup-steps", default=0, type=int,
+                   help="untimed steps excluded from the throughput window at the first epoch")
+    g.add_argument("--profile-sync", action="store_true",
+                   help="hipEvent timeline: per-step forward/backward/all-reduce/optimizer times")
+    g.add_argument("--profile-out", default=None, type=str,
+                   help="JSON file for the --profile-sync report (default output-dir/sync_profile.json)")
+    g.add_argument("--roctx", action="store_true", help="emit roctx ranges for rocprofv3 --marker-trace")
+    g.add_argument("--grad-accum", default=1, type=int,
+                   help="micro-batches per optimizer step (all-reduce only on the last)")
+    g.add_argument("--save-every", default=0, type=int,
+                   help="write a checkpoint every N epochs (0 = never, the reference default)")
+    g.add_argument("--resume", default=None, type=str, help="checkpoint file to resume from")
+    g.add_argument("--no-val", dest="validate", action="store_false", help="skip validation")
+    g.add_argument("--dist-timeout", default=1800, type=int,
+                   help="process-group timeout in seconds")
+    g.add_argument("--check-consistency", default=0, type=int,
+                   help="debug: every N steps verify parameters are identical across ranks")
+    g.add_argument("--cuda-graph", action="store_true",
+                   help="capture the training step in a hipGraph (static shapes, native impl)")
+    return p
+
+
+def parse_args(argv: Optional[Sequence[str]] = None) -> argparse.Namespace:
+    args = build_parser().parse_args(argv)
+    return finalize(args)
+
+
+def finalize(args: argparse.Namespace) -> argparse.Namespace:
+    """Fill the data-dependent defaults."""
+    if args.image_size is None:
+        args.image_size = 32 if args.dataset == "cifar10" else 224
+    if args.num_classes is None:
+        args.num_classes = 10 if args.dataset == "cifar10" else 1000
+    if args.backend == "nccl":
+        args.backend = "rccl"
+    b = [float(v) for v in str(args.betas).split(",")]
+    if len(b) != 2:
+        raise ValueError("--betas expects two comma-separated floats")
+    args.betas = tuple(b)
+    if args.grad_accum < 1:
+        raise ValueError("--grad-accum must be >= 1")
+    return args

@@ -1,0 +1,272 @@
+"""Training / validation engine.
+
+Output contract (byte-identical to the reference):
+* step line every ``print_freq`` steps on rank 0 (reference train_ddp.py:228-244);
+* epoch train metrics = SUM-all-reduced (loss*bs, correct, total) (reference :247-263);
+* validation over the full, unsharded split on every rank (reference :266-300).
+
+Two engines share that contract:
+* ``impl="torch"`` - the reference's exact mechanics on PyTorch-ROCm: torch DDP with
+  defaults, ``torch.amp.GradScaler``, foreach SGD/Adam, two ``.item()`` host syncs per
+  step.  This is the stock baseline the native engine is measured against.
+* ``impl="native"`` - the MI355X path: ``NativeDDP`` (flat arenas + C++ reducer over RCCL),
+  ``DeviceGradScaler``, one fused HIP optimizer launch, device-side metric accumulation;
+  zero host synchronisations per step.  The host syncs at print boundaries only, so the
+  throughput window is timed from sync to sync (the reference's window times each step
+  after the loader yields; with on-device loaders the loader wait is a kernel launch).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .. import ops
+from ..amp import DeviceGradScaler, autocast
+from ..profiling.timeline import StepTimeline
+
+
+def format_step_line(epoch: int, i: int, n: int, avg_loss: float, avg_acc: float, thr: float) -> str:
+    return (f"Epoch [{epoch+1}] Step [{i+1}/{n}] "
+            f"Loss: {avg_loss:.4f}  "
+            f"Acc: {avg_acc:.2f}%  "
+            f"Throughput: {thr:.2f} samples/s (global)")
+
+
+def format_epoch_line(epoch: int, epochs: int, tl: float, ta: float, vl: float, va: float, et: float) -> str:
+    return (f"[Epoch {epoch+1}/{epochs}] "
+            f"Train: loss={tl:.4f}, acc={ta:.2f}% | "
+            f"Val: loss={vl:.4f}, acc={va:.2f}% | "
+            f"Epoch time: {et:.2f}s")
+
+
+@dataclass
+class EpochStats:
+    loss: Optional[float]
+    acc: Optional[float]
+    epoch_time: float
+    steps: int = 0
+    samples: int = 0
+    windows: List[Dict[str, float]] = field(default_factory=list)
+
+
+def _sync(device: torch.device) -> None:
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+class Trainer:
+    """Owns model/optimizer/scaler wiring for one of the two engines."""
+
+    def __init__(self, model: nn.Module, args, rank: int, world_size: int, device: torch.device,
+                 comm=None, log: Callable[[str], None] = print) -> None:
+        self.args, self.rank, self.world_size, self.device = args, rank, world_size, device
+        self.impl = args.impl
+        self.log = log
+        self.amp = bool(args.amp)
+        self.amp_dtype = getattr(args, "amp_dtype", "fp16")
+        self.criterion = nn.CrossEntropyLoss().to(device)
+        self.timeline = StepTimeline(device, enabled=getattr(args, "profile_sync", False))
+        self.global_step = 0
+        self.grad_accum = max(1, getattr(args, "grad_accum", 1))
+        if self.impl == "native":
+            self._init_native(model, comm)
+        else:
+            self._init_torch(model)
+
+    # ------------------------------------------------------------------ construction
+    def _init_native(self, model: nn.Module, comm) -> None:
+        from ..optim import build_optimizer
+        from ..parallel.ddp import NativeDDP
+
+        args = self.args
+        params_in_order = [p for p in model.parameters() if p.requires_grad]
+        self.scaler = DeviceGradScaler(self.device, enabled=self.amp)
+        self.ddp = NativeDDP(model, rank=self.rank, world_size=self.world_size, device=self.device,
+                             bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb,
+                             broadcast_buffers=args.broadcast_buffers, grad_dtype=args.grad_dtype,
+                             found_inf=self.scaler.found_inf, scale=self.scaler.scale_tensor,
+                             check_inf=self.amp, profile=self.timeline.enabled, comm=comm)
+        self.model = self.ddp
+        self.module = model
+        self.optimizer = build_optimizer(args.optimizer, self.ddp.arena, args, params_in_order)
+        self.metrics = torch.zeros(3, dtype=torch.float64, device=self.device)
+
+    def _init_torch(self, model: nn.Module) -> None:
+        args = self.args
+        self.module = model
+        if self.world_size > 1:
+            kw = dict(device_ids=[self.device.index], output_device=self.device.index) \
+                if self.device.type == "cuda" else {}
+            self.model = nn.parallel.DistributedDataParallel(
+                model, find_unused_parameters=False, bucket_cap_mb=args.bucket_cap_mb,
+                broadcast_buffers=args.broadcast_buffers, **kw)
+        else:
+            self.model = model
+        params = model.parameters()
+        if args.optimizer == "sgd":
+            self.optimizer = torch.optim.SGD(params, lr=args.lr, momentum=args.momentum,
+                                             weight_decay=args.weight_decay,
+                                             nesterov=getattr(args, "nesterov", False))
+        elif args.optimizer == "adam":
+            self.optimizer = torch.optim.Adam(params, lr=args.lr, betas=args.betas, eps=args.eps,
+                                              weight_decay=args.weight_decay)
+        else:
+            self.optimizer = torch.optim.AdamW(params, lr=args.lr, betas=args.betas, eps=args.eps,
+                                               weight_decay=args.weight_decay)
+        self.scaler = torch.amp.GradScaler(self.device.type, enabled=self.amp and self.device.type == "cuda")
+        self.ddp = None
+
+    # ------------------------------------------------------------------ one step
+    def train_step(self, images: torch.Tensor, targets: torch.Tensor):
+        """Forward + backward + optimizer for one batch; returns (outputs, loss)."""
+        if self.impl == "native":
+            return self._native_step(images, targets)
+        return self._torch_step(images, targets)
+
+    def _native_step(self, images, targets):
+        tl = self.timeline
+        tl.mark("start")
+        with autocast(self.device, self.amp, self.amp_dtype):
+            outputs = self.model(images)
+            loss = self.criterion(outputs, targets)
+        tl.mark("fwd")
+        (self.scaler.scale(loss) if self.amp else loss).backward()
+        tl.mark("bwd")
+        if self.ddp.maybe_rebuild_buckets(self.optimizer) and self.rank == 0 and getattr(self.args, "verbose", False):
+            self.log(f"rebuilt buckets: {self.ddp.bucket_sizes_mib()}")
+        self.optimizer.step(self.scaler if self.amp else None, host_factor=self.ddp.grad_factor,
+                            grads_checked=self.ddp.grads_checked)
+        tl.mark("opt")
+        ops.accumulate_metrics(outputs, targets, loss, self.metrics)
+        tl.end_step(self.ddp.comm_profile() if tl.enabled else None)
+        self.global_step += 1
+        return outputs, loss
+
+    def _torch_step(self, images, targets):
+        self.optimizer.zero_grad(set_to_none=True)
+        if self.amp and self.scaler.is_enabled():
+            with autocast(self.device, True, self.amp_dtype):
+                outputs = self.model(images)
+                loss = self.criterion(outputs, targets)
+            self.scaler.scale(loss).backward()
+            self.scaler.step(self.optimizer)
+            self.scaler.update()
+        else:
+            with autocast(self.device, self.amp, self.amp_dtype):
+                outputs = self.model(images)
+                loss = self.criterion(outputs, targets)
+            loss.backward()
+            self.optimizer.step()
+        self.global_step += 1
+        return outputs, loss
+
+    # ------------------------------------------------------------------ epochs
+    def train_one_epoch(self, epoch: int, loader, train_sampler=None) -> EpochStats:
+        args, rank, ws = self.args, self.rank, self.world_size
+        self.model.train()
+        if train_sampler is not None:
+            train_sampler.set_epoch(epoch)
+        if hasattr(loader, "set_epoch") and train_sampler is None:
+            loader.set_epoch(epoch)
+        n = len(loader)
+        native = self.impl == "native"
+        if native:
+            self.metrics.zero_()
+        epoch_loss, epoch_correct, epoch_total = 0.0, 0, 0
+        windows = []
+        _sync(self.device)
+        start_epoch = time.time()
+        accum_time, accum_samples = 0.0, 0
+        win_start = time.time()
+        steps = 0
+        for i, (images, targets) in enumerate(loader):
+            if native:
+                self.train_step(images, targets)
+                bs = images.size(0)
+                accum_samples += bs * ws
+                steps += 1
+                if rank == 0 and (i + 1) % args.print_freq == 0:
+                    _sync(self.device)
+                    now = time.time()
+                    accum_time = now - win_start
+                    m = self.metrics.tolist()
+                    avg_loss = m[0] / m[2]
+                    avg_acc = 100.0 * m[1] / m[2]
+                    thr = accum_samples / accum_time if accum_time > 0 else 0.0
+                    self.log(format_step_line(epoch, i, n, avg_loss, avg_acc, thr))
+                    windows.append({"step": i + 1, "seconds": accum_time, "samples": accum_samples,
+                                    "throughput": thr})
+                    accum_samples = 0
+                    win_start = time.time()
+            else:
+                batch_start = time.time()
+                outputs, loss = self.train_step(images, targets)
+                bs = images.size(0)
+                epoch_loss += loss.item() * bs
+                _, preds = outputs.max(1)
+                epoch_correct += preds.eq(targets).sum().item()
+                epoch_total += bs
+                accum_time += time.time() - batch_start
+                accum_samples += bs * ws
+                steps += 1
+                if rank == 0 and (i + 1) % args.print_freq == 0:
+                    thr = accum_samples / accum_time if accum_time > 0 else 0.0
+                    self.log(format_step_line(epoch, i, n, epoch_loss / epoch_total,
+                                              100.0 * epoch_correct / epoch_total, thr))
+                    windows.append({"step": i + 1, "seconds": accum_time, "samples": accum_samples,
+                                    "throughput": thr})
+                    accum_time, accum_samples = 0.0, 0
+        # ---- epoch reduction (one float64[3] all-reduce instead of three scalars)
+        if native:
+            tot = self.metrics.clone()
+        else:
+            tot = torch.tensor([epoch_loss, float(epoch_correct), float(epoch_total)],
+                               dtype=torch.float64, device=self.device)
+        if ws > 1:
+            dist.all_reduce(tot)
+        _sync(self.device)
+        epoch_time = time.time() - start_epoch
+        t = tot.tolist()
+        samples = int(t[2])
+        if rank == 0 and t[2] > 0:
+            return EpochStats(t[0] / t[2], 100.0 * t[1] / t[2], epoch_time, steps, samples, windows)
+        return EpochStats(None, None, epoch_time, steps, samples, windows)
+
+    @torch.no_grad()
+    def validate(self, loader) -> EpochStats:
+        self.model.eval()
+        acc = torch.zeros(3, dtype=torch.float64, device=self.device)
+        t0 = time.time()
+        for images, targets in loader:
+            with autocast(self.device, self.amp, self.amp_dtype):
+                outputs = self.model(images)
+                loss = self.criterion(outputs, targets)
+            if self.impl == "native":
+                ops.accumulate_metrics(outputs, targets, loss, acc)
+            else:
+                bs = images.size(0)
+                acc[0] += loss.item() * bs
+                _, preds = outputs.max(1)
+                acc[1] += preds.eq(targets).sum().item()
+                acc[2] += bs
+        if self.world_size > 1:
+            dist.all_reduce(acc)
+        t = acc.tolist()
+        if self.rank == 0 and t[2] > 0:
+            return EpochStats(t[0] / t[2], 100.0 * t[1] / t[2], time.time() - t0)
+        return EpochStats(None, None, time.time() - t0)
+
+    # ------------------------------------------------------------------ checkpoint glue
+    def model_state(self):
+        return self.module.state_dict()
+
+    def optimizer_state(self):
+        return self.optimizer.state_dict()
+
+    def scaler_state(self):
+        return self.scaler.state_dict()

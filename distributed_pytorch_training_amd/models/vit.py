@@ -1,0 +1,116 @@
+"""ViT-B/16 with torchvision-identical parameter names, shapes and init (86,567,656 params).
+
+BASELINE.json config 5 trains ViT-B/16 under DDP to stress large-parameter bucket sizing
+(330 MiB of fp32 gradients).  The reference itself only trains ResNet-18
+(reference ``train_ddp.py:154``); this module is the model-zoo extension the baseline names.
+
+MI355X notes
+------------
+* Self-attention uses ``F.scaled_dot_product_attention`` (PyTorch-ROCm dispatches it to its
+  fused CK/aotriton flash kernels on gfx950) instead of ``nn.MultiheadAttention``'s unfused
+  training path.  The parameters keep ``nn.MultiheadAttention``'s names (``in_proj_weight``,
+  ``in_proj_bias``, ``out_proj.*``) so state dicts load into torchvision unchanged.
+* 197 tokens (14x14 patches + CLS): no sequence sharding is needed.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class SelfAttention(nn.Module):
+    def __init__(self, dim: int, heads: int, dropout: float = 0.0) -> None:
+        super().__init__()
+        self.dim, self.heads, self.dropout = dim, heads, dropout
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * dim, dim))
+        self.in_proj_bias = nn.Parameter(torch.zeros(3 * dim))
+        self.out_proj = nn.Linear(dim, dim)
+        # nn.MultiheadAttention._reset_parameters
+        nn.init.xavier_uniform_(self.in_proj_weight)
+        nn.init.zeros_(self.out_proj.bias)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        b, s, d = x.shape
+        qkv = F.linear(x, self.in_proj_weight, self.in_proj_bias)
+        qkv = qkv.view(b, s, 3, self.heads, d // self.heads).permute(2, 0, 3, 1, 4)
+        y = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2],
+                                           dropout_p=self.dropout if self.training else 0.0)
+        return self.out_proj(y.transpose(1, 2).reshape(b, s, d))
+
+
+class MLPBlock(nn.Sequential):
+    """Linear(0) - GELU(1) - Dropout(2) - Linear(3) - Dropout(4), torchvision key layout."""
+
+    def __init__(self, dim: int, mlp_dim: int, dropout: float) -> None:
+        super().__init__(nn.Linear(dim, mlp_dim), nn.GELU(), nn.Dropout(dropout),
+                         nn.Linear(mlp_dim, dim), nn.Dropout(dropout))
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.xavier_uniform_(m.weight)
+                nn.init.normal_(m.bias, std=1e-6)
+
+
+class EncoderBlock(nn.Module):
+    def __init__(self, heads: int, dim: int, mlp_dim: int, dropout: float, attn_dropout: float) -> None:
+        super().__init__()
+        self.ln_1 = nn.LayerNorm(dim, eps=1e-6)
+        self.self_attention = SelfAttention(dim, heads, attn_dropout)
+        self.dropout = nn.Dropout(dropout)
+        self.ln_2 = nn.LayerNorm(dim, eps=1e-6)
+        self.mlp = MLPBlock(dim, mlp_dim, dropout)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = x + self.dropout(self.self_attention(self.ln_1(x)))
+        return x + self.mlp(self.ln_2(x))
+
+
+class Encoder(nn.Module):
+    def __init__(self, seq_len: int, layers: int, heads: int, dim: int, mlp_dim: int,
+                 dropout: float, attn_dropout: float) -> None:
+        super().__init__()
+        self.pos_embedding = nn.Parameter(torch.empty(1, seq_len, dim).normal_(std=0.02))
+        self.dropout = nn.Dropout(dropout)
+        self.layers = nn.Sequential(OrderedDict(
+            (f"encoder_layer_{i}", EncoderBlock(heads, dim, mlp_dim, dropout, attn_dropout))
+            for i in range(layers)))
+        self.ln = nn.LayerNorm(dim, eps=1e-6)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.ln(self.layers(self.dropout(x + self.pos_embedding)))
+
+
+class VisionTransformer(nn.Module):
+    def __init__(self, image_size: int = 224, patch_size: int = 16, layers: int = 12,
+                 heads: int = 12, dim: int = 768, mlp_dim: int = 3072, num_classes: int = 1000,
+                 dropout: float = 0.0, attn_dropout: float = 0.0) -> None:
+        super().__init__()
+        if image_size % patch_size:
+            raise ValueError(f"image_size {image_size} not divisible by patch_size {patch_size}")
+        self.image_size, self.patch_size, self.dim = image_size, patch_size, dim
+        self.conv_proj = nn.Conv2d(3, dim, kernel_size=patch_size, stride=patch_size)
+        seq_len = (image_size // patch_size) ** 2 + 1
+        self.class_token = nn.Parameter(torch.zeros(1, 1, dim))
+        self.encoder = Encoder(seq_len, layers, heads, dim, mlp_dim, dropout, attn_dropout)
+        self.heads = nn.Sequential(OrderedDict(head=nn.Linear(dim, num_classes)))
+
+        fan_in = 3 * patch_size * patch_size
+        nn.init.trunc_normal_(self.conv_proj.weight, std=math.sqrt(1 / fan_in))
+        nn.init.zeros_(self.conv_proj.bias)
+        nn.init.zeros_(self.heads.head.weight)
+        nn.init.zeros_(self.heads.head.bias)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        n = x.shape[0]
+        x = self.conv_proj(x).flatten(2).transpose(1, 2)          # [N, 196, 768]
+        x = torch.cat([self.class_token.expand(n, -1, -1), x], dim=1)
+        x = self.encoder(x)
+        return self.heads(x[:, 0])
+
+
+def vit_b_16(num_classes: int = 1000, image_size: int = 224, **kw) -> VisionTransformer:
+    return VisionTransformer(image_size=image_size, patch_size=16, layers=12, heads=12,
+                             dim=768, mlp_dim=3072, num_classes=num_classes, **kw)

@@ -1,0 +1,70 @@
+"""Gradient bucket planning.
+
+Same policy as the reference's inherited DDP reducer:
+walk the parameters in gradient-ready order (reverse definition order before the first
+backward, the observed order after it), close a bucket once its byte size reaches the
+current cap, and use a small first cap (1 MiB) so the first all-reduce starts early in
+backward, then the regular cap (25 MiB).  ``assign_buckets`` reproduces
+``torch.distributed._compute_bucket_assignment_by_size`` for one dtype (tested).
+
+Bucket caps are a first-class tuning knob on MI355X: an all-reduce over 8 GPUs on 7
+point-to-point xGMI links wants per-channel chunks past the latency knee, so the bench
+sweeps caps rather than assuming NVSwitch-era defaults.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Sequence
+
+MiB = 1024 * 1024
+
+
+def assign_buckets(sizes_bytes: Sequence[int], caps_bytes: Sequence[int]) -> List[List[int]]:
+    """Indices of ``sizes_bytes`` grouped into buckets (input order preserved)."""
+    buckets: List[List[int]] = []
+    cur: List[int] = []
+    cur_size = 0
+    cap_i = 0
+    for i, s in enumerate(sizes_bytes):
+        cur.append(i)
+        cur_size += s
+        if cur_size >= caps_bytes[cap_i]:
+            buckets.append(cur)
+            cur, cur_size = [], 0
+            cap_i = min(cap_i + 1, len(caps_bytes) - 1)
+    if cur:
+        buckets.append(cur)
+    return buckets
+
+
+@dataclass
+class BucketPlan:
+    offsets: List[int]        # element offset of each bucket in the arena
+    numels: List[int]         # elements per bucket (contiguous, includes alignment padding)
+    param_bucket: List[int]   # bucket index of each arena parameter
+    members: List[List[int]]  # arena parameter indices per bucket
+
+    @property
+    def num_buckets(self) -> int:
+        return len(self.offsets)
+
+    def sizes_mib(self, elem_bytes: int = 4) -> List[float]:
+        return [n * elem_bytes / MiB for n in self.numels]
+
+
+def plan_for_arena(arena, bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0) -> BucketPlan:
+    """Partition ``arena`` (already laid out in ready order) into contiguous buckets."""
+    elem = arena.param_flat.element_size()
+    sizes = [p.numel() * elem for p in arena.params]
+    caps = [max(1, int(first_bucket_mb * MiB)), max(1, int(bucket_cap_mb * MiB))]
+    groups = assign_buckets(sizes, caps)
+    offsets, numels, param_bucket = [], [], [0] * len(arena.params)
+    for b, members in enumerate(groups):
+        start = arena.offsets[members[0]]
+        for i in members:
+            param_bucket[i] = b
+        offsets.append(start)
+    for b in range(len(groups)):
+        end = offsets[b + 1] if b + 1 < len(groups) else arena.numel
+        numels.append(end - offsets[b])
+    return BucketPlan(offsets, numels, param_bucket, groups)

@@ -1,0 +1,206 @@
+"""Native data-parallel front-end (the MI355X replacement for torch DDP).
+
+Behavioural parity with what the reference gets from ``DistributedDataParallel(model,
+device_ids=[local_rank], output_device=local_rank, find_unused_parameters=False)``
+(reference train_ddp.py:303-311):
+
+* construction: parameter-shape verification across ranks (row A2), rank-0 broadcast of
+  parameters and buffers (row A3) - here ONE collective per arena instead of 250 MiB
+  coalesced chunks of per-tensor copies;
+* every forward whose predecessor ran with grad enabled first broadcasts rank 0's module
+  buffers (BN running stats, row B, ``broadcast_buffers=True``) - one collective per dtype
+  through the flat ``BufferArena``;
+* backward: gradients are averaged over ranks by bucketed all-reduce overlapped with the
+  backward pass (row C), driven by the C++ ``Reducer`` over the framework's RCCL
+  communicator; buckets are rebuilt once in the observed gradient-ready order;
+* ``no_sync()`` for gradient accumulation.
+
+Differences by design: averaging (÷world_size) and AMP unscale are applied by the fused
+optimizer kernel (``host_factor``), so ``param.grad`` after backward holds the *sum* of
+the ranks' (loss-scaled) gradients until the optimizer consumes it; ``averaged_grads()``
+materialises the torch-DDP view for inspection and tests.
+"""
+from __future__ import annotations
+
+import contextlib
+import hashlib
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .. import ops
+from ..ops import reference
+from .bucketing import BucketPlan, plan_for_arena
+from .comm import broadcast_, make_comm
+from .flat import BufferArena, FlatArena
+
+
+class NativeDDP(nn.Module):
+    def __init__(self, module: nn.Module, *, rank: int = 0, world_size: int = 1,
+                 device: Optional[torch.device] = None, bucket_cap_mb: float = 25.0,
+                 first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
+                 grad_dtype: str = "fp32", found_inf: Optional[torch.Tensor] = None,
+                 scale: Optional[torch.Tensor] = None, check_inf: bool = False,
+                 profile: bool = False, rebuild_buckets: bool = True, comm=None) -> None:
+        super().__init__()
+        self.module = module
+        self.rank, self.world_size = rank, world_size
+        self.device = device or next(module.parameters()).device
+        self.bucket_cap_mb, self.first_bucket_mb = bucket_cap_mb, first_bucket_mb
+        self.broadcast_buffers = broadcast_buffers
+        self.grad_dtype = grad_dtype
+        self.profile = profile
+        self.rebuild_buckets = rebuild_buckets and world_size > 1
+        self.require_backward_grad_sync = True
+        self._sync_buffers_next = True
+        self._rebuilt = False
+        self.found_inf = found_inf if found_inf is not None else torch.zeros(1, device=self.device)
+        self.scale = scale
+        self.check_inf = check_inf
+
+        named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
+        if world_size > 1:
+            self._verify_shapes([p for _, p in named])
+        # Arena order = reverse definition order ~ gradient-ready order (first bucket = head).
+        named = list(reversed(named))
+        self.arena = FlatArena([p for _, p in named], names=[n for n, _ in named])
+        self.buffers_arena = BufferArena(module)
+        self.comm = comm if comm is not None else (make_comm(self.device, rank, world_size)
+                                                   if world_size > 1 else None)
+        if world_size > 1:
+            broadcast_(self.arena.param_flat, self.comm, 0)
+            for t in self.buffers_arena.tensors():
+                broadcast_(t, self.comm, 0)
+        self.reducer = None
+        self.plan: Optional[BucketPlan] = None
+        self._wire_buf = None
+        self._build_reducer()
+
+    # ------------------------------------------------------------------ construction
+    def _verify_shapes(self, params: List[torch.Tensor]) -> None:
+        desc = ";".join(f"{tuple(p.shape)}:{p.dtype}" for p in params)
+        digest = hashlib.sha1(desc.encode()).hexdigest()
+        gathered = [None] * self.world_size
+        dist.all_gather_object(gathered, (digest, len(params)))
+        if any(g != gathered[0] for g in gathered):
+            raise RuntimeError(f"NativeDDP: parameter shapes differ across ranks: {gathered}")
+
+    def _build_reducer(self) -> None:
+        self.plan = plan_for_arena(self.arena, self.bucket_cap_mb, self.first_bucket_mb)
+        if self.reducer is not None:
+            self.reducer.remove_hooks()
+            self.reducer = None
+        if self.world_size <= 1:
+            return
+        C = ops.native()  # the reducer is C++ on both the GPU and the gloo/CPU path
+        gpu = self.device.type == "cuda"
+        wire = 1 if self.grad_dtype == "bf16" else 0
+        if wire and gpu:
+            self._wire_buf = torch.zeros(self.arena.numel, dtype=torch.bfloat16, device=self.device)
+        wire_buf = self._wire_buf if self._wire_buf is not None else torch.empty(0)
+        py_cb = None if gpu else self._cpu_allreduce
+        self.reducer = C.Reducer(
+            list(self.arena.params), list(self.arena.grad_views), self.arena.grad_flat,
+            self.plan.offsets, self.plan.numels, self.plan.param_bucket, self.comm, py_cb, wire,
+            wire_buf, self.found_inf, self.scale if self.scale is not None else torch.empty(0),
+            1.0 / self.world_size, bool(self.check_inf), bool(self.profile))
+
+    def _cpu_allreduce(self, b: int, off: int, n: int) -> None:
+        """gloo path: called by the C++ reducer when bucket ``b`` is complete."""
+        view = self.arena.grad_flat[off:off + n]
+        if self.grad_dtype == "bf16":
+            wire = view.to(torch.bfloat16)
+            dist.all_reduce(wire)
+            view.copy_(wire.float())
+        else:
+            dist.all_reduce(view)
+        if self.check_inf:
+            reference.grad_check(view, self.scale, 1.0 / self.world_size, self.found_inf)
+
+    # ------------------------------------------------------------------ runtime
+    @property
+    def grad_factor(self) -> float:
+        """Host-side factor the optimizer applies to the arena gradients (1/world_size)."""
+        return 1.0 / self.world_size
+
+    @property
+    def grads_checked(self) -> bool:
+        """True when the reducer already ran the non-finite check on every bucket."""
+        return self.reducer is not None and self.check_inf and self.require_backward_grad_sync
+
+    def forward(self, *args, **kwargs):
+        if self.world_size > 1 and self.broadcast_buffers and self._sync_buffers_next \
+                and len(self.buffers_arena):
+            for t in self.buffers_arena.tensors():
+                broadcast_(t, self.comm, 0)
+        out = self.module(*args, **kwargs)
+        grad_on = torch.is_grad_enabled()
+        if grad_on and self.reducer is not None and self.require_backward_grad_sync:
+            self.reducer.prepare_for_backward()
+        self._sync_buffers_next = grad_on and self.require_backward_grad_sync
+        return out
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        if self.reducer is not None:
+            self.reducer.set_require_sync(False)
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+            if self.reducer is not None:
+                self.reducer.set_require_sync(old)
+
+    def maybe_rebuild_buckets(self, optimizer=None) -> bool:
+        """Once, after the first synced backward: re-lay the arena in observed ready order.
+
+        Must be called after backward and before the optimizer creates state (or the
+        optimizer must expose ``arena_state()`` / ``set_arena_state()`` to be permuted).
+        """
+        if not self.rebuild_buckets or self._rebuilt or self.reducer is None:
+            return False
+        if self.reducer.backward_count < 1:
+            return False
+        self._rebuilt = True
+        order = list(self.reducer.ready_order())
+        n = len(self.arena.params)
+        seen = set(order)
+        order += [i for i in range(n) if i not in seen]   # unused params keep relative order
+        if order == list(range(n)):
+            return False
+        # Ranks must agree on the layout: use rank 0's observed order.
+        box = [order]
+        if dist.is_initialized() and self.world_size > 1:
+            dist.broadcast_object_list(box, src=0)
+        order = box[0]
+        state = optimizer.arena_state() if optimizer is not None and hasattr(optimizer, "arena_state") else []
+        perm = self.arena.relayout(order, extra=state)
+        if state:
+            optimizer.set_arena_state(perm.extra)
+        if self._wire_buf is not None:
+            self._wire_buf = torch.zeros(self.arena.numel, dtype=torch.bfloat16, device=self.device)
+        self._build_reducer()
+        return True
+
+    def averaged_grads(self) -> List[torch.Tensor]:
+        """Per-parameter gradients as torch DDP would present them (sum / world_size)."""
+        return [g / self.world_size for g in self.arena.grad_views]
+
+    def bucket_sizes_mib(self) -> List[float]:
+        return self.plan.sizes_mib(self.arena.param_flat.element_size()) if self.plan else []
+
+    def comm_profile(self):
+        if self.reducer is None:
+            return None
+        return {"bucket_ms": list(self.reducer.bucket_times_ms()),
+                "step_ms": list(self.reducer.step_times_ms())}
+
+    def state_dict(self, *a, **kw):  # unwrapped keys, torchvision-compatible
+        return self.module.state_dict(*a, **kw)
+
+    def load_state_dict(self, sd, strict: bool = True):
+        return self.module.load_state_dict(sd, strict=strict)
