@@ -36,7 +36,7 @@ const float* opt_f32(const c10::optional<Tensor>& t, const char* name) {
 void grad_check(Tensor g, c10::optional<Tensor> scale, double host_factor, Tensor found_inf) {
   check_flat_f32(g, "grad");
   check_flat_f32(found_inf, "found_inf", 1);
-  c10::hip::HIPGuard guard(g.device());
+  c10::hip::HIPGuard guard(g.device().index());
   dpt::launch_grad_check(g.data_ptr<float>(), g.numel(), opt_f32(scale, "scale"), (float)host_factor,
                          found_inf.data_ptr<float>(), cur_stream(g));
 }
@@ -51,7 +51,7 @@ void sgd_step(Tensor p, Tensor g, Tensor buf, double lr, double momentum, double
     check_flat_f32(buf, "momentum_buffer");
     TORCH_CHECK(buf.numel() == p.numel(), "momentum buffer size mismatch");
   }
-  c10::hip::HIPGuard guard(p.device());
+  c10::hip::HIPGuard guard(p.device().index());
   dpt::launch_sgd(p.data_ptr<float>(), g.data_ptr<float>(),
                   momentum != 0.0 ? buf.data_ptr<float>() : nullptr, p.numel(), (float)lr,
                   (float)momentum, (float)dampening, (float)wd, nesterov, opt_f32(scale, "scale"),
@@ -68,7 +68,7 @@ void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, double lr, double beta1, 
   check_flat_f32(v, "exp_avg_sq");
   TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(),
               "adam arena size mismatch");
-  c10::hip::HIPGuard guard(p.device());
+  c10::hip::HIPGuard guard(p.device().index());
   dpt::launch_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                    p.numel(), (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, adamw,
                    opt_f32(scale, "scale"), (float)host_factor, opt_f32(found_inf, "found_inf"),
@@ -87,7 +87,7 @@ void optim_tail(c10::optional<Tensor> scale, c10::optional<Tensor> growth_tracke
   }
   float* sc = const_cast<float*>(opt_f32(scale, "scale"));
   TORCH_CHECK(sc == nullptr || gt != nullptr, "scale needs a growth_tracker");
-  c10::hip::HIPGuard guard(found_inf.device());
+  c10::hip::HIPGuard guard(found_inf.device().index());
   dpt::launch_optim_tail(sc, gt, found_inf.data_ptr<float>(), const_cast<float*>(opt_f32(step, "step")),
                          (float)growth_factor, (float)backoff_factor, (int)growth_interval,
                          cur_stream(found_inf));
@@ -97,7 +97,7 @@ void pack_bf16(Tensor src, Tensor dst) {
   check_flat_f32(src, "src", 8);
   TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kBFloat16 && dst.is_contiguous() &&
                   dst.numel() == src.numel(), "dst must be a contiguous bf16 GPU tensor of src's size");
-  c10::hip::HIPGuard guard(src.device());
+  c10::hip::HIPGuard guard(src.device().index());
   dpt::launch_pack_bf16(src.data_ptr<float>(), reinterpret_cast<uint16_t*>(dst.data_ptr()), src.numel(),
                         cur_stream(src));
 }
@@ -107,7 +107,7 @@ void unpack_bf16(Tensor src, Tensor dst, c10::optional<Tensor> scale, double hos
   check_flat_f32(dst, "dst", 8);
   TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kBFloat16 && src.is_contiguous() &&
                   dst.numel() == src.numel(), "src must be a contiguous bf16 GPU tensor of dst's size");
-  c10::hip::HIPGuard guard(dst.device());
+  c10::hip::HIPGuard guard(dst.device().index());
   dpt::launch_unpack_bf16(reinterpret_cast<const uint16_t*>(src.data_ptr()), dst.data_ptr<float>(),
                           dst.numel(), opt_f32(scale, "scale"), (float)host_factor,
                           const_cast<float*>(opt_f32(found_inf, "found_inf")), cur_stream(dst));
@@ -133,7 +133,7 @@ void accumulate_metrics(Tensor logits, Tensor targets, c10::optional<Tensor> los
     lf = loss->detach().to(at::kFloat).reshape({1});
     lp = lf.data_ptr<float>();
   }
-  c10::hip::HIPGuard guard(logits.device());
+  c10::hip::HIPGuard guard(logits.device().index());
   dpt::launch_metrics(logits.data_ptr(), dt, logits.size(0), logits.size(1), logits.stride(0),
                       targets.data_ptr<int64_t>(), lp, acc.data_ptr<double>(), cur_stream(logits));
 }
@@ -165,7 +165,7 @@ void augment(Tensor data, Tensor idx, c10::optional<Tensor> offs, c10::optional<
   }
   dpt::AugNorm n{};
   for (int c = 0; c < C; ++c) { n.mean[c] = (float)mean[c]; n.inv_std[c] = (float)(1.0 / std[c]); }
-  c10::hip::HIPGuard guard(data.device());
+  c10::hip::HIPGuard guard(data.device().index());
   dpt::launch_augment(data.data_ptr<uint8_t>(), idx.data_ptr<int64_t>(), op, fp, out.data_ptr(),
                       out.scalar_type() == at::kBFloat16, nhwc, B, (int)C, (int)H, (int)W, (int)pad, n,
                       cur_stream(data));
@@ -205,7 +205,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                case at::kLong: w = dpt::WireType::kI64; break;
                default: TORCH_CHECK(false, "unsupported all_reduce dtype");
              }
-             c10::hip::HIPGuard guard(t.device());
+             c10::hip::HIPGuard guard(t.device().index());
              hipStream_t s = cur_stream(t);
              c.all_reduce(t.data_ptr(), (size_t)t.numel(), w, on_current_stream ? s : c.stream());
            }, py::arg("tensor"), py::arg("on_current_stream") = true)
@@ -219,7 +219,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                case at::kLong: w = dpt::WireType::kI64; break;
                default: TORCH_CHECK(false, "unsupported broadcast dtype");
              }
-             c10::hip::HIPGuard guard(t.device());
+             c10::hip::HIPGuard guard(t.device().index());
              c.broadcast(t.data_ptr(), (size_t)t.numel(), w, root, cur_stream(t));
            }, py::arg("tensor"), py::arg("root") = 0)
       .def("abort", &dpt::RcclComm::abort)

@@ -28,10 +28,13 @@ def setup_miopen_env(scratch: str | None = None) -> str:
     cache.mkdir(parents=True, exist_ok=True)
     if SHIPPED_DB.is_dir():
         for f in SHIPPED_DB.iterdir():
-            if f.is_file() and f.suffix in (".txt", ".fdb", ".udb", ".ufdb", ".db") or f.name.endswith(".txt"):
-                dst = db / f.name
-                if not dst.exists():
-                    shutil.copy2(f, dst)
+            if not f.is_file():
+                continue
+            # find/perf databases (text) seed the user db; the compiled-kernel cache (.ukdb)
+            # seeds the kernel cache so a fresh box does not recompile MIOpen's kernels.
+            dst = (cache if f.suffix == ".ukdb" else db) / f.name
+            if not dst.exists():
+                shutil.copy2(f, dst)
     os.environ["MIOPEN_USER_DB_PATH"] = str(db)
     os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", str(cache))
     return str(db)
@@ -47,6 +50,11 @@ def export_miopen_db(dest: str | None = None) -> int:
     n = 0
     for f in src.iterdir():
         if f.is_file() and f.name.endswith(".txt"):
+            shutil.copy2(f, out / f.name)
+            n += 1
+    cache = Path(os.environ.get("MIOPEN_CUSTOM_CACHE_DIR", ""))
+    if cache.is_dir():
+        for f in cache.glob("*.ukdb"):
             shutil.copy2(f, out / f.name)
             n += 1
     return n
