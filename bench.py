@@ -48,6 +48,9 @@ def parse(argv=None):
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--first-bucket-mb", type=float, default=1.0)
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--no-fused-bn", action="store_true", help="A/B: MIOpen BN + separate ReLU/add")
+    ap.add_argument("--no-find", action="store_true",
+                    help="cudnn.benchmark=False: MIOpen immediate mode (find-db / heuristics, no find)")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="extra steps after the timed window with the hipEvent sync timeline")
     ap.add_argument("--json-out", default=None)
@@ -66,6 +69,8 @@ def train_args(a):
         argv.append("--amp")
     if not a.no_channels_last:
         argv.append("--channels-last")
+    if a.no_fused_bn:
+        argv.append("--no-fused-bn")
     return parse_args(argv)
 
 
@@ -84,7 +89,7 @@ def main(argv=None) -> int:
     if ws != a.gpus and rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={ws}; reporting WORLD_SIZE", file=sys.stderr)
     set_seed(0, rank)
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = not a.no_find
 
     model = build_model(args.model, args.num_classes, device, image_size=args.image_size,
                         channels_last=args.channels_last)
@@ -139,7 +144,8 @@ def main(argv=None) -> int:
         "config": {"model": args.model, "global_batch": a.batch_size * ws, "per_gpu_batch": a.batch_size,
                    "seq_len": None, "image_size": args.image_size, "parallelism": f"dp{ws}",
                    "impl": a.impl, "optimizer": a.optimizer, "channels_last": bool(args.channels_last),
-                   "bucket_cap_mb": a.bucket_cap_mb, "grad_dtype": a.grad_dtype},
+                   "bucket_cap_mb": a.bucket_cap_mb, "grad_dtype": a.grad_dtype,
+                   "fused_bn": bool(args.fused_bn and a.impl == "native" and args.channels_last)},
         "baseline": {"stock_torch_1gpu_img_s": base, "source": "BASELINE.md (MI355X, --impl torch)"},
         "warmup_seconds": round(warm_s, 1),
     }

@@ -171,6 +171,105 @@ void augment(Tensor data, Tensor idx, c10::optional<Tensor> offs, c10::optional<
                       cur_stream(data));
 }
 
+int bn_dtype(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kHalf: return 2;
+    default: TORCH_CHECK(false, "fused BN supports f32/bf16/f16 activations");
+  }
+  return 0;
+}
+
+// Activation as a row-major [M, C] view: 4-D channels_last or 2-D contiguous.
+std::pair<int64_t, int64_t> bn_rows(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  if (t.dim() == 4) {
+    TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name, " must be channels_last");
+    return {t.size(0) * t.size(2) * t.size(3), t.size(1)};
+  }
+  TORCH_CHECK(t.dim() == 2 && t.is_contiguous(), name, " must be 4-D channels_last or 2-D contiguous");
+  return {t.size(0), t.size(1)};
+}
+
+float* f32_param(const c10::optional<Tensor>& t, int64_t C, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C,
+              name, " must be a contiguous float32 GPU tensor of C elements");
+  return t->data_ptr<float>();
+}
+
+std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::optional<Tensor> weight,
+                                 c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
+                                 c10::optional<Tensor> running_var, c10::optional<Tensor> num_batches,
+                                 double momentum, double eps, bool relu) {
+  auto [M, C] = bn_rows(x, "x");
+  TORCH_CHECK(dpt::bn_supported(C), "fused BN: unsupported channel count ", C);
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->scalar_type() == x.scalar_type(), "residual mismatch");
+    bn_rows(*residual, "residual");
+    rp = residual->data_ptr();
+  }
+  int64_t* nb = nullptr;
+  if (num_batches.has_value() && num_batches->defined()) {
+    TORCH_CHECK(num_batches->is_cuda() && num_batches->scalar_type() == at::kLong, "num_batches must be int64 GPU");
+    nb = num_batches->data_ptr<int64_t>();
+  }
+  auto y = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  auto ws = at::empty({dpt::bn_workspace_floats(M, C)}, fopt);
+  c10::hip::HIPGuard guard(x.device().index());
+  dpt::launch_bn_fwd_train(bn_dtype(x), x.data_ptr(), rp, y.data_ptr(), M, C, f32_param(weight, C, "weight"),
+                           f32_param(bias, C, "bias"), (float)eps, (float)momentum,
+                           f32_param(running_mean, C, "running_mean"), f32_param(running_var, C, "running_var"), nb,
+                           mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr<float>(), relu,
+                           cur_stream(x));
+  return {y, mean, invstd};
+}
+
+Tensor bn_apply(Tensor x, c10::optional<Tensor> residual, Tensor a, Tensor b, bool relu) {
+  auto [M, C] = bn_rows(x, "x");
+  TORCH_CHECK(dpt::bn_supported(C), "fused BN: unsupported channel count ", C);
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->scalar_type() == x.scalar_type(), "residual mismatch");
+    bn_rows(*residual, "residual");
+    rp = residual->data_ptr();
+  }
+  auto y = at::empty_like(x);
+  c10::hip::HIPGuard guard(x.device().index());
+  dpt::launch_bn_apply(bn_dtype(x), x.data_ptr(), rp, y.data_ptr(), M, C, f32_param(a, C, "a"),
+                       f32_param(b, C, "b"), relu, cur_stream(x));
+  return y;
+}
+
+std::vector<Tensor> bn_bwd(Tensor dy, c10::optional<Tensor> y, Tensor x, c10::optional<Tensor> weight, Tensor mean,
+                           Tensor invstd, bool relu, bool want_dres, bool want_dparams) {
+  auto [M, C] = bn_rows(x, "x");
+  auto [Md, Cd] = bn_rows(dy, "grad_output");
+  TORCH_CHECK(M == Md && C == Cd && dy.scalar_type() == x.scalar_type(), "grad_output mismatch");
+  const void* yp = nullptr;
+  if (relu) {
+    TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the saved output");
+    bn_rows(*y, "y");
+    yp = y->data_ptr();
+  }
+  auto fopt = x.options().dtype(at::kFloat);
+  auto dx = at::empty_like(x);
+  Tensor dres = want_dres ? at::empty_like(x) : Tensor();
+  Tensor dg = want_dparams ? at::empty({C}, fopt) : Tensor();
+  Tensor db = want_dparams ? at::empty({C}, fopt) : Tensor();
+  auto ws = at::empty({dpt::bn_workspace_floats(M, C)}, fopt);
+  c10::hip::HIPGuard guard(x.device().index());
+  dpt::launch_bn_bwd(bn_dtype(x), dy.data_ptr(), yp, x.data_ptr(), M, C, f32_param(weight, C, "weight"),
+                     f32_param(mean, C, "mean"), f32_param(invstd, C, "invstd"),
+                     want_dparams ? dg.data_ptr<float>() : nullptr, want_dparams ? db.data_ptr<float>() : nullptr,
+                     dx.data_ptr(), want_dres ? dres.data_ptr() : nullptr, ws.data_ptr<float>(), relu, cur_stream(x));
+  return {dx, dg, db, dres};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -189,6 +288,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("accumulate_metrics", &accumulate_metrics, py::arg("logits"), py::arg("targets"), py::arg("loss"), py::arg("acc"));
   m.def("augment", &augment, py::arg("data"), py::arg("idx"), py::arg("offs"), py::arg("flips"), py::arg("out"),
         py::arg("nhwc"), py::arg("pad"), py::arg("mean"), py::arg("std"));
+  m.def("bn_supported", [](int64_t C) { return dpt::bn_supported(C); });
+  m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("residual"), py::arg("weight"), py::arg("bias"),
+        py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches"), py::arg("momentum"), py::arg("eps"),
+        py::arg("relu"));
+  m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("residual"), py::arg("a"), py::arg("b"), py::arg("relu"));
+  m.def("bn_bwd", &bn_bwd, py::arg("grad_output"), py::arg("y"), py::arg("x"), py::arg("weight"), py::arg("mean"),
+        py::arg("invstd"), py::arg("relu"), py::arg("want_dres"), py::arg("want_dparams"));
   m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
 
   py::class_<dpt::RcclComm, std::shared_ptr<dpt::RcclComm>>(m, "RcclComm")

@@ -39,4 +39,23 @@ void launch_augment(const uint8_t* data, const int64_t* idx, const int32_t* offs
                     const uint8_t* flips, void* out, bool out_bf16, bool nhwc, int64_t B, int C,
                     int H, int W, int pad, AugNorm norm, hipStream_t s);
 
+// bn_kernels.hip  (dtype: 0 f32, 1 bf16, 2 f16; activations channels_last = row-major [M, C])
+struct BnGeometry {
+  int64_t rows_per_chunk;
+  int chunks;
+  int apply_blocks;
+};
+bool bn_supported(int64_t C);
+BnGeometry bn_geometry(int64_t M, int64_t C);
+int64_t bn_workspace_floats(int64_t M, int64_t C);
+void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
+                         const float* gamma, const float* beta, float eps, float momentum, float* run_mean,
+                         float* run_var, int64_t* num_batches, float* save_mean, float* save_invstd,
+                         float* workspace, bool relu, hipStream_t s);
+void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
+                     const float* coef_a, const float* coef_b, bool relu, hipStream_t s);
+void launch_bn_bwd(int dtype, const void* dy, const void* y, const void* x, int64_t M, int64_t C,
+                   const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                   void* dx, void* dres, float* workspace, bool relu, hipStream_t s);
+
 }  // namespace dpt

@@ -76,6 +76,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="all-reduce wire dtype (bf16 = gradient compression, native only)")
     g.add_argument("--channels-last", action="store_true",
                    help="NHWC activations/weights (MIOpen's fast layout on gfx950)")
+    g.add_argument("--no-fused-bn", dest="fused_bn", action="store_false",
+                   help="native impl: keep MIOpen BatchNorm + separate ReLU/add instead of the fused "
+                        "gfx950 BN(+add)(+ReLU) kernels (channels_last GPU runs)")
     g.add_argument("--max-steps", default=0, type=int,
                    help="stop each epoch after this many steps (0 = full epoch)")
     g.add_argument("--warmup-steps", default=0, type=int,

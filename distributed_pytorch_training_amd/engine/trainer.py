@@ -17,6 +17,7 @@ Two engines share that contract:
 """
 from __future__ import annotations
 
+import contextlib
 import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
@@ -73,6 +74,7 @@ class Trainer:
         self.timeline = StepTimeline(device, enabled=getattr(args, "profile_sync", False))
         self.global_step = 0
         self.grad_accum = max(1, getattr(args, "grad_accum", 1))
+        self._accum_fresh = True
         if self.impl == "native":
             self._init_native(model, comm)
         else:
@@ -84,6 +86,10 @@ class Trainer:
         from ..parallel.ddp import NativeDDP
 
         args = self.args
+        if (getattr(args, "fused_bn", True) and self.device.type == "cuda"
+                and getattr(args, "channels_last", False)):
+            from ..models.layers import fuse_batchnorm
+            fuse_batchnorm(model)
         params_in_order = [p for p in model.parameters() if p.requires_grad]
         self.scaler = DeviceGradScaler(self.device, enabled=self.amp)
         self.ddp = NativeDDP(model, rank=self.rank, world_size=self.world_size, device=self.device,
@@ -122,21 +128,32 @@ class Trainer:
         self.ddp = None
 
     # ------------------------------------------------------------------ one step
-    def train_step(self, images: torch.Tensor, targets: torch.Tensor):
-        """Forward + backward + optimizer for one batch; returns (outputs, loss)."""
-        if self.impl == "native":
-            return self._native_step(images, targets)
-        return self._torch_step(images, targets)
+    def train_step(self, images: torch.Tensor, targets: torch.Tensor, sync: bool = True):
+        """Forward + backward (+ optimizer when ``sync``) for one batch; returns (outputs, loss).
 
-    def _native_step(self, images, targets):
+        ``sync=False`` is a gradient-accumulation micro-batch (``--grad-accum``): no
+        all-reduce (``no_sync``), no optimizer step, gradients keep accumulating.
+        """
+        if self.impl == "native":
+            return self._native_step(images, targets, sync)
+        return self._torch_step(images, targets, sync)
+
+    def _native_step(self, images, targets, sync: bool = True):
         tl = self.timeline
         tl.mark("start")
-        with autocast(self.device, self.amp, self.amp_dtype):
-            outputs = self.model(images)
-            loss = self.criterion(outputs, targets)
-        tl.mark("fwd")
-        (self.scaler.scale(loss) if self.amp else loss).backward()
+        ctx = self.ddp.no_sync() if not sync else contextlib.nullcontext()
+        with ctx:
+            with autocast(self.device, self.amp, self.amp_dtype):
+                outputs = self.model(images)
+                loss = self.criterion(outputs, targets)
+            tl.mark("fwd")
+            scaled = loss / self.grad_accum if self.grad_accum > 1 else loss
+            (self.scaler.scale(scaled) if self.amp else scaled).backward()
         tl.mark("bwd")
+        if not sync:
+            ops.accumulate_metrics(outputs, targets, loss, self.metrics)
+            tl.discard()
+            return outputs, loss
         if self.ddp.maybe_rebuild_buckets(self.optimizer) and self.rank == 0 and getattr(self.args, "verbose", False):
             self.log(f"rebuilt buckets: {self.ddp.bucket_sizes_mib()}")
         self.optimizer.step(self.scaler if self.amp else None, host_factor=self.ddp.grad_factor,
@@ -147,20 +164,24 @@ class Trainer:
         self.global_step += 1
         return outputs, loss
 
-    def _torch_step(self, images, targets):
-        self.optimizer.zero_grad(set_to_none=True)
-        if self.amp and self.scaler.is_enabled():
-            with autocast(self.device, True, self.amp_dtype):
-                outputs = self.model(images)
-                loss = self.criterion(outputs, targets)
-            self.scaler.scale(loss).backward()
-            self.scaler.step(self.optimizer)
-            self.scaler.update()
-        else:
+    def _torch_step(self, images, targets, sync: bool = True):
+        if self._accum_fresh:
+            self.optimizer.zero_grad(set_to_none=True)
+        use_scaler = self.amp and self.scaler.is_enabled()
+        ctx = self.model.no_sync() if (not sync and hasattr(self.model, "no_sync")) else contextlib.nullcontext()
+        with ctx:
             with autocast(self.device, self.amp, self.amp_dtype):
                 outputs = self.model(images)
                 loss = self.criterion(outputs, targets)
-            loss.backward()
+            scaled = loss / self.grad_accum if self.grad_accum > 1 else loss
+            (self.scaler.scale(scaled) if use_scaler else scaled).backward()
+        self._accum_fresh = sync
+        if not sync:
+            return outputs, loss
+        if use_scaler:
+            self.scaler.step(self.optimizer)
+            self.scaler.update()
+        else:
             self.optimizer.step()
         self.global_step += 1
         return outputs, loss
@@ -185,8 +206,9 @@ class Trainer:
         win_start = time.time()
         steps = 0
         for i, (images, targets) in enumerate(loader):
+            sync = (i + 1) % self.grad_accum == 0 or i + 1 == n
             if native:
-                self.train_step(images, targets)
+                self.train_step(images, targets, sync)
                 bs = images.size(0)
                 accum_samples += bs * ws
                 steps += 1
@@ -205,7 +227,7 @@ class Trainer:
                     win_start = time.time()
             else:
                 batch_start = time.time()
-                outputs, loss = self.train_step(images, targets)
+                outputs, loss = self.train_step(images, targets, sync)
                 bs = images.size(0)
                 epoch_loss += loss.item() * bs
                 _, preds = outputs.max(1)

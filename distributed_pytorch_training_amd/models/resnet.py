@@ -13,8 +13,10 @@ MI355X notes
   because that is what the reference trains.
 * ``memory_format=torch.channels_last`` is applied by the trainer, not here: MIOpen's NHWC
   bf16 convolutions are the fast path on gfx950 and the choice is a runtime flag.
-* ReLU is in-place and the residual add is ``out += identity`` so the autograd graph keeps
-  one activation buffer per block boundary (HBM traffic is the bound for the 1x1 convs).
+* BN -> (+identity) -> ReLU goes through ``layers.bn_act``: the torchvision composition
+  (in-place add and ReLU) with stock ``nn.BatchNorm2d``, or one fused gfx950 kernel chain
+  once ``layers.fuse_batchnorm`` has installed ``FusedBatchNorm2d`` (the native engine
+  does this for channels_last GPU runs).
 """
 from __future__ import annotations
 
@@ -22,6 +24,8 @@ from typing import List, Optional, Type, Union
 
 import torch
 import torch.nn as nn
+
+from .layers import bn_act
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -48,10 +52,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         identity = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        out += identity
-        return self.relu(out)
+        out = bn_act(self.bn1, self.conv1(x))
+        return bn_act(self.bn2, self.conv2(out), residual=identity)
 
 
 class Bottleneck(nn.Module):
@@ -74,11 +76,9 @@ class Bottleneck(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         identity = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        out += identity
-        return self.relu(out)
+        out = bn_act(self.bn1, self.conv1(x))
+        out = bn_act(self.bn2, self.conv2(out))
+        return bn_act(self.bn3, self.conv3(out), residual=identity)
 
 
 class ResNet(nn.Module):
@@ -126,7 +126,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(bn_act(self.bn1, self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

@@ -1,0 +1,84 @@
+"""Fused BatchNorm(+ReLU)(+residual add) autograd op on the gfx950 kernels (bn_kernels.hip).
+
+Semantics are exactly ``relu(batch_norm(x) + residual)`` in training mode (batch
+statistics, biased variance for normalisation, unbiased for the running variance,
+``momentum`` update, ``num_batches_tracked += 1``) and ``relu(x*a + b + residual)`` with
+the running statistics in eval mode - the composition the reference's ResNet blocks run as
+separate MIOpen/ATen kernels (BN, in-place add, in-place ReLU).
+
+Saved for backward: the BN input ``x`` and (with ReLU) the output ``y`` - the same tensors
+the unfused graph keeps alive (BN saves its input, ReLU its output, and ``y`` is the next
+convolution's saved input anyway), so the fusion costs no extra activation memory.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import native, native_available
+
+
+def _cl(t: torch.Tensor) -> torch.Tensor:
+    if t.dim() == 4 and not t.is_contiguous(memory_format=torch.channels_last):
+        return t.contiguous(memory_format=torch.channels_last)
+    return t
+
+
+class _BNActTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu):
+        C = native()
+        y, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var, num_batches,
+                                         float(momentum), float(eps), bool(relu))
+        ctx.relu = bool(relu)
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, mean, invstd = ctx.saved_tensors
+        want_params = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        dx, dg, db, dr = native().bn_bwd(_cl(dy), y, x, weight, mean, invstd, ctx.relu,
+                                         ctx.has_res and ctx.needs_input_grad[1], bool(want_params))
+        return (dx, dr if ctx.has_res and ctx.needs_input_grad[1] else None,
+                dg if want_params else None, db if want_params else None,
+                None, None, None, None, None, None)
+
+
+def bn_act_supported(x: torch.Tensor, num_features: int) -> bool:
+    return (x.is_cuda and native_available() and x.dim() == 4
+            and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and native().bn_supported(num_features))
+
+
+def bn_act_train(x: torch.Tensor, residual: Optional[torch.Tensor], weight, bias, running_mean, running_var,
+                 num_batches, momentum: float, eps: float, relu: bool) -> torch.Tensor:
+    if residual is not None:
+        residual = _cl(residual.to(x.dtype))
+    return _BNActTrain.apply(x, residual, weight, bias, running_mean, running_var, num_batches,
+                             momentum, eps, relu)
+
+
+@torch.no_grad()
+def bn_act_eval(x: torch.Tensor, residual: Optional[torch.Tensor], weight, bias, running_mean, running_var,
+                eps: float, relu: bool) -> torch.Tensor:
+    a = torch.rsqrt(running_var.float() + eps)
+    if weight is not None:
+        a = a * weight.float()
+    b = -running_mean.float() * a
+    if bias is not None:
+        b = b + bias.float()
+    if residual is not None:
+        residual = _cl(residual.to(x.dtype))
+    return native().bn_apply(x, residual, a.contiguous(), b.contiguous(), bool(relu))
+
+
+def reference_bn_act(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu):
+    """Unfused PyTorch composition (CPU path and test oracle)."""
+    y = torch.nn.functional.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return torch.relu(y) if relu else y

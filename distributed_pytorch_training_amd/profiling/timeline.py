@@ -42,6 +42,10 @@ class StepTimeline:
         ev.record()
         self._marks[name] = ev
 
+    def discard(self) -> None:
+        """Drop the marks of a step that did not run the optimizer (accumulation micro-batch)."""
+        self._marks = {}
+
     def end_step(self, comm_profile: Optional[dict]) -> None:
         if not self.enabled:
             return

@@ -32,8 +32,11 @@ def test_native_matches_torch_fp32(cuda, opt):
         y = torch.randint(0, 10, (16,), device=cuda, generator=g)
         nat.train_step(x, y)
         ref.train_step(x, y)
+    # Adam moves every weight by ~lr*sign(m/sqrt(v)); near-zero gradients flip sign on fp noise
+    # between two conv algorithm runs, so its parity bound is a few lr steps.
+    atol = 2e-4 if opt == "sgd" else 4e-3
     for (n, p), (_, q) in zip(nat.module.named_parameters(), ref.module.named_parameters()):
-        torch.testing.assert_close(p, q, rtol=2e-3, atol=2e-4, msg=n)
+        torch.testing.assert_close(p, q, rtol=2e-3, atol=atol, msg=n)
 
 
 def test_native_amp_bf16_step_and_scaler(cuda):
