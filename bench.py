@@ -49,8 +49,10 @@ def parse(argv=None):
     ap.add_argument("--first-bucket-mb", type=float, default=1.0)
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--no-fused-bn", action="store_true", help="A/B: MIOpen BN + separate ReLU/add")
-    ap.add_argument("--no-find", action="store_true",
-                    help="cudnn.benchmark=False: MIOpen immediate mode (find-db / heuristics, no find)")
+    ap.add_argument("--find", action="store_true",
+                    help="cudnn.benchmark=True: run MIOpen find (minutes on a fresh box). Default is "
+                         "immediate mode, which reads the find-db shipped in miopen_db/ (tuned on MI355X "
+                         "for this config) and skips the search")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="extra steps after the timed window with the hipEvent sync timeline")
     ap.add_argument("--json-out", default=None)
@@ -89,7 +91,7 @@ def main(argv=None) -> int:
     if ws != a.gpus and rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={ws}; reporting WORLD_SIZE", file=sys.stderr)
     set_seed(0, rank)
-    torch.backends.cudnn.benchmark = not a.no_find
+    torch.backends.cudnn.benchmark = bool(a.find)
 
     model = build_model(args.model, args.num_classes, device, image_size=args.image_size,
                         channels_last=args.channels_last)
@@ -145,7 +147,8 @@ def main(argv=None) -> int:
                    "seq_len": None, "image_size": args.image_size, "parallelism": f"dp{ws}",
                    "impl": a.impl, "optimizer": a.optimizer, "channels_last": bool(args.channels_last),
                    "bucket_cap_mb": a.bucket_cap_mb, "grad_dtype": a.grad_dtype,
-                   "fused_bn": bool(args.fused_bn and a.impl == "native" and args.channels_last)},
+                   "fused_bn": bool(args.fused_bn and a.impl == "native" and args.channels_last),
+                   "miopen": "find" if a.find else "immediate(find-db)"},
         "baseline": {"stock_torch_1gpu_img_s": base, "source": "BASELINE.md (MI355X, --impl torch)"},
         "warmup_seconds": round(warm_s, 1),
     }

@@ -2,7 +2,7 @@
 //
 // Why: on MI355X a ResNet-50 bf16 step (batch 256, channels_last) spends 37% of its kernel
 // time in MIOpen's BatchNorm kernels and another ~15% in the ReLU / threshold-backward /
-// residual-add elementwise kernels around them (profiles/resnet50_stock_breakdown.md) - all
+// residual-add elementwise kernels around them (profiles/resnet50_miopen_bn_breakdown.md) - all
 // HBM-bound passes over the same activations.  These kernels fuse them:
 //
 //   forward  (train): stats     read x                      -> per-chunk (sum, sumsq) partials
@@ -119,17 +119,19 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_stats_kernel(const void* __rest
   const int64_t row1 = min(row0 + rows_per_chunk, M);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int64_t r = row0 + rr;
-  for (; r + rpi < row1; r += 2 * rpi) {  // two rows in flight per thread
-    float a[8], b[8];
-    IO::load8(x, r * C + cg * 8, a);
-    IO::load8(x, (r + rpi) * C + cg * 8, b);
+  for (; r + 3 * rpi < row1; r += 4 * rpi) {  // four 16-byte rows in flight per thread
+    float a[4][8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      s[k] += a[k] + b[k];
-      q[k] += a[k] * a[k] + b[k] * b[k];
-    }
+    for (int u = 0; u < 4; ++u) IO::load8(x, (r + u * rpi) * C + cg * 8, a[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[k] += a[u][k];
+        q[k] += a[u][k] * a[u][k];
+      }
   }
-  if (r < row1) {
+  for (; r < row1; r += rpi) {
     float a[8];
     IO::load8(x, r * C + cg * 8, a);
 #pragma unroll
@@ -151,15 +153,30 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_stats_kernel(const void* __rest
   }
 }
 
-// Sum `chunks` partials of channel c with 32 lanes (one half-wave) in fp64.
+// Sum `chunks` partials of channel c with 32 lanes (one half-wave) in fp64.  Eight
+// independent loads in flight per lane: the partials are L2-resident, so this loop is
+// latency-bound, not bandwidth-bound.
 __device__ __forceinline__ void half_wave_sum2(const float* p1, const float* p2, int64_t c, int chunks,
                                                int part, double& s1, double& s2) {
+  constexpr int U = 8;
+  double a[U], b[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) { a[u] = 0.0; b[u] = 0.0; }
+  const float* q1 = p1 + c * chunks;
+  const float* q2 = p2 + c * chunks;
+  int k = part;
+  for (; k + 32 * (U - 1) < chunks; k += 32 * U) {
+    float x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) { x[u] = q1[k + 32 * u]; y[u] = q2[k + 32 * u]; }
+#pragma unroll
+    for (int u = 0; u < U; ++u) { a[u] += (double)x[u]; b[u] += (double)y[u]; }
+  }
+  for (; k < chunks; k += 32) { a[0] += (double)q1[k]; b[0] += (double)q2[k]; }
   s1 = 0.0;
   s2 = 0.0;
-  for (int k = part; k < chunks; k += 32) {
-    s1 += (double)p1[c * chunks + k];
-    s2 += (double)p2[c * chunks + k];
-  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) { s1 += a[u]; s2 += b[u]; }
 #pragma unroll
   for (int off = 16; off > 0; off >>= 1) {
     s1 += __shfl_xor(s1, off, 64);
@@ -256,7 +273,26 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_stats_kernel(const void* __rest
   const int64_t row0 = (int64_t)blockIdx.x * rows_per_chunk;
   const int64_t row1 = min(row0 + rows_per_chunk, M);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int64_t r = row0 + rr; r < row1; r += rpi) {
+  int64_t r = row0 + rr;
+  for (; r + rpi < row1; r += 2 * rpi) {  // two rows x three tensors in flight per thread
+    float g[2][8], xv[2][8];
+    bool m[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      IO::load8(dy, (r + u * rpi) * C + cg * 8, g[u]);
+      IO::load8(x, (r + u * rpi) * C + cg * 8, xv[u]);
+      if (RELU) IO::pos8(y, (r + u * rpi) * C + cg * 8, m[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float dz = (!RELU || m[u][k]) ? g[u][k] : 0.0f;
+        s[k] += dz;
+        q[k] += dz * (xv[u][k] - mu[k]);
+      }
+  }
+  for (; r < row1; r += rpi) {
     float g[8], xv[8];
     bool m[8];
     IO::load8(dy, r * C + cg * 8, g);
@@ -353,9 +389,10 @@ bool bn_supported(int64_t C) {
 BnGeometry bn_geometry(int64_t M, int64_t C) {
   BnGeometry g;
   const int64_t rpi = kBlock / (C / 8);
-  // Enough chunks to fill the chip (<= 2048 blocks), >= 64 rows each so the fp32 partials
-  // stay a few percent of the activation bytes; rows_per_chunk is a multiple of rpi.
-  int64_t rows = (M + 2047) / 2048;
+  // Enough chunks to fill the chip (<= 1024 blocks of 256 threads, 4 per CU), >= 64 rows
+  // each so the fp32 partials stay a few percent of the activation bytes and the finalize
+  // sweep stays short; rows_per_chunk is a multiple of rpi.
+  int64_t rows = (M + 1023) / 1024;
   if (rows < 64) rows = 64;
   rows = (rows + rpi - 1) / rpi * rpi;
   g.rows_per_chunk = rows;

@@ -82,6 +82,18 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             with perf_path.open("w") as f:
                 f.write(PERF_HEADER)
 
+    try:
+        _epochs(args, trainer, train_loader, val_loader, train_sampler, start_epoch, rank, world_size,
+                metrics_path, perf_path)
+    except BaseException:
+        trainer.abort()  # unblock peers stuck in RCCL collectives, then re-raise
+        raise
+    cleanup_distributed()
+    return 0
+
+
+def _epochs(args, trainer, train_loader, val_loader, train_sampler, start_epoch, rank, world_size,
+            metrics_path, perf_path) -> None:
     for epoch in range(start_epoch, args.epochs):
         st = trainer.train_one_epoch(epoch, train_loader, train_sampler)
         if args.validate:
@@ -110,5 +122,3 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                  "buckets_mib": trainer.ddp.bucket_sizes_mib() if trainer.ddp else []}
         trainer.timeline.dump(out, extra)
         print("sync-profile " + json.dumps(trainer.timeline.summary()), flush=True)
-    cleanup_distributed()
-    return 0

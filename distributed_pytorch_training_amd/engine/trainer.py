@@ -28,7 +28,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..amp import DeviceGradScaler, autocast
-from ..profiling.timeline import StepTimeline
+from ..profiling.timeline import StepTimeline, roctx_range
 
 
 def format_step_line(epoch: int, i: int, n: int, avg_loss: float, avg_acc: float, thr: float) -> str:
@@ -75,6 +75,7 @@ class Trainer:
         self.global_step = 0
         self.grad_accum = max(1, getattr(args, "grad_accum", 1))
         self._accum_fresh = True
+        self.roctx = bool(getattr(args, "roctx", False))
         if self.impl == "native":
             self._init_native(model, comm)
         else:
@@ -142,13 +143,15 @@ class Trainer:
         tl = self.timeline
         tl.mark("start")
         ctx = self.ddp.no_sync() if not sync else contextlib.nullcontext()
+        rx = self.roctx
         with ctx:
-            with autocast(self.device, self.amp, self.amp_dtype):
+            with roctx_range("forward", rx), autocast(self.device, self.amp, self.amp_dtype):
                 outputs = self.model(images)
                 loss = self.criterion(outputs, targets)
             tl.mark("fwd")
             scaled = loss / self.grad_accum if self.grad_accum > 1 else loss
-            (self.scaler.scale(scaled) if self.amp else scaled).backward()
+            with roctx_range("backward+allreduce", rx):
+                (self.scaler.scale(scaled) if self.amp else scaled).backward()
         tl.mark("bwd")
         if not sync:
             ops.accumulate_metrics(outputs, targets, loss, self.metrics)
@@ -156,8 +159,9 @@ class Trainer:
             return outputs, loss
         if self.ddp.maybe_rebuild_buckets(self.optimizer) and self.rank == 0 and getattr(self.args, "verbose", False):
             self.log(f"rebuilt buckets: {self.ddp.bucket_sizes_mib()}")
-        self.optimizer.step(self.scaler if self.amp else None, host_factor=self.ddp.grad_factor,
-                            grads_checked=self.ddp.grads_checked)
+        with roctx_range("optimizer", rx):
+            self.optimizer.step(self.scaler if self.amp else None, host_factor=self.ddp.grad_factor,
+                                grads_checked=self.ddp.grads_checked)
         tl.mark("opt")
         ops.accumulate_metrics(outputs, targets, loss, self.metrics)
         tl.end_step(self.ddp.comm_profile() if tl.enabled else None)
@@ -282,6 +286,13 @@ class Trainer:
         if self.rank == 0 and t[2] > 0:
             return EpochStats(t[0] / t[2], 100.0 * t[1] / t[2], time.time() - t0)
         return EpochStats(None, None, time.time() - t0)
+
+    def abort(self) -> None:
+        """Failure path: abort the RCCL communicator so peers blocked in a
+        collective error out instead of hanging until the process-group timeout."""
+        comm = getattr(self.ddp, "comm", None) if self.ddp is not None else None
+        if comm is not None:
+            comm.abort()
 
     # ------------------------------------------------------------------ checkpoint glue
     def model_state(self):

@@ -34,10 +34,14 @@ def test_fused_bn_train_matches_reference(cuda, dtype, shape, relu, res):
     xr = x.detach().float().requires_grad_()
     rr = r.detach().float().requires_grad_() if res else None
     y = bn_act(bn, x, relu=relu, residual=r)
-    yr = reference_bn_act(xr, rr, w, b, ref_rm, ref_rv, True, bn.momentum, bn.eps, relu)
+    zr = reference_bn_act(xr, rr, w, b, ref_rm, ref_rv, True, bn.momentum, bn.eps, False)
     rt, at = TOL[dtype]
     assert y.dtype == dtype and y.is_contiguous(memory_format=torch.channels_last)
-    torch.testing.assert_close(y.float(), yr, rtol=rt, atol=at)
+    torch.testing.assert_close(y.float(), torch.relu(zr) if relu else zr, rtol=rt, atol=at)
+    # Backward oracle through OUR ReLU mask: at z ~ 0 the two roundings of z may disagree on
+    # the sign, which flips one gradient element between pass-through and zero (a tie, not
+    # an error).
+    yr = zr * (y.detach() > 0).float() if relu else zr
     torch.testing.assert_close(bn.running_mean, ref_rm, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(bn.running_var, ref_rv, rtol=1e-4, atol=1e-5)
     assert bn.num_batches_tracked.item() == 1
