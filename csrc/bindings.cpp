@@ -245,11 +245,21 @@ Tensor bn_apply(Tensor x, c10::optional<Tensor> residual, Tensor a, Tensor b, bo
   return y;
 }
 
-std::vector<Tensor> bn_bwd(Tensor dy, c10::optional<Tensor> y, Tensor x, c10::optional<Tensor> weight, Tensor mean,
-                           Tensor invstd, bool relu, bool want_dres, bool want_dparams) {
+// Returns {dx, dgamma, dbeta, dz}.  dy2: gradient of the second (aliased) output, if the
+// forward exposed one.  dz (= the residual-path gradient) is materialised when want_dz or
+// dy2 is given.
+std::vector<Tensor> bn_bwd(Tensor dy, c10::optional<Tensor> dy2, c10::optional<Tensor> y, Tensor x,
+                           c10::optional<Tensor> weight, Tensor mean, Tensor invstd, bool relu, bool want_dz,
+                           bool want_dparams) {
   auto [M, C] = bn_rows(x, "x");
   auto [Md, Cd] = bn_rows(dy, "grad_output");
   TORCH_CHECK(M == Md && C == Cd && dy.scalar_type() == x.scalar_type(), "grad_output mismatch");
+  const void* d2 = nullptr;
+  if (dy2.has_value() && dy2->defined()) {
+    auto [M2, C2] = bn_rows(*dy2, "grad_output2");
+    TORCH_CHECK(M2 == M && C2 == C && dy2->scalar_type() == x.scalar_type(), "grad_output2 mismatch");
+    d2 = dy2->data_ptr();
+  }
   const void* yp = nullptr;
   if (relu) {
     TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the saved output");
@@ -258,16 +268,17 @@ std::vector<Tensor> bn_bwd(Tensor dy, c10::optional<Tensor> y, Tensor x, c10::op
   }
   auto fopt = x.options().dtype(at::kFloat);
   auto dx = at::empty_like(x);
-  Tensor dres = want_dres ? at::empty_like(x) : Tensor();
+  const bool make_dz = want_dz || d2 != nullptr;
+  Tensor dz = make_dz ? at::empty_like(x) : Tensor();
   Tensor dg = want_dparams ? at::empty({C}, fopt) : Tensor();
   Tensor db = want_dparams ? at::empty({C}, fopt) : Tensor();
   auto ws = at::empty({dpt::bn_workspace_floats(M, C)}, fopt);
   c10::hip::HIPGuard guard(x.device().index());
-  dpt::launch_bn_bwd(bn_dtype(x), dy.data_ptr(), yp, x.data_ptr(), M, C, f32_param(weight, C, "weight"),
+  dpt::launch_bn_bwd(bn_dtype(x), dy.data_ptr(), d2, yp, x.data_ptr(), M, C, f32_param(weight, C, "weight"),
                      f32_param(mean, C, "mean"), f32_param(invstd, C, "invstd"),
                      want_dparams ? dg.data_ptr<float>() : nullptr, want_dparams ? db.data_ptr<float>() : nullptr,
-                     dx.data_ptr(), want_dres ? dres.data_ptr() : nullptr, ws.data_ptr<float>(), relu, cur_stream(x));
-  return {dx, dg, db, dres};
+                     dx.data_ptr(), make_dz ? dz.data_ptr() : nullptr, ws.data_ptr<float>(), relu, cur_stream(x));
+  return {dx, dg, db, dz};
 }
 
 }  // namespace
@@ -293,8 +304,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches"), py::arg("momentum"), py::arg("eps"),
         py::arg("relu"));
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("residual"), py::arg("a"), py::arg("b"), py::arg("relu"));
-  m.def("bn_bwd", &bn_bwd, py::arg("grad_output"), py::arg("y"), py::arg("x"), py::arg("weight"), py::arg("mean"),
-        py::arg("invstd"), py::arg("relu"), py::arg("want_dres"), py::arg("want_dparams"));
+  m.def("bn_bwd", &bn_bwd, py::arg("grad_output"), py::arg("grad_output2"), py::arg("y"), py::arg("x"),
+        py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("relu"), py::arg("want_dz"),
+        py::arg("want_dparams"));
   m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
 
   py::class_<dpt::RcclComm, std::shared_ptr<dpt::RcclComm>>(m, "RcclComm")

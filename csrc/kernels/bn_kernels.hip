@@ -9,9 +9,10 @@
 //                     finalize  partials -> mean, invstd, a = g*invstd, b = beta - mean*a,
 //                               running stats (momentum, unbiased var), num_batches_tracked++
 //                     apply     y = relu(x*a + b [+ r])      read x [, r], write y
-//   backward:         stats     dz = dy * (y > 0);  s1 = sum dz, s2 = sum dz*(x - mean)
+//   backward:         stats     dz = (dy [+ dy2]) * (y > 0);  s1 = sum dz, s2 = sum dz*(x - mean)
+//                               [residual blocks: store dz - it IS the residual-path gradient]
 //                     finalize  dgamma = s2*invstd, dbeta = s1, dx coefficients k1,k2,k3
-//                     apply     dx = k1*dz + k2*(x - mean) + k3 [, dr = dz]
+//                     apply     dx = k1*dz + k2*(x - mean) + k3   (dz recomputed or read back)
 //
 // Layout: a channels_last activation is a row-major [M = N*H*W, C] matrix.  Threads are
 // "channel-stationary": with 256 threads and C/8 threads per row, each thread owns one
@@ -255,15 +256,21 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(const void* __rest
   }
 }
 
-// ---- backward statistics: s1 = sum dz, s2 = sum dz*(x-mean), dz = dy*(y>0) --------------------
-template <typename IO, bool RELU>
+// ---- backward statistics: s1 = sum dz, s2 = sum dz*(x-mean), dz = (dy [+ dy2]) * (y > 0) ------
+// TWO: the output had two consumers (conv path + identity path of the next residual block,
+// see ops/bn.py "pair" outputs); their gradients arrive separately and are summed here
+// instead of in an autograd add kernel.  WDZ: also store dz (it is the residual-path
+// gradient dres, and the apply pass then reads dz instead of dy, dy2 and y).
+template <typename IO, bool RELU, bool TWO, bool WDZ>
 __global__ __launch_bounds__(kBlock) void bn_bwd_stats_kernel(const void* __restrict__ dy,
+                                                              const void* __restrict__ dy2,
                                                               const void* __restrict__ y,
                                                               const void* __restrict__ x,
                                                               const float* __restrict__ mean, int64_t M,
                                                               int C, int64_t rows_per_chunk, int chunks,
                                                               float* __restrict__ p1,
-                                                              float* __restrict__ p2) {
+                                                              float* __restrict__ p2,
+                                                              void* __restrict__ dz_out) {
   __shared__ float lds[2 * kBlock * 8];
   const int tpr = C >> 3, rpi = kBlock / tpr;
   const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
@@ -274,36 +281,47 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_stats_kernel(const void* __rest
   const int64_t row1 = min(row0 + rows_per_chunk, M);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int64_t r = row0 + rr;
-  for (; r + rpi < row1; r += 2 * rpi) {  // two rows x three tensors in flight per thread
-    float g[2][8], xv[2][8];
+  for (; r + rpi < row1; r += 2 * rpi) {  // two rows x (3 or 4) tensors in flight per thread
+    float g[2][8], g2[2][8], xv[2][8];
     bool m[2][8];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      IO::load8(dy, (r + u * rpi) * C + cg * 8, g[u]);
-      IO::load8(x, (r + u * rpi) * C + cg * 8, xv[u]);
-      if (RELU) IO::pos8(y, (r + u * rpi) * C + cg * 8, m[u]);
+      const int64_t off = (r + u * rpi) * C + cg * 8;
+      IO::load8(dy, off, g[u]);
+      if (TWO) IO::load8(dy2, off, g2[u]);
+      IO::load8(x, off, xv[u]);
+      if (RELU) IO::pos8(y, off, m[u]);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        float dz = (!RELU || m[u][k]) ? g[u][k] : 0.0f;
+        float gk = TWO ? g[u][k] + g2[u][k] : g[u][k];
+        float dz = (!RELU || m[u][k]) ? gk : 0.0f;
+        g[u][k] = dz;
         s[k] += dz;
         q[k] += dz * (xv[u][k] - mu[k]);
       }
+      if (WDZ) IO::store8(dz_out, (r + u * rpi) * C + cg * 8, g[u]);
+    }
   }
   for (; r < row1; r += rpi) {
-    float g[8], xv[8];
+    const int64_t off = r * C + cg * 8;
+    float g[8], g2[8], xv[8];
     bool m[8];
-    IO::load8(dy, r * C + cg * 8, g);
-    IO::load8(x, r * C + cg * 8, xv);
-    if (RELU) IO::pos8(y, r * C + cg * 8, m);
+    IO::load8(dy, off, g);
+    if (TWO) IO::load8(dy2, off, g2);
+    IO::load8(x, off, xv);
+    if (RELU) IO::pos8(y, off, m);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float dz = (!RELU || m[k]) ? g[k] : 0.0f;
+      float gk = TWO ? g[k] + g2[k] : g[k];
+      float dz = (!RELU || m[k]) ? gk : 0.0f;
+      g[k] = dz;
       s[k] += dz;
       q[k] += dz * (xv[k] - mu[k]);
     }
+    if (WDZ) IO::store8(dz_out, off, g);
   }
   float* ls = lds;
   float* lq = lds + kBlock * 8;
@@ -342,7 +360,8 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(
   k3[c] = (float)(-a * s1 / (double)M);
 }
 
-template <typename IO, bool RELU, bool RES>
+// dx = k1*dz + k2*(x - mean) + k3, dz = dy*(y>0) recomputed (RELU) or read back (FROM_DZ).
+template <typename IO, bool RELU, bool FROM_DZ>
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const void* __restrict__ dy,
                                                               const void* __restrict__ y,
                                                               const void* __restrict__ x,
@@ -350,7 +369,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const void* __rest
                                                               const float* __restrict__ k1,
                                                               const float* __restrict__ k2,
                                                               const float* __restrict__ k3, void* dx,
-                                                              void* dres, int64_t M, int C) {
+                                                              int64_t M, int C) {
   const int tpr = C >> 3, rpi = kBlock / tpr;
   const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
   float mu[8], c1[8], c2[8], c3[8];
@@ -367,15 +386,13 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const void* __rest
     bool m[8];
     IO::load8(dy, r * C + cg * 8, g);
     IO::load8(x, r * C + cg * 8, xv);
-    if (RELU) IO::pos8(y, r * C + cg * 8, m);
+    if (RELU && !FROM_DZ) IO::pos8(y, r * C + cg * 8, m);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float dz = (!RELU || m[k]) ? g[k] : 0.0f;
-      g[k] = dz;
+      float dz = (FROM_DZ || !RELU || m[k]) ? g[k] : 0.0f;
       o[k] = c1[k] * dz + c2[k] * (xv[k] - mu[k]) + c3[k];
     }
     IO::store8(dx, r * C + cg * 8, o);
-    if (RES) IO::store8(dres, r * C + cg * 8, g);
   }
 }
 
@@ -448,25 +465,34 @@ void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t
 }
 
 template <typename IO>
-static void bwd_dispatch(bool relu, bool res, const void* dy, const void* y, const void* x, const float* mean,
-                         int64_t M, int C, const BnGeometry& g, float* p1, float* p2, const float* gamma,
-                         const float* invstd, float* dgamma, float* dbeta, float* k1, float* k2, float* k3,
-                         void* dx, void* dres, hipStream_t s) {
-  dim3 bl(kBlock);
-  if (relu) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true>), dim3(g.chunks), bl, 0, s, dy, y, x, mean, M, C, g.rows_per_chunk, g.chunks, p1, p2);
-  else hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false>), dim3(g.chunks), bl, 0, s, dy, y, x, mean, M, C, g.rows_per_chunk, g.chunks, p1, p2);
+static void bwd_dispatch(bool relu, const void* dy, const void* dy2, const void* y, const void* x,
+                         const float* mean, int64_t M, int C, const BnGeometry& g, float* p1, float* p2,
+                         const float* gamma, const float* invstd, float* dgamma, float* dbeta, float* k1,
+                         float* k2, float* k3, void* dx, void* dz, hipStream_t s) {
+  dim3 bl(kBlock), gs(g.chunks);
+  const int64_t rpc = g.rows_per_chunk;
+  if (dz != nullptr) {  // dz written by the stats pass, read back by the apply pass
+    if (relu && dy2) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true, true, true>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+    else if (relu) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true, false, true>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+    else if (dy2) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false, true, true>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+    else hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false, false, true>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+  } else {
+    if (relu) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true, false, false>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+    else hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false, false, false>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+  }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p2, g.chunks, C, M, gamma,
                      invstd, dgamma, dbeta, k1, k2, k3);
   dim3 ga(g.apply_blocks * 2 > 4 * kMaxBlocks ? 4 * kMaxBlocks : g.apply_blocks * 2);
-  if (relu && res) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, true>), ga, bl, 0, s, dy, y, x, mean, k1, k2, k3, dx, dres, M, C);
-  else if (relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false>), ga, bl, 0, s, dy, y, x, mean, k1, k2, k3, dx, dres, M, C);
-  else if (res) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, true>), ga, bl, 0, s, dy, y, x, mean, k1, k2, k3, dx, dres, M, C);
-  else hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, false>), ga, bl, 0, s, dy, y, x, mean, k1, k2, k3, dx, dres, M, C);
+  if (dz != nullptr) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, true>), ga, bl, 0, s, dz, y, x, mean, k1, k2, k3, dx, M, C);
+  else if (relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false>), ga, bl, 0, s, dy, y, x, mean, k1, k2, k3, dx, M, C);
+  else hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, false>), ga, bl, 0, s, dy, y, x, mean, k1, k2, k3, dx, M, C);
 }
 
-void launch_bn_bwd(int dtype, const void* dy, const void* y, const void* x, int64_t M, int64_t C,
-                   const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
-                   void* dx, void* dres, float* workspace, bool relu, hipStream_t s) {
+// dz: if non-null, receives dz = (dy [+ dy2]) * relu_mask (the residual-path gradient);
+// required when dy2 is given.
+void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, const void* x, int64_t M,
+                   int64_t C, const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                   float* dbeta, void* dx, void* dz, float* workspace, bool relu, hipStream_t s) {
   BnGeometry g = bn_geometry(M, C);
   float* p1 = workspace;
   float* p2 = p1 + (int64_t)C * g.chunks;
@@ -474,9 +500,9 @@ void launch_bn_bwd(int dtype, const void* dy, const void* y, const void* x, int6
   float* k2 = k1 + C;
   float* k3 = k2 + C;
   switch (dtype) {
-    case 0: bwd_dispatch<F32>(relu, dres != nullptr, dy, y, x, mean, M, (int)C, g, p1, p2, gamma, invstd, dgamma, dbeta, k1, k2, k3, dx, dres, s); break;
-    case 1: bwd_dispatch<BF16>(relu, dres != nullptr, dy, y, x, mean, M, (int)C, g, p1, p2, gamma, invstd, dgamma, dbeta, k1, k2, k3, dx, dres, s); break;
-    default: bwd_dispatch<F16>(relu, dres != nullptr, dy, y, x, mean, M, (int)C, g, p1, p2, gamma, invstd, dgamma, dbeta, k1, k2, k3, dx, dres, s); break;
+    case 0: bwd_dispatch<F32>(relu, dy, dy2, y, x, mean, M, (int)C, g, p1, p2, gamma, invstd, dgamma, dbeta, k1, k2, k3, dx, dz, s); break;
+    case 1: bwd_dispatch<BF16>(relu, dy, dy2, y, x, mean, M, (int)C, g, p1, p2, gamma, invstd, dgamma, dbeta, k1, k2, k3, dx, dz, s); break;
+    default: bwd_dispatch<F16>(relu, dy, dy2, y, x, mean, M, (int)C, g, p1, p2, gamma, invstd, dgamma, dbeta, k1, k2, k3, dx, dz, s); break;
   }
 }
 

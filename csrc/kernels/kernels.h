@@ -54,8 +54,8 @@ void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int
                          float* workspace, bool relu, hipStream_t s);
 void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                      const float* coef_a, const float* coef_b, bool relu, hipStream_t s);
-void launch_bn_bwd(int dtype, const void* dy, const void* y, const void* x, int64_t M, int64_t C,
-                   const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
-                   void* dx, void* dres, float* workspace, bool relu, hipStream_t s);
+void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, const void* x, int64_t M,
+                   int64_t C, const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                   float* dbeta, void* dx, void* dz, float* workspace, bool relu, hipStream_t s);
 
 }  // namespace dpt

@@ -29,13 +29,14 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
             return False
         return fused_bn.bn_act_supported(x, self.num_features)
 
-    def act(self, x: torch.Tensor, relu: bool, residual: Optional[torch.Tensor]) -> torch.Tensor:
+    def act(self, x: torch.Tensor, relu: bool, residual: Optional[torch.Tensor], pair: bool = False):
         if self.training:
             return fused_bn.bn_act_train(x, residual, self.weight, self.bias, self.running_mean,
                                          self.running_var, self.num_batches_tracked, self.momentum,
-                                         self.eps, relu)
-        return fused_bn.bn_act_eval(x, residual, self.weight, self.bias, self.running_mean,
-                                    self.running_var, self.eps, relu)
+                                         self.eps, relu, pair)
+        y = fused_bn.bn_act_eval(x, residual, self.weight, self.bias, self.running_mean,
+                                 self.running_var, self.eps, relu)
+        return (y, y) if pair else y
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.can_fuse(x):
@@ -51,6 +52,24 @@ def bn_act(bn: nn.Module, x: torch.Tensor, relu: bool = True,
     if residual is not None:
         out += residual
     return F.relu(out, inplace=True) if relu else out
+
+
+def bn_act_block_out(bn: nn.Module, x: torch.Tensor, residual: torch.Tensor):
+    """Residual-block tail ``relu(bn(x) + residual)``.
+
+    With a fused BN it returns ``(y_conv, y_identity)``: two aliases of the output whose
+    gradients reach the fused backward separately (see ops/bn.py ``_BNActTrainPair``); the
+    next block feeds the first to its conv path and the second to its identity path.
+    Otherwise it returns the plain tensor.
+    """
+    if isinstance(bn, FusedBatchNorm2d) and bn.can_fuse(x):
+        return bn.act(x, True, residual, pair=True)
+    return bn_act(bn, x, True, residual)
+
+
+def split_block_input(x):
+    """(conv-path input, identity-path input) of a residual block."""
+    return x if isinstance(x, tuple) else (x, x)
 
 
 def fuse_batchnorm(model: nn.Module) -> int:

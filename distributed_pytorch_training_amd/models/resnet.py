@@ -25,7 +25,7 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
-from .layers import bn_act
+from .layers import bn_act, bn_act_block_out, split_block_input
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -50,10 +50,11 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
-        out = bn_act(self.bn1, self.conv1(x))
-        return bn_act(self.bn2, self.conv2(out), residual=identity)
+    def forward(self, x):
+        xc, xi = split_block_input(x)
+        identity = xi if self.downsample is None else self.downsample(xi)
+        out = bn_act(self.bn1, self.conv1(xc))
+        return bn_act_block_out(self.bn2, self.conv2(out), identity)
 
 
 class Bottleneck(nn.Module):
@@ -74,11 +75,12 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
-        out = bn_act(self.bn1, self.conv1(x))
+    def forward(self, x):
+        xc, xi = split_block_input(x)
+        identity = xi if self.downsample is None else self.downsample(xi)
+        out = bn_act(self.bn1, self.conv1(xc))
         out = bn_act(self.bn2, self.conv2(out))
-        return bn_act(self.bn3, self.conv3(out), residual=identity)
+        return bn_act_block_out(self.bn3, self.conv3(out), identity)
 
 
 class ResNet(nn.Module):
@@ -128,6 +130,8 @@ class ResNet(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = self.maxpool(bn_act(self.bn1, self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        if isinstance(x, tuple):  # fused block tails hand (conv-path, identity-path) aliases along
+            x = x[0]
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 

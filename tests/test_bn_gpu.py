@@ -89,25 +89,66 @@ def test_fused_bn_large_batch_statistics(cuda):
     assert abs(yf.mean().item()) < 2e-2 and abs(yf.std().item() - 1) < 2e-2
 
 
-def test_resnet_fused_matches_unfused_step(cuda):
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("batch,size", [(8, 64), (32, 64)])
+def test_resnet_fused_matches_unfused(cuda, batch, size):
+    """Whole-network check: fp32 fused == fp32 unfused tightly; in bf16 autocast the fused
+    network's deviation from the fp32 result is no worse than the unfused network's."""
     import copy
 
     from distributed_pytorch_training_amd.models import build_model
     from distributed_pytorch_training_amd.models.layers import fuse_batchnorm
 
     torch.manual_seed(0)
-    ref = build_model("resnet50", 100, cuda, image_size=64, channels_last=True)
+    ref = build_model("resnet50", 100, cuda, image_size=size, channels_last=True)
     fused = copy.deepcopy(ref)
     assert fuse_batchnorm(fused) == 53
-    x = torch.randn(8, 3, 64, 64, device=cuda).contiguous(memory_format=torch.channels_last)
-    with torch.autocast("cuda", dtype=torch.bfloat16):
-        a = ref(x)
-        b = fused(x)
-    torch.testing.assert_close(b.float(), a.float(), rtol=5e-2, atol=5e-2)
-    a.float().sum().backward()
-    b.float().sum().backward()
+    x = torch.randn(batch, 3, size, size, device=cuda).contiguous(memory_format=torch.channels_last)
+    torch.backends.cudnn.deterministic = True
+    a32 = ref(x)
+    b32 = fused(x)
+    if isinstance(b32, tuple):
+        b32 = b32[0]
+    assert _rel(b32, a32) < 1e-3, _rel(b32, a32)
+    a32.sum().backward()
+    b32.sum().backward()
     for (n, p), q in zip(ref.named_parameters(), fused.parameters()):
-        scale = p.grad.abs().max().item() + 1e-6
-        assert (p.grad - q.grad).abs().max().item() / scale < 0.1, n
-    for (n, p), q in zip(ref.named_buffers(), fused.buffers()):
-        torch.testing.assert_close(p.float(), q.float(), rtol=1e-2, atol=1e-2, msg=n)
+        assert _rel(q.grad, p.grad) < 2e-2, (n, _rel(q.grad, p.grad))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        a16 = ref(x)
+        b16 = fused(x)
+    err_unfused, err_fused = _rel(a16, a32), _rel(b16, a32)
+    assert err_fused < max(3 * err_unfused, 0.05), (err_fused, err_unfused)
+
+
+@pytest.mark.parametrize("use", ["both", "first", "second"])
+def test_pair_outputs_sum_gradients(cuda, use):
+    """Block-tail op with two aliased outputs: gradients of both consumers are summed in-kernel."""
+    from distributed_pytorch_training_amd.models.layers import bn_act_block_out
+
+    shape = (8, 256, 7, 7)
+    x = _mk(shape, torch.bfloat16, cuda, 11).requires_grad_()
+    r = _mk(shape, torch.bfloat16, cuda, 12).requires_grad_()
+    bn = FusedBatchNorm2d(256).to(cuda)
+    xr, rr = x.detach().float().requires_grad_(), r.detach().float().requires_grad_()
+    w = bn.weight.detach().clone().requires_grad_()
+    b = bn.bias.detach().clone().requires_grad_()
+    y1, y2 = bn_act_block_out(bn, x, r)
+    assert y1.data_ptr() == y2.data_ptr()
+    g1, g2 = _mk(shape, torch.bfloat16, cuda, 13), _mk(shape, torch.bfloat16, cuda, 14)
+    loss = 0
+    if use in ("both", "first"):
+        loss = loss + (y1.float() * g1.float()).sum()
+    if use in ("both", "second"):
+        loss = loss + (y2.float() * g2.float()).sum()
+    loss.backward()
+    zr = reference_bn_act(xr, rr, w, b, bn.running_mean.clone(), bn.running_var.clone(), True, 0.1, bn.eps, False)
+    yr = zr * (y1.detach() > 0).float()
+    gsum = (g1.float() if use != "second" else 0) + (g2.float() if use != "first" else 0)
+    (yr * gsum).sum().backward()
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=8e-2, atol=8e-2)
+    torch.testing.assert_close(r.grad.float(), rr.grad, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(bn.bias.grad, b.grad, rtol=2e-2, atol=0.5)
