@@ -281,6 +281,35 @@ std::vector<Tensor> bn_bwd(Tensor dy, c10::optional<Tensor> dy2, c10::optional<T
   return {dx, dg, db, dz};
 }
 
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t stride, int64_t pad) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "maxpool: x must be a 4-D channels_last GPU tensor");
+  const int64_t B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && k >= 1 && k * k <= 255 && stride >= 1 && pad >= 0 && pad <= k / 2, "maxpool: bad config");
+  const int64_t Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  auto y = at::empty({B, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto idx = at::empty({B, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(x.device().index());
+  dpt::launch_maxpool_fwd(bn_dtype(x), x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), B, (int)H, (int)W,
+                          (int)C, (int)Ho, (int)Wo, (int)k, (int)stride, (int)pad, cur_stream(x));
+  return {y, idx};
+}
+
+Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64_t stride, int64_t pad) {
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "maxpool_bwd: grad must be channels_last");
+  TORCH_CHECK(idx.sizes() == dy.sizes() && idx.scalar_type() == at::kByte &&
+                  idx.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool_bwd: idx mismatch");
+  const int64_t B = dy.size(0), C = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  TORCH_CHECK(C % 8 == 0 && Ho == (H + 2 * pad - k) / stride + 1 && Wo == (W + 2 * pad - k) / stride + 1,
+              "maxpool_bwd: geometry mismatch");
+  auto dx = at::empty({B, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(dy.device().index());
+  dpt::launch_maxpool_bwd(bn_dtype(dy), dy.data_ptr(), idx.data_ptr<uint8_t>(), dx.data_ptr(), B, (int)H, (int)W,
+                          (int)C, (int)Ho, (int)Wo, (int)k, (int)stride, (int)pad, cur_stream(dy));
+  return dx;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -307,6 +336,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &bn_bwd, py::arg("grad_output"), py::arg("grad_output2"), py::arg("y"), py::arg("x"),
         py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("relu"), py::arg("want_dz"),
         py::arg("want_dparams"));
+  m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("stride"), py::arg("pad"));
+  m.def("maxpool_bwd", &maxpool_bwd, py::arg("grad_output"), py::arg("idx"), py::arg("H"), py::arg("W"),
+        py::arg("k"), py::arg("stride"), py::arg("pad"));
   m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
 
   py::class_<dpt::RcclComm, std::shared_ptr<dpt::RcclComm>>(m, "RcclComm")

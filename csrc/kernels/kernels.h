@@ -58,4 +58,10 @@ void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, co
                    int64_t C, const float* gamma, const float* mean, const float* invstd, float* dgamma,
                    float* dbeta, void* dx, void* dz, float* workspace, bool relu, hipStream_t s);
 
+// pool_kernels.hip  (channels_last [B,H,W,C], C % 8 == 0; idx = window-local uint8 argmax)
+void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t B, int H, int W, int C, int Ho,
+                        int Wo, int K, int S, int P, hipStream_t s);
+void launch_maxpool_bwd(int dtype, const void* dy, const uint8_t* idx, void* dx, int64_t B, int H, int W, int C,
+                        int Ho, int Wo, int K, int S, int P, hipStream_t s);
+
 }  // namespace dpt

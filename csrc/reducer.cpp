@@ -5,6 +5,7 @@
 #include <torch/csrc/autograd/utils/lambda_post_hook.h>
 #include <torch/csrc/autograd/variable.h>
 
+#include <cstdlib>
 #include <stdexcept>
 
 #include "kernels/kernels.h"
@@ -181,7 +182,13 @@ void Reducer::launch_bucket(int64_t b) {
   float* g = flat_grad_.data_ptr<float>() + off;
   const float* scale = (scale_.defined() && scale_.numel() > 0) ? scale_.data_ptr<float>() : nullptr;
   float* finf = check_inf_ ? found_inf_.data_ptr<float>() : nullptr;
-  if (comm_->world_size() > 1) {
+  // DPT_FORCE_COLLECTIVES=1 runs the RCCL path even at world size 1 (single-GPU tests of the
+  // collective + wire-format code path; a 1-rank all-reduce is an identity).
+  static const bool force = [] {
+    const char* e = std::getenv("DPT_FORCE_COLLECTIVES");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (comm_->world_size() > 1 || force) {
     if (wire_ == 1) {
       uint16_t* w = reinterpret_cast<uint16_t*>(wire_buf_.data_ptr()) + off;
       launch_pack_bf16(g, w, n, cs);

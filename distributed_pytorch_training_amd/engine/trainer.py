@@ -89,8 +89,8 @@ class Trainer:
         args = self.args
         if (getattr(args, "fused_bn", True) and self.device.type == "cuda"
                 and getattr(args, "channels_last", False)):
-            from ..models.layers import fuse_batchnorm
-            fuse_batchnorm(model)
+            from ..models.layers import fuse_native_layers
+            fuse_native_layers(model)
         params_in_order = [p for p in model.parameters() if p.requires_grad]
         self.scaler = DeviceGradScaler(self.device, enabled=self.amp)
         self.ddp = NativeDDP(model, rank=self.rank, world_size=self.world_size, device=self.device,

@@ -17,6 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import bn as fused_bn
+from ..ops import pool as fused_pool
 
 
 class FusedBatchNorm2d(nn.BatchNorm2d):
@@ -70,6 +71,33 @@ def bn_act_block_out(bn: nn.Module, x: torch.Tensor, residual: torch.Tensor):
 def split_block_input(x):
     """(conv-path input, identity-path input) of a residual block."""
     return x if isinstance(x, tuple) else (x, x)
+
+
+class FusedMaxPool2d(nn.MaxPool2d):
+    """``nn.MaxPool2d`` that runs the gfx950 channels-last kernels when it can."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not self.return_indices and fused_pool.maxpool_supported(
+                x, self.kernel_size, self.stride, self.padding, self.dilation, self.ceil_mode):
+            as_int = lambda v: v if isinstance(v, int) else v[0]
+            return fused_pool.max_pool2d_nhwc(x, as_int(self.kernel_size), as_int(self.stride),
+                                              as_int(self.padding))
+        return super().forward(x)
+
+
+def fuse_native_layers(model: nn.Module) -> int:
+    """Install the gfx950 fused layers: BatchNorm2d -> FusedBatchNorm2d (fused with ReLU /
+    residual add by the model's ``bn_act`` calls) and MaxPool2d -> FusedMaxPool2d.  Modules
+    keep their parameters/buffers, so state dicts and checkpoints are unchanged."""
+    n = fuse_batchnorm(model)
+    for parent in model.modules():
+        for name, child in list(parent.named_children()):
+            if type(child) is nn.MaxPool2d:
+                new = FusedMaxPool2d.__new__(FusedMaxPool2d)
+                new.__dict__ = child.__dict__
+                setattr(parent, name, new)
+                n += 1
+    return n
 
 
 def fuse_batchnorm(model: nn.Module) -> int:

@@ -88,3 +88,51 @@ def test_reducer_single_rank_checks_buckets(cuda):
     (model(x).sum() * float("inf")).backward()
     torch.cuda.synchronize()
     assert fi.item() == 1.0
+
+
+@pytest.mark.parametrize("wire", [0, 1])
+def test_reducer_rccl_path_single_rank(cuda, wire, monkeypatch):
+    """Exercise ncclAllReduce (+ bf16 pack/unpack) through the C++ reducer on one GPU: a
+    1-rank all-reduce is an identity, so gradients must come out unchanged (fp32 wire) or
+    bf16-rounded (bf16 wire)."""
+    import subprocess
+    import sys
+    import textwrap
+
+    code = textwrap.dedent(f"""
+        import torch
+        from distributed_pytorch_training_amd import ops
+        from distributed_pytorch_training_amd.parallel.bucketing import plan_for_arena
+        from distributed_pytorch_training_amd.parallel.comm import make_comm
+        from distributed_pytorch_training_amd.parallel.flat import FlatArena
+        dev = torch.device("cuda:0")
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(), torch.nn.Linear(256, 10)).to(dev)
+        ref = [p.detach().clone() for p in model.parameters()]
+        x = torch.randn(8, 64, device=dev)
+        model(x).sum().backward()
+        want = [p.grad.clone() for p in model.parameters()]
+        for p in model.parameters():
+            p.grad = None
+        arena = FlatArena(list(reversed(list(model.parameters()))))
+        plan = plan_for_arena(arena, bucket_cap_mb=0.02, first_bucket_mb=0.001)
+        comm = make_comm(dev, 0, 1)
+        fi = torch.zeros(1, device=dev)
+        wire_buf = torch.zeros(arena.numel, dtype=torch.bfloat16, device=dev) if {wire} else torch.empty(0)
+        red = ops.native().Reducer(arena.params, arena.grad_views, arena.grad_flat, plan.offsets, plan.numels,
+                                   plan.param_bucket, comm, None, {wire}, wire_buf, fi, torch.empty(0), 1.0, True, False)
+        red.prepare_for_backward()
+        model(x).sum().backward()
+        torch.cuda.synchronize()
+        for p, w in zip(model.parameters(), want):
+            exp = w.to(torch.bfloat16).float() if {wire} else w
+            assert torch.equal(p.grad, exp), (p.shape, (p.grad - exp).abs().max().item())
+        t = torch.arange(16, dtype=torch.float32, device=dev)
+        comm.all_reduce(t, True)
+        torch.cuda.synchronize()
+        assert torch.equal(t, torch.arange(16, dtype=torch.float32, device=dev))
+        print("ok")
+    """)
+    env = dict(__import__("os").environ, DPT_FORCE_COLLECTIVES="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
