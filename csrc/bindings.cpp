@@ -380,16 +380,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<dpt::Reducer, std::shared_ptr<dpt::Reducer>>(m, "Reducer")
       .def(py::init<std::vector<Tensor>, std::vector<Tensor>, Tensor, std::vector<int64_t>, std::vector<int64_t>,
                     std::vector<int64_t>, std::shared_ptr<dpt::RcclComm>, py::object, int, Tensor, Tensor, Tensor,
-                    double, bool, bool>(),
+                    double, bool, bool, bool>(),
            py::arg("params"), py::arg("grad_views"), py::arg("flat_grad"), py::arg("bucket_offsets"),
            py::arg("bucket_numels"), py::arg("param_bucket"), py::arg("comm"), py::arg("py_allreduce"),
            py::arg("wire"), py::arg("wire_buf"), py::arg("found_inf"), py::arg("scale"), py::arg("host_factor"),
-           py::arg("check_inf"), py::arg("profile"))
+           py::arg("check_inf"), py::arg("profile"), py::arg("steal_grads") = false)
       .def("prepare_for_backward", &dpt::Reducer::prepare_for_backward)
       .def("mark_ready", &dpt::Reducer::mark_ready)
       .def("finalize", &dpt::Reducer::finalize)
       .def("set_require_sync", &dpt::Reducer::set_require_sync)
       .def("set_check_inf", &dpt::Reducer::set_check_inf)
+      .def("set_accumulate", &dpt::Reducer::set_accumulate)
       .def_property_readonly("require_sync", &dpt::Reducer::require_sync)
       .def("ready_order", &dpt::Reducer::ready_order)
       .def_property_readonly("num_buckets", &dpt::Reducer::num_buckets)

@@ -64,4 +64,14 @@ void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t
 void launch_maxpool_bwd(int dtype, const void* dy, const uint8_t* idx, void* dx, int64_t B, int H, int W, int C,
                         int Ho, int Wo, int K, int S, int P, hipStream_t s);
 
+// gather_kernels.hip: up to kGatherMax tensors per launch (kernel-argument struct)
+constexpr int kGatherMax = 48;
+struct GatherBatch {
+  const float* src[kGatherMax];
+  float* dst[kGatherMax];
+  int64_t numel[kGatherMax];
+  int count;
+};
+void launch_gather(const GatherBatch& batch, bool accumulate, hipStream_t s);
+
 }  // namespace dpt

@@ -27,7 +27,7 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
                  std::vector<int64_t> bucket_numels, std::vector<int64_t> param_bucket,
                  std::shared_ptr<RcclComm> comm, py::object py_allreduce, int wire,
                  at::Tensor wire_buf, at::Tensor found_inf, at::Tensor scale, double host_factor,
-                 bool check_inf, bool profile)
+                 bool check_inf, bool profile, bool steal_grads)
     : params_(std::move(params)),
       grad_views_(std::move(grad_views)),
       flat_grad_(std::move(flat_grad)),
@@ -47,7 +47,8 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
   if (grad_views_.size() != P || param_bucket_.size() != P || bucket_numels_.size() != B)
     throw std::invalid_argument("Reducer: inconsistent parameter/bucket metadata");
   gpu_ = flat_grad_.is_cuda();
-  if (gpu_ && !comm_) throw std::invalid_argument("Reducer: GPU arena needs an RcclComm");
+  steal_ = steal_grads && gpu_;
+  // gpu_ && !comm_: local reducer (world size 1): gather + AMP check, no collectives.
   if (!gpu_ && py_allreduce_.is_none())
     throw std::invalid_argument("Reducer: CPU arena needs a Python all-reduce callback");
   if (gpu_ && wire_ == 1 && (!wire_buf_.defined() || wire_buf_.numel() < flat_grad_.numel()))
@@ -67,6 +68,11 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
   pending_ = bucket_size_;
   launched_.assign(B, 0);
   marked_.assign(P, 0);
+  stolen_.resize(P);
+  members_.assign(B, {});
+  for (size_t i = 0; i < P; ++i) members_[param_bucket_[i]].push_back((int64_t)i);
+  if (steal_ && flat_grad_.scalar_type() != at::kFloat)
+    throw std::invalid_argument("Reducer: steal mode needs a float32 arena");
 
   if (gpu_) {
     const unsigned flags = profile_ ? hipEventDefault : hipEventDisableTiming;
@@ -131,6 +137,11 @@ void Reducer::prepare_for_backward() {
   callback_queued_ = false;
   if (record_order_) ready_order_.clear();
   if (gpu_) caller_stream_ = c10::hip::getCurrentHIPStream(flat_grad_.device().index()).stream();
+  if (steal_) {
+    // Undefined .grad: AccumulateGrad steals the fresh gradient (no per-parameter kernel).
+    for (size_t i = 0; i < params_.size(); ++i) params_[i].mutable_grad().reset();
+    return;
+  }
   // Re-attach arena views if someone replaced or cleared .grad (e.g. zero_grad(set_to_none)).
   for (size_t i = 0; i < params_.size(); ++i) {
     const at::Tensor& g = params_[i].grad();
@@ -153,11 +164,13 @@ void Reducer::mark_ready(int64_t index) {
     if (gpu_ && profile_) DPT_HIP_OK(hipEventRecord(ev_first_, caller_stream_));
     torch::autograd::Engine::get_default_engine().queue_callback([this] { this->finalize(); });
   }
+  if (steal_) stolen_[index] = params_[index].grad();
   const int64_t b = param_bucket_[index];
   if (--pending_[b] == 0) {
     if (gpu_) {
       // The gradient was produced on this thread's current stream.
       hipStream_t producer = c10::hip::getCurrentHIPStream(flat_grad_.device().index()).stream();
+      if (steal_) gather_bucket(b, producer);
       DPT_HIP_OK(hipEventRecord(ev_ready_[b], producer));
     }
     launched_[b] = 1;  // "ready"; the launch itself happens in index order below
@@ -169,11 +182,51 @@ void Reducer::mark_ready(int64_t index) {
   }
 }
 
+// Move the stolen gradients of bucket b into the arena (one launch per <= kGatherMax
+// tensors).  Gradients whose layout differs from their arena view (rare: a non-dense or
+// differently-strided gradient) go through a strided copy instead; parameters that got no
+// gradient this backward have their region zeroed unless accumulating.
+void Reducer::gather_bucket(int64_t b, hipStream_t s) {
+  GatherBatch batch;
+  batch.count = 0;
+  for (int64_t i : members_[b]) {
+    at::Tensor& g = stolen_[i];
+    const at::Tensor& v = grad_views_[i];
+    if (!g.defined()) {
+      if (!accumulate_) DPT_HIP_OK(hipMemsetAsync(v.data_ptr<float>(), 0, v.numel() * sizeof(float), s));
+      continue;
+    }
+    const bool same = g.scalar_type() == at::kFloat && g.is_cuda() && g.strides() == v.strides() &&
+                      g.sizes() == v.sizes() && g.is_non_overlapping_and_dense();
+    if (!same) {
+      at::Tensor vv = v;  // strided fallback on the current stream
+      if (accumulate_) vv.add_(g);
+      else vv.copy_(g);
+      continue;
+    }
+    batch.src[batch.count] = g.data_ptr<float>();
+    batch.dst[batch.count] = v.data_ptr<float>();
+    batch.numel[batch.count] = v.numel();
+    if (++batch.count == kGatherMax) {
+      launch_gather(batch, accumulate_, s);
+      batch.count = 0;
+    }
+  }
+  launch_gather(batch, accumulate_, s);
+}
+
 void Reducer::launch_bucket(int64_t b) {
   const int64_t off = bucket_offsets_[b], n = bucket_numels_[b];
   if (!gpu_) {
     py::gil_scoped_acquire g;
     py_allreduce_(b, off, n);
+    return;
+  }
+  if (!comm_) {  // local reducer: the AMP check runs right behind the gather, same stream
+    const float* scale = (scale_.defined() && scale_.numel() > 0) ? scale_.data_ptr<float>() : nullptr;
+    hipStream_t producer = c10::hip::getCurrentHIPStream(flat_grad_.device().index()).stream();
+    if (check_inf_) launch_grad_check(flat_grad_.data_ptr<float>() + off, n, scale, host_factor_,
+                                      found_inf_.data_ptr<float>(), producer);
     return;
   }
   hipStream_t cs = comm_->stream();
@@ -210,8 +263,12 @@ void Reducer::finalize() {
   // still reduced, in order, so every rank issues the same collective sequence.
   if (gpu_) {
     hipStream_t producer = c10::hip::getCurrentHIPStream(flat_grad_.device().index()).stream();
-    for (size_t b = 0; b < launched_.size(); ++b)
-      if (launched_[b] == 0) DPT_HIP_OK(hipEventRecord(ev_ready_[b], producer));
+    for (size_t b = 0; b < launched_.size(); ++b) {
+      if (launched_[b] == 0) {
+        if (steal_) gather_bucket((int64_t)b, producer);
+        DPT_HIP_OK(hipEventRecord(ev_ready_[b], producer));
+      }
+    }
     if (profile_) DPT_HIP_OK(hipEventRecord(ev_bwd_end_, caller_stream_));
   }
   for (size_t b = 0; b < launched_.size(); ++b) {
@@ -221,17 +278,28 @@ void Reducer::finalize() {
     }
   }
   next_launch_ = (int64_t)launched_.size();
-  if (gpu_) {
+  if (gpu_ && comm_) {
     DPT_HIP_OK(hipEventRecord(ev_done_, comm_->stream()));
     DPT_HIP_OK(hipStreamWaitEvent(caller_stream_, ev_done_, 0));
+  } else if (gpu_ && profile_) {
+    DPT_HIP_OK(hipEventRecord(ev_done_, caller_stream_));
   }
+  if (steal_) {
+    // Hand the arena views back as .grad and drop the stolen tensors (their memory returns to
+    // the caching allocator stream-ordered behind the gather kernels).
+    for (size_t i = 0; i < params_.size(); ++i) {
+      params_[i].mutable_grad() = grad_views_[i];
+      stolen_[i].reset();
+    }
+  }
+  accumulate_ = false;
   if (record_order_ && !ready_order_.empty()) record_order_ = false;
   ++backward_count_;
 }
 
 std::vector<double> Reducer::bucket_times_ms() {
   std::vector<double> out;
-  if (!gpu_ || !profile_) return out;
+  if (!gpu_ || !profile_ || !comm_) return out;
   for (size_t b = 0; b < ev_start_.size(); ++b) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, ev_start_[b], ev_end_[b]) != hipSuccess) ms = -1.f;
@@ -244,7 +312,7 @@ std::vector<double> Reducer::step_times_ms() {
   // {first-grad-ready -> backward end, backward end -> comm done (exposed), first bucket
   //  start -> comm done (comm span)}
   std::vector<double> out;
-  if (!gpu_ || !profile_ || ev_start_.empty()) return out;
+  if (!gpu_ || !profile_ || ev_start_.empty() || !comm_) return out;
   float a = 0.f, b = 0.f, c = 0.f;
   hipEventElapsedTime(&a, ev_first_, ev_bwd_end_);
   hipEventElapsedTime(&b, ev_bwd_end_, ev_done_);

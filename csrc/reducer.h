@@ -16,6 +16,10 @@
 //     host synchronisation anywhere on the step;
 //   * the observed gradient-ready order of the first backward is recorded so the Python
 //     front-end can rebuild buckets in that order (torch DDP's iteration-2 rebuild).
+// Steal mode (GPU): .grad is cleared before backward so AccumulateGrad hands each fresh
+// gradient over without a kernel; a completed bucket is gathered into the arena with ONE
+// multi-tensor launch (gather_kernels.hip) instead of one accumulate launch per parameter.
+// With no communicator (world size 1) the reducer still runs locally: gather + AMP check.
 // Without a GPU (gloo/CPU runs) the same bookkeeping drives a Python all-reduce callback.
 #pragma once
 
@@ -39,7 +43,7 @@ class Reducer {
           std::vector<int64_t> bucket_offsets, std::vector<int64_t> bucket_numels,
           std::vector<int64_t> param_bucket, std::shared_ptr<RcclComm> comm,
           pybind11::object py_allreduce, int wire, at::Tensor wire_buf, at::Tensor found_inf,
-          at::Tensor scale, double host_factor, bool check_inf, bool profile);
+          at::Tensor scale, double host_factor, bool check_inf, bool profile, bool steal_grads);
   ~Reducer();
 
   void prepare_for_backward();
@@ -48,6 +52,8 @@ class Reducer {
   void set_require_sync(bool v) { require_sync_ = v; }
   bool require_sync() const { return require_sync_; }
   void set_check_inf(bool v) { check_inf_ = v; }
+  // Next synced backward adds into the arena (it holds no_sync micro-batch gradients).
+  void set_accumulate(bool v) { accumulate_ = v; }
   std::vector<int64_t> ready_order() const { return ready_order_; }
   int64_t num_buckets() const { return (int64_t)bucket_offsets_.size(); }
   int64_t backward_count() const { return backward_count_; }
@@ -58,6 +64,7 @@ class Reducer {
 
  private:
   void launch_bucket(int64_t b);
+  void gather_bucket(int64_t b, hipStream_t s);
 
   std::vector<at::Tensor> params_, grad_views_;
   at::Tensor flat_grad_, wire_buf_, found_inf_, scale_;
@@ -72,7 +79,9 @@ class Reducer {
   pybind11::object py_allreduce_;
   int wire_;
   float host_factor_;
-  bool check_inf_, profile_, gpu_;
+  bool check_inf_, profile_, gpu_, steal_ = false, accumulate_ = false;
+  std::vector<at::Tensor> stolen_;        // gradients autograd handed over (steal mode)
+  std::vector<std::vector<int64_t>> members_;
   bool require_sync_ = true;
   bool callback_queued_ = false;
   bool record_order_ = true;

@@ -55,6 +55,7 @@ class NativeDDP(nn.Module):
         self.rebuild_buckets = rebuild_buckets and world_size > 1
         self.require_backward_grad_sync = True
         self._sync_buffers_next = True
+        self._pending_accum = False
         self._rebuilt = False
         self.found_inf = found_inf if found_inf is not None else torch.zeros(1, device=self.device)
         self.scale = scale
@@ -92,10 +93,13 @@ class NativeDDP(nn.Module):
         if self.reducer is not None:
             self.reducer.remove_hooks()
             self.reducer = None
-        if self.world_size <= 1:
-            return
-        C = ops.native()  # the reducer is C++ on both the GPU and the gloo/CPU path
         gpu = self.device.type == "cuda"
+        if self.world_size <= 1 and not gpu:
+            return
+        # GPU: always a C++ reducer - with world size 1 it runs "local" (no communicator):
+        # it still gathers the stolen gradients into the arena with one launch per bucket
+        # and runs the AMP check per bucket.  CPU world size 1: autograd writes the arena.
+        C = ops.native()  # the reducer is C++ on both the GPU and the gloo/CPU path
         wire = 1 if self.grad_dtype == "bf16" else 0
         if wire and gpu:
             self._wire_buf = torch.zeros(self.arena.numel, dtype=torch.bfloat16, device=self.device)
@@ -105,7 +109,7 @@ class NativeDDP(nn.Module):
             list(self.arena.params), list(self.arena.grad_views), self.arena.grad_flat,
             self.plan.offsets, self.plan.numels, self.plan.param_bucket, self.comm, py_cb, wire,
             wire_buf, self.found_inf, self.scale if self.scale is not None else torch.empty(0),
-            1.0 / self.world_size, bool(self.check_inf), bool(self.profile))
+            1.0 / self.world_size, bool(self.check_inf), bool(self.profile), gpu)
 
     def _cpu_allreduce(self, b: int, off: int, n: int) -> None:
         """gloo path: called by the C++ reducer when bucket ``b`` is complete."""
@@ -138,6 +142,9 @@ class NativeDDP(nn.Module):
         out = self.module(*args, **kwargs)
         grad_on = torch.is_grad_enabled()
         if grad_on and self.reducer is not None and self.require_backward_grad_sync:
+            # after no_sync micro-batches the arena holds their gradients: add, don't overwrite
+            self.reducer.set_accumulate(self._pending_accum)
+            self._pending_accum = False
             self.reducer.prepare_for_backward()
         self._sync_buffers_next = grad_on and self.require_backward_grad_sync
         return out
@@ -146,6 +153,7 @@ class NativeDDP(nn.Module):
     def no_sync(self):
         old = self.require_backward_grad_sync
         self.require_backward_grad_sync = False
+        self._pending_accum = True
         if self.reducer is not None:
             self.reducer.set_require_sync(False)
         try:
@@ -194,7 +202,7 @@ class NativeDDP(nn.Module):
         return self.plan.sizes_mib(self.arena.param_flat.element_size()) if self.plan else []
 
     def comm_profile(self):
-        if self.reducer is None:
+        if self.reducer is None or self.comm is None:
             return None
         return {"bucket_ms": list(self.reducer.bucket_times_ms()),
                 "step_ms": list(self.reducer.step_times_ms())}

@@ -93,36 +93,41 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("batch,size", [(8, 64), (32, 64)])
+@pytest.mark.parametrize("batch,size", [(32, 64), (8, 64)])
 def test_resnet_fused_matches_unfused(cuda, batch, size):
-    """Whole-network check: fp32 fused == fp32 unfused tightly; in bf16 autocast the fused
-    network's deviation from the fp32 result is no worse than the unfused network's."""
+    """Whole network against an fp64 reference: the fused network's error (forward output and
+    every parameter gradient) must be of the same order as the stock MIOpen network's error.
+    (Small-batch BN backward is ill-conditioned, so fp32-vs-fp32 differences alone say little.)"""
     import copy
 
     from distributed_pytorch_training_amd.models import build_model
-    from distributed_pytorch_training_amd.models.layers import fuse_batchnorm
+    from distributed_pytorch_training_amd.models.layers import fuse_native_layers
 
     torch.manual_seed(0)
     ref = build_model("resnet50", 100, cuda, image_size=size, channels_last=True)
     fused = copy.deepcopy(ref)
-    assert fuse_batchnorm(fused) == 53
+    f64 = copy.deepcopy(ref).double()
+    assert fuse_native_layers(fused) == 54
     x = torch.randn(batch, 3, size, size, device=cuda).contiguous(memory_format=torch.channels_last)
     torch.backends.cudnn.deterministic = True
-    a32 = ref(x)
-    b32 = fused(x)
-    if isinstance(b32, tuple):
-        b32 = b32[0]
-    assert _rel(b32, a32) < 1e-3, _rel(b32, a32)
-    a32.sum().backward()
-    b32.sum().backward()
-    # ReLU-mask ties flip differently in the two arithmetic orders and the flips compound
-    # through 50 layers into the first layers' weight gradients: bound the median and the max.
-    errs = sorted(_rel(q.grad, p.grad) for p, q in zip(ref.parameters(), fused.parameters()))
-    assert errs[len(errs) // 2] < 5e-3 and errs[-1] < 0.1, (errs[len(errs) // 2], errs[-1])
+    outs = []
+    for m, xx in ((f64, x.double()), (ref, x), (fused, x)):
+        y = m(xx)
+        y = y[0] if isinstance(y, tuple) else y
+        y.sum().backward()
+        outs.append(y)
+    e_ref, e_fused = _rel(outs[1], outs[0]), _rel(outs[2], outs[0])
+    assert e_fused < max(3 * e_ref, 1e-5), (e_fused, e_ref)
+    gr = [_rel(p.grad, q.grad) for p, q in zip(ref.parameters(), f64.parameters())]
+    gf = [_rel(p.grad, q.grad) for p, q in zip(fused.parameters(), f64.parameters())]
+    med = lambda v: sorted(v)[len(v) // 2]
+    assert med(gf) < max(3 * med(gr), 1e-4), (med(gf), med(gr))
+    assert max(gf) < max(3 * max(gr), 1e-3), (max(gf), max(gr))
     with torch.autocast("cuda", dtype=torch.bfloat16):
         a16 = ref(x)
         b16 = fused(x)
-    err_unfused, err_fused = _rel(a16, a32), _rel(b16, a32)
+    b16 = b16[0] if isinstance(b16, tuple) else b16
+    err_unfused, err_fused = _rel(a16, outs[0]), _rel(b16, outs[0])
     assert err_fused < max(3 * err_unfused, 0.05), (err_fused, err_unfused)
 
 
