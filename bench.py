@@ -162,6 +162,8 @@ def main(argv=None) -> int:
                 f.write(line + "\n")
     if ws > 1:
         dist.barrier()
+    trainer.close()
+    if ws > 1:
         dist.destroy_process_group()
     return 0
 

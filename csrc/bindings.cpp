@@ -373,6 +373,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.broadcast(t.data_ptr(), (size_t)t.numel(), w, root, cur_stream(t));
            }, py::arg("tensor"), py::arg("root") = 0)
       .def("abort", &dpt::RcclComm::abort)
+      .def("destroy", &dpt::RcclComm::destroy)
       .def_property_readonly("rank", &dpt::RcclComm::rank)
       .def_property_readonly("world_size", &dpt::RcclComm::world_size)
       .def_property_readonly("device", &dpt::RcclComm::device);

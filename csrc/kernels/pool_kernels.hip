@@ -10,6 +10,10 @@
 //   backward: gather, no atomics - one thread per (input pixel, 8-channel group) visits the
 //             <= ceil(K/S)^2 windows covering it and sums the gradients of those whose argmax
 //             points at it; every input gradient element is written exactly once.
+// Note: an earlier forward with a loop-carried "first in-bounds element" flag returned the
+// first window element instead of the max for the fp32 instantiation on gfx950 (bf16 was
+// right); the analytic clipped window seeded with -inf below is what tests/test_bn_gpu.py
+// verifies for every dtype.
 #include "common.h"
 #include "kernels.h"
 
@@ -64,27 +68,28 @@ __global__ __launch_bounds__(kBlock) void maxpool_fwd_kernel(const void* __restr
   pix /= Wo;
   const int oy = (int)(pix % Ho);
   const int64_t b = pix / Ho;
+  // Window clipped to the image; the first in-bounds position seeds the argmax (ATen keeps
+  // it when every value is -inf), the running max starts at -inf.
+  const int ky0 = max(0, P - oy * S), ky1 = min(K, H + P - oy * S);
+  const int kx0 = max(0, P - ox * S), kx1 = min(K, W + P - ox * S);
   float best[8];
-  uint8_t arg[8];
+  int arg[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { best[k] = -__builtin_inff(); arg[k] = 0; }
-  bool first = true;
-  for (int ky = 0; ky < K; ++ky) {
+  for (int k = 0; k < 8; ++k) { best[k] = -__builtin_inff(); arg[k] = ky0 * K + kx0; }
+  for (int ky = ky0; ky < ky1; ++ky) {
     const int iy = oy * S - P + ky;
-    if (iy < 0 || iy >= H) continue;
-    for (int kx = 0; kx < K; ++kx) {
+    for (int kx = kx0; kx < kx1; ++kx) {
       const int ix = ox * S - P + kx;
-      if (ix < 0 || ix >= W) continue;
       float v[8];
       pool_load8(DT, x, ((b * H + iy) * W + ix) * C + cg * 8, v);
-      const uint8_t pos = (uint8_t)(ky * K + kx);
+      const int pos = ky * K + kx;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const bool bn = best[k] != best[k];
-        const bool take = first || (!bn && (v[k] > best[k] || v[k] != v[k]));
-        if (take) { best[k] = v[k]; arg[k] = pos; }
+        // strictly greater (first max wins), and a NaN wins unless one is already held
+        const bool take = (v[k] > best[k]) || (v[k] != v[k] && best[k] == best[k]);
+        best[k] = take ? v[k] : best[k];
+        arg[k] = take ? pos : arg[k];
       }
-      first = false;
     }
   }
   const int64_t o = ((b * Ho + oy) * Wo + ox) * C + cg * 8;

@@ -52,19 +52,26 @@ RcclComm::RcclComm(const std::string& unique_id, int rank, int world_size, int d
   DPT_RCCL_CHECK(ncclCommInitRank(&comm_, world_size, id, rank));
 }
 
-RcclComm::~RcclComm() {
-  if (comm_ != nullptr && !aborted_) ncclCommDestroy(comm_);
+RcclComm::~RcclComm() { destroy(); }
+
+void RcclComm::destroy() {
+  if (comm_ != nullptr && !aborted_) {
+    hipStreamSynchronize(stream_);
+    ncclCommDestroy(comm_);
+  }
+  comm_ = nullptr;
   if (stream_ != nullptr) hipStreamDestroy(stream_);
+  stream_ = nullptr;
 }
 
 void RcclComm::all_reduce(void* ptr, size_t count, WireType t, hipStream_t stream) {
-  if (aborted_) throw std::runtime_error("RcclComm: communicator was aborted");
+  if (aborted_ || comm_ == nullptr) throw std::runtime_error("RcclComm: communicator was aborted or destroyed");
   if (count == 0) return;
   DPT_RCCL_CHECK(ncclAllReduce(ptr, ptr, count, to_nccl(t), ncclSum, comm_, stream ? stream : stream_));
 }
 
 void RcclComm::broadcast(void* ptr, size_t count, WireType t, int root, hipStream_t stream) {
-  if (aborted_) throw std::runtime_error("RcclComm: communicator was aborted");
+  if (aborted_ || comm_ == nullptr) throw std::runtime_error("RcclComm: communicator was aborted or destroyed");
   if (count == 0) return;
   DPT_RCCL_CHECK(ncclBroadcast(ptr, ptr, count, to_nccl(t), root, comm_, stream ? stream : stream_));
 }

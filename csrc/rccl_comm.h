@@ -40,6 +40,9 @@ class RcclComm {
   int device() const { return device_; }
   // Abort outstanding operations (failure path); the object is unusable after.
   void abort();
+  // Orderly teardown (idempotent): destroy the communicator and its stream now, not at
+  // interpreter exit when the HIP runtime may already be gone.
+  void destroy();
 
  private:
   ncclComm_t comm_ = nullptr;

@@ -88,6 +88,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     except BaseException:
         trainer.abort()  # unblock peers stuck in RCCL collectives, then re-raise
         raise
+    trainer.close()
     cleanup_distributed()
     return 0
 

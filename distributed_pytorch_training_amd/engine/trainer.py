@@ -287,6 +287,10 @@ class Trainer:
             return EpochStats(t[0] / t[2], 100.0 * t[1] / t[2], time.time() - t0)
         return EpochStats(None, None, time.time() - t0)
 
+    def close(self) -> None:
+        if self.ddp is not None:
+            self.ddp.close()
+
     def abort(self) -> None:
         """Failure path: abort the RCCL communicator so peers blocked in a
         collective error out instead of hanging until the process-group timeout."""

@@ -194,6 +194,18 @@ class NativeDDP(nn.Module):
         self._build_reducer()
         return True
 
+    def close(self) -> None:
+        """Orderly teardown: unhook the reducer, then destroy the RCCL communicator (after the
+        device is idle).  Call on every rank before ``destroy_process_group``."""
+        if self.reducer is not None:
+            self.reducer.remove_hooks()
+            self.reducer = None
+        if self.comm is not None:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self.comm.destroy()
+            self.comm = None
+
     def averaged_grads(self) -> List[torch.Tensor]:
         """Per-parameter gradients as torch DDP would present them (sum / world_size)."""
         return [g / self.world_size for g in self.arena.grad_views]
