@@ -70,7 +70,7 @@ void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, double lr, double beta1, 
               "adam arena size mismatch");
   c10::hip::HIPGuard guard(p.device().index());
   dpt::launch_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
-                   p.numel(), (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, adamw,
+                   p.numel(), lr, beta1, beta2, eps, wd, adamw,
                    opt_f32(scale, "scale"), (float)host_factor, opt_f32(found_inf, "found_inf"),
                    opt_f32(step, "step"), zero_grad, cur_stream(p));
 }

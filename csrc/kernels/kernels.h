@@ -18,8 +18,8 @@ void launch_grad_check(const float* g, int64_t n, const float* scale, float host
 void launch_sgd(float* p, float* g, float* buf, int64_t n, float lr, float momentum,
                 float dampening, float wd, bool nesterov, const float* scale, float host_factor,
                 const float* found_inf, const float* step, bool zero_grad, hipStream_t s);
-void launch_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float beta1,
-                 float beta2, float eps, float wd, bool adamw, const float* scale, float host_factor,
+void launch_adam(float* p, float* g, float* m, float* v, int64_t n, double lr, double beta1,
+                 double beta2, double eps, double wd, bool adamw, const float* scale, float host_factor,
                  const float* found_inf, const float* step, bool zero_grad, hipStream_t s);
 void launch_optim_tail(float* scale, int* growth_tracker, float* found_inf, float* step,
                        float growth_factor, float backoff_factor, int growth_interval,

@@ -48,7 +48,7 @@ __global__ __launch_bounds__(kBlock) void grad_check_kernel(const float4* __rest
 template <int UNROLL, bool MOMENTUM, bool NESTEROV>
 __global__ __launch_bounds__(kBlock) void sgd_kernel(float4* __restrict__ p, float4* __restrict__ g,
                                                      float4* __restrict__ buf, int64_t nvec, float lr,
-                                                     float momentum, float dampening, float wd,
+                                                     float momentum, float one_m_damp, float wd,
                                                      const float* scale, float host_factor,
                                                      const float* found_inf, const float* step,
                                                      int zero_grad) {
@@ -67,7 +67,6 @@ __global__ __launch_bounds__(kBlock) void sgd_kernel(float4* __restrict__ p, flo
   }
   const float f = grad_factor(scale, host_factor);
   const bool first = MOMENTUM && (step == nullptr || step[0] == 0.0f);
-  const float one_m_damp = 1.0f - dampening;
   for (int64_t base = (int64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec; base += stride) {
     float4 pv[UNROLL], gv[UNROLL], bv[UNROLL];
 #pragma unroll
@@ -102,11 +101,18 @@ __global__ __launch_bounds__(kBlock) void sgd_kernel(float4* __restrict__ p, flo
   }
 }
 
+// Scalar coefficients are formed in double (on the host, or in-kernel for the step-dependent
+// bias corrections) and rounded once, as torch does with its Python-float hyper-parameters:
+// 1 - 0.999f in fp32 is 1.3e-5 away from fp32(0.001).
+struct AdamCoef {
+  float lr, beta1, beta2, one_m_beta1, one_m_beta2, eps, wd, decay;
+  double beta1_d, beta2_d;
+};
+
 template <int UNROLL, bool ADAMW>
 __global__ __launch_bounds__(kBlock) void adam_kernel(float4* __restrict__ p, float4* __restrict__ g,
                                                       float4* __restrict__ m, float4* __restrict__ v,
-                                                      int64_t nvec, float lr, float beta1, float beta2,
-                                                      float eps, float wd, const float* scale,
+                                                      int64_t nvec, AdamCoef co, const float* scale,
                                                       float host_factor, const float* found_inf,
                                                       const float* step, int zero_grad) {
   const bool skip = found_inf != nullptr && found_inf[0] != 0.0f;
@@ -123,11 +129,11 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float4* __restrict__ p, fl
     return;
   }
   const float f = grad_factor(scale, host_factor);
-  const float t = (step ? step[0] : 0.0f) + 1.0f;
-  const float bc1 = 1.0f - powf(beta1, t);
-  const float bc2_sqrt = sqrtf(1.0f - powf(beta2, t));
-  const float step_size = lr / bc1;
-  const float decay = ADAMW ? 1.0f - lr * wd : 1.0f;
+  const double t = (double)(step ? step[0] : 0.0f) + 1.0;
+  const float bc2_sqrt = (float)sqrt(1.0 - pow(co.beta2_d, t));
+  const float step_size = (float)((double)co.lr / (1.0 - pow(co.beta1_d, t)));
+  const float beta2 = co.beta2, one_m_beta1 = co.one_m_beta1, one_m_beta2 = co.one_m_beta2;
+  const float eps = co.eps, wd = co.wd, decay = co.decay;
   for (int64_t base = (int64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec; base += stride) {
     float4 pv[UNROLL], gv[UNROLL], mv[UNROLL], vv[UNROLL];
 #pragma unroll
@@ -148,8 +154,8 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float4* __restrict__ p, fl
         float gr = gg[k] * f;
         if (ADAMW) pp[k] *= decay;
         else gr += wd * pp[k];
-        mm[k] = mm[k] + (1.0f - beta1) * (gr - mm[k]);       // m.lerp_(g, 1-beta1)
-        vq[k] = beta2 * vq[k] + (1.0f - beta2) * gr * gr;
+        mm[k] = mm[k] + one_m_beta1 * (gr - mm[k]);          // m.lerp_(g, 1-beta1)
+        vq[k] = beta2 * vq[k] + one_m_beta2 * gr * gr;
         float denom = sqrtf(vq[k]) / bc2_sqrt + eps;
         pp[k] = pp[k] - step_size * (mm[k] / denom);
       }
@@ -198,6 +204,7 @@ void launch_grad_check(const float* g, int64_t n, const float* scale, float host
 void launch_sgd(float* p, float* g, float* buf, int64_t n, float lr, float momentum,
                 float dampening, float wd, bool nesterov, const float* scale, float host_factor,
                 const float* found_inf, const float* step, bool zero_grad, hipStream_t s) {
+  const float one_m_damp = (float)(1.0 - (double)dampening);  // formed in double, as torch does
   int64_t nvec = n / 4;
   if (nvec == 0) return;
   dim3 grid(grid_for(nvec, kUnroll)), block(kBlock);
@@ -206,18 +213,18 @@ void launch_sgd(float* p, float* g, float* buf, int64_t n, float lr, float momen
   auto B = reinterpret_cast<float4*>(buf);
   if (momentum == 0.0f) {
     hipLaunchKernelGGL((sgd_kernel<kUnroll, false, false>), grid, block, 0, s, P, G, B, nvec, lr,
-                       momentum, dampening, wd, scale, host_factor, found_inf, step, (int)zero_grad);
+                       momentum, one_m_damp, wd, scale, host_factor, found_inf, step, (int)zero_grad);
   } else if (nesterov) {
     hipLaunchKernelGGL((sgd_kernel<kUnroll, true, true>), grid, block, 0, s, P, G, B, nvec, lr,
-                       momentum, dampening, wd, scale, host_factor, found_inf, step, (int)zero_grad);
+                       momentum, one_m_damp, wd, scale, host_factor, found_inf, step, (int)zero_grad);
   } else {
     hipLaunchKernelGGL((sgd_kernel<kUnroll, true, false>), grid, block, 0, s, P, G, B, nvec, lr,
-                       momentum, dampening, wd, scale, host_factor, found_inf, step, (int)zero_grad);
+                       momentum, one_m_damp, wd, scale, host_factor, found_inf, step, (int)zero_grad);
   }
 }
 
-void launch_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float beta1,
-                 float beta2, float eps, float wd, bool adamw, const float* scale, float host_factor,
+void launch_adam(float* p, float* g, float* m, float* v, int64_t n, double lr, double beta1,
+                 double beta2, double eps, double wd, bool adamw, const float* scale, float host_factor,
                  const float* found_inf, const float* step, bool zero_grad, hipStream_t s) {
   int64_t nvec = n / 4;
   if (nvec == 0) return;
@@ -226,12 +233,23 @@ void launch_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, fl
   auto G = reinterpret_cast<float4*>(g);
   auto M = reinterpret_cast<float4*>(m);
   auto V = reinterpret_cast<float4*>(v);
+  AdamCoef co;
+  co.lr = (float)lr;
+  co.beta1 = (float)beta1;
+  co.beta2 = (float)beta2;
+  co.one_m_beta1 = (float)(1.0 - beta1);
+  co.one_m_beta2 = (float)(1.0 - beta2);
+  co.eps = (float)eps;
+  co.wd = (float)wd;
+  co.decay = adamw ? (float)(1.0 - lr * wd) : 1.0f;
+  co.beta1_d = beta1;
+  co.beta2_d = beta2;
   if (adamw)
-    hipLaunchKernelGGL((adam_kernel<kUnroll, true>), grid, block, 0, s, P, G, M, V, nvec, lr, beta1,
-                       beta2, eps, wd, scale, host_factor, found_inf, step, (int)zero_grad);
+    hipLaunchKernelGGL((adam_kernel<kUnroll, true>), grid, block, 0, s, P, G, M, V, nvec, co, scale,
+                       host_factor, found_inf, step, (int)zero_grad);
   else
-    hipLaunchKernelGGL((adam_kernel<kUnroll, false>), grid, block, 0, s, P, G, M, V, nvec, lr, beta1,
-                       beta2, eps, wd, scale, host_factor, found_inf, step, (int)zero_grad);
+    hipLaunchKernelGGL((adam_kernel<kUnroll, false>), grid, block, 0, s, P, G, M, V, nvec, co, scale,
+                       host_factor, found_inf, step, (int)zero_grad);
 }
 
 void launch_optim_tail(float* scale, int* growth_tracker, float* found_inf, float* step,

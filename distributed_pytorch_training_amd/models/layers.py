@@ -85,15 +85,43 @@ class FusedMaxPool2d(nn.MaxPool2d):
         return super().forward(x)
 
 
-def fuse_native_layers(model: nn.Module) -> int:
+class GemmConv1x1(nn.Conv2d):
+    """1x1 / stride-1 / unpadded conv routed to a GEMM on channels_last activations.
+
+    In channels_last memory the activation is a row-major [N*H*W, Cin] matrix, so the conv is
+    ``x @ W^T`` with no data movement (hipBLASLt on gfx950, bf16 under autocast); autograd's
+    matmul backward gives dgrad and wgrad as GEMMs as well.  Parameters and state-dict keys
+    are the Conv2d's.
+    """
+
+    def gemm_ok(self, x: torch.Tensor) -> bool:
+        return (x.is_cuda and x.dim() == 4 and self.groups == 1 and self.bias is None
+                and self.kernel_size == (1, 1) and self.stride == (1, 1) and self.padding == (0, 0)
+                and self.dilation == (1, 1) and x.is_contiguous(memory_format=torch.channels_last))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not self.gemm_ok(x):
+            return super().forward(x)
+        n, c, h, w = x.shape
+        y = F.linear(x.permute(0, 2, 3, 1), self.weight.view(self.out_channels, c))
+        return y.permute(0, 3, 1, 2)
+
+
+def fuse_native_layers(model: nn.Module, gemm_1x1: bool = False) -> int:
     """Install the gfx950 fused layers: BatchNorm2d -> FusedBatchNorm2d (fused with ReLU /
     residual add by the model's ``bn_act`` calls) and MaxPool2d -> FusedMaxPool2d.  Modules
     keep their parameters/buffers, so state dicts and checkpoints are unchanged."""
     n = fuse_batchnorm(model)
     for parent in model.modules():
         for name, child in list(parent.named_children()):
+            new_cls = None
             if type(child) is nn.MaxPool2d:
-                new = FusedMaxPool2d.__new__(FusedMaxPool2d)
+                new_cls = FusedMaxPool2d
+            elif gemm_1x1 and type(child) is nn.Conv2d and child.kernel_size == (1, 1) \
+                    and child.stride == (1, 1) and child.groups == 1 and child.bias is None:
+                new_cls = GemmConv1x1
+            if new_cls is not None:
+                new = new_cls.__new__(new_cls)
                 new.__dict__ = child.__dict__
                 setattr(parent, name, new)
                 n += 1
