@@ -53,6 +53,7 @@ def parse(argv=None):
                     help="cudnn.benchmark=True: run MIOpen find (minutes on a fresh box). Default is "
                          "immediate mode, which reads the find-db shipped in miopen_db/ (tuned on MI355X "
                          "for this config) and skips the search")
+    ap.add_argument("--cuda-graph", action="store_true", help="replay the captured step as a hipGraph")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="extra steps after the timed window with the hipEvent sync timeline")
     ap.add_argument("--json-out", default=None)
@@ -73,6 +74,8 @@ def train_args(a):
         argv.append("--channels-last")
     if a.no_fused_bn:
         argv.append("--no-fused-bn")
+    if a.cuda_graph:
+        argv.append("--cuda-graph")
     return parse_args(argv)
 
 
@@ -148,7 +151,9 @@ def main(argv=None) -> int:
                    "impl": a.impl, "optimizer": a.optimizer, "channels_last": bool(args.channels_last),
                    "bucket_cap_mb": a.bucket_cap_mb, "grad_dtype": a.grad_dtype,
                    "fused_bn": bool(args.fused_bn and a.impl == "native" and args.channels_last),
-                   "miopen": "find" if a.find else "immediate(find-db)"},
+                   "miopen": "find" if a.find else "immediate(find-db)",
+                   "cuda_graph": bool(a.cuda_graph and trainer.graphed is not None
+                                      and trainer.graphed.graph is not None)},
         "baseline": {"stock_torch_1gpu_img_s": base, "source": "BASELINE.md (MI355X, --impl torch)"},
         "warmup_seconds": round(warm_s, 1),
     }

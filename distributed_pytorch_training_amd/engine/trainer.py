@@ -76,6 +76,7 @@ class Trainer:
         self.grad_accum = max(1, getattr(args, "grad_accum", 1))
         self._accum_fresh = True
         self.roctx = bool(getattr(args, "roctx", False))
+        self.graphed = None
         if self.impl == "native":
             self._init_native(model, comm)
         else:
@@ -102,6 +103,10 @@ class Trainer:
         self.module = model
         self.optimizer = build_optimizer(args.optimizer, self.ddp.arena, args, params_in_order)
         self.metrics = torch.zeros(3, dtype=torch.float64, device=self.device)
+        self.graphed = None
+        if getattr(args, "cuda_graph", False) and self.device.type == "cuda":
+            from .graph import GraphedStep
+            self.graphed = GraphedStep(self)
 
     def _init_torch(self, model: nn.Module) -> None:
         args = self.args
@@ -136,6 +141,8 @@ class Trainer:
         all-reduce (``no_sync``), no optimizer step, gradients keep accumulating.
         """
         if self.impl == "native":
+            if self.graphed is not None and sync and self.grad_accum == 1:
+                return self.graphed(images, targets)
             return self._native_step(images, targets, sync)
         return self._torch_step(images, targets, sync)
 

@@ -136,3 +136,27 @@ def test_reducer_rccl_path_single_rank(cuda, wire, monkeypatch):
     env = dict(__import__("os").environ, DPT_FORCE_COLLECTIVES="1")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_cuda_graph_step_matches_eager(cuda):
+    """hipGraph-replayed native steps produce the same parameters as eager steps."""
+    import copy
+
+    torch.manual_seed(0)
+    base = build_model("resnet18", 10, cuda, image_size=32, channels_last=True)
+    ea = parse_args(["--dataset", "synthetic", "--amp", "--amp-dtype", "bf16", "--channels-last"])
+    ga = parse_args(["--dataset", "synthetic", "--amp", "--amp-dtype", "bf16", "--channels-last", "--cuda-graph"])
+    eager = Trainer(copy.deepcopy(base), ea, 0, 1, cuda, log=lambda s: None)
+    graph = Trainer(copy.deepcopy(base), ga, 0, 1, cuda, log=lambda s: None)
+    torch.backends.cudnn.deterministic = True
+    g = torch.Generator(device=cuda).manual_seed(3)
+    for _ in range(7):
+        x = torch.randn(32, 3, 32, 32, device=cuda, generator=g).contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 10, (32,), device=cuda, generator=g)
+        eager.train_step(x, y)
+        graph.train_step(x, y)
+    torch.cuda.synchronize()
+    assert graph.graphed.graph is not None and graph.graphed.replays == 4, (graph.graphed.failed, graph.graphed.replays)
+    torch.testing.assert_close(graph.ddp.arena.param_flat, eager.ddp.arena.param_flat, rtol=1e-3, atol=1e-4)
+    assert graph.metrics[2].item() == eager.metrics[2].item() == 7 * 32
+    assert graph.scaler.get_scale() == eager.scaler.get_scale()
