@@ -23,6 +23,8 @@
 //
 // Reductions are deterministic two-level: fixed row chunks -> fp32 partials [C][chunks]
 // -> fp64 per-channel sums in a finalize kernel (one wave per 2 channels).  No atomics.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(const void* __rest
 // see ops/bn.py "pair" outputs); their gradients arrive separately and are summed here
 // instead of in an autograd add kernel.  WDZ: also store dz (it is the residual-path
 // gradient dres, and the apply pass then reads dz instead of dy, dy2 and y).
-template <typename IO, bool RELU, bool TWO, bool WDZ>
+template <typename IO, bool RELU, bool TWO, bool WDZ, int UNR>
 __global__ __launch_bounds__(kBlock) void bn_bwd_stats_kernel(const void* __restrict__ dy,
                                                               const void* __restrict__ dy2,
                                                               const void* __restrict__ y,
@@ -281,11 +283,11 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_stats_kernel(const void* __rest
   const int64_t row1 = min(row0 + rows_per_chunk, M);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int64_t r = row0 + rr;
-  for (; r + rpi < row1; r += 2 * rpi) {  // two rows x (3 or 4) tensors in flight per thread
-    float g[2][8], g2[2][8], xv[2][8];
-    bool m[2][8];
+  for (; r + (UNR - 1) * rpi < row1; r += UNR * rpi) {  // UNR rows x (3 or 4) tensors in flight
+    float g[UNR][8], g2[UNR][8], xv[UNR][8];
+    bool m[UNR][8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const int64_t off = (r + u * rpi) * C + cg * 8;
       IO::load8(dy, off, g[u]);
       if (TWO) IO::load8(dy2, off, g2[u]);
@@ -293,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_stats_kernel(const void* __rest
       if (RELU) IO::pos8(y, off, m[u]);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < UNR; ++u) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float gk = TWO ? g[u][k] + g2[u][k] : g[u][k];
@@ -403,20 +405,31 @@ bool bn_supported(int64_t C) {
   return C >= 8 && C % 8 == 0 && C <= 8 * kBlock && kBlock % (C / 8) == 0;
 }
 
+// Tuning knobs (read once): DPT_BN_MAX_CHUNKS (stats blocks, default 1024),
+// DPT_BN_BWD_UNROLL (rows in flight in the backward stats pass: 2 or 4, default 2),
+// DPT_BN_APPLY_MAX (apply-grid cap in blocks, default 8192).
+static int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+static const int kBnMaxChunks = env_int("DPT_BN_MAX_CHUNKS", 1024);
+static const int kBnBwdUnroll = env_int("DPT_BN_BWD_UNROLL", 2);
+static const int kBnApplyMax = env_int("DPT_BN_APPLY_MAX", 4 * kMaxBlocks);
+
 BnGeometry bn_geometry(int64_t M, int64_t C) {
   BnGeometry g;
   const int64_t rpi = kBlock / (C / 8);
   // Enough chunks to fill the chip (<= 1024 blocks of 256 threads, 4 per CU), >= 64 rows
   // each so the fp32 partials stay a few percent of the activation bytes and the finalize
   // sweep stays short; rows_per_chunk is a multiple of rpi.
-  int64_t rows = (M + 1023) / 1024;
+  int64_t rows = (M + kBnMaxChunks - 1) / kBnMaxChunks;
   if (rows < 64) rows = 64;
   rows = (rows + rpi - 1) / rpi * rpi;
   g.rows_per_chunk = rows;
   g.chunks = (int)((M + rows - 1) / rows);
   if (g.chunks < 1) g.chunks = 1;
   int64_t apply = (M + rpi * 2 - 1) / (rpi * 2);
-  g.apply_blocks = (int)(apply < 1 ? 1 : (apply > 4 * kMaxBlocks ? 4 * kMaxBlocks : apply));
+  g.apply_blocks = (int)(apply < 1 ? 1 : (apply > kBnApplyMax ? kBnApplyMax : apply));
   return g;
 }
 
@@ -464,25 +477,37 @@ void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t
   }
 }
 
+template <typename IO, int UNR>
+static void bwd_stats_dispatch(bool relu, const void* dy, const void* dy2, const void* y, const void* x,
+                               const float* mean, int64_t M, int C, const BnGeometry& g, float* p1, float* p2,
+                               void* dz, hipStream_t s) {
+  dim3 bl(kBlock), gs(g.chunks);
+  const int64_t rpc = g.rows_per_chunk;
+  if (dz != nullptr) {  // dz written by the stats pass, read back by the apply pass
+    if (relu && dy2) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true, true, true, UNR>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+    else if (relu) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true, false, true, UNR>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+    else if (dy2) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false, true, true, UNR>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+    else hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false, false, true, UNR>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+  } else {
+    if (relu) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true, false, false, UNR>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+    else hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false, false, false, UNR>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+  }
+}
+
 template <typename IO>
 static void bwd_dispatch(bool relu, const void* dy, const void* dy2, const void* y, const void* x,
                          const float* mean, int64_t M, int C, const BnGeometry& g, float* p1, float* p2,
                          const float* gamma, const float* invstd, float* dgamma, float* dbeta, float* k1,
                          float* k2, float* k3, void* dx, void* dz, hipStream_t s) {
-  dim3 bl(kBlock), gs(g.chunks);
-  const int64_t rpc = g.rows_per_chunk;
-  if (dz != nullptr) {  // dz written by the stats pass, read back by the apply pass
-    if (relu && dy2) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true, true, true>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
-    else if (relu) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true, false, true>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
-    else if (dy2) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false, true, true>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
-    else hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false, false, true>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+  dim3 bl(kBlock);
+  if (kBnBwdUnroll == 4) {
+    bwd_stats_dispatch<IO, 4>(relu, dy, dy2, y, x, mean, M, C, g, p1, p2, dz, s);
   } else {
-    if (relu) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true, false, false>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
-    else hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false, false, false>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+    bwd_stats_dispatch<IO, 2>(relu, dy, dy2, y, x, mean, M, C, g, p1, p2, dz, s);
   }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p2, g.chunks, C, M, gamma,
                      invstd, dgamma, dbeta, k1, k2, k3);
-  dim3 ga(g.apply_blocks * 2 > 4 * kMaxBlocks ? 4 * kMaxBlocks : g.apply_blocks * 2);
+  dim3 ga(g.apply_blocks * 2 > kBnApplyMax ? kBnApplyMax : g.apply_blocks * 2);
   if (dz != nullptr) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, true>), ga, bl, 0, s, dz, y, x, mean, k1, k2, k3, dx, M, C);
   else if (relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false>), ga, bl, 0, s, dy, y, x, mean, k1, k2, k3, dx, M, C);
   else hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, false>), ga, bl, 0, s, dy, y, x, mean, k1, k2, k3, dx, M, C);
