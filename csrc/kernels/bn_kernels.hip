@@ -405,16 +405,19 @@ bool bn_supported(int64_t C) {
   return C >= 8 && C % 8 == 0 && C <= 8 * kBlock && kBlock % (C / 8) == 0;
 }
 
-// Tuning knobs (read once): DPT_BN_MAX_CHUNKS (stats blocks, default 1024),
-// DPT_BN_BWD_UNROLL (rows in flight in the backward stats pass: 2 or 4, default 2),
-// DPT_BN_APPLY_MAX (apply-grid cap in blocks, default 8192).
+// Tuning knobs (read once; defaults from bench/bn_micro.py on MI355X, ResNet-50 tail shapes):
+// DPT_BN_MAX_CHUNKS (stats blocks, default 512), DPT_BN_BWD_UNROLL (rows in flight in the
+// backward stats pass: 2 or 4, default 2), DPT_BN_APPLY_MAX (forward-apply grid cap, default
+// 32768: one 2-row iteration per thread), DPT_BN_BWD_APPLY_MAX (backward-apply grid cap,
+// default 8192).
 static int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
 }
-static const int kBnMaxChunks = env_int("DPT_BN_MAX_CHUNKS", 1024);
+static const int kBnMaxChunks = env_int("DPT_BN_MAX_CHUNKS", 512);
 static const int kBnBwdUnroll = env_int("DPT_BN_BWD_UNROLL", 2);
-static const int kBnApplyMax = env_int("DPT_BN_APPLY_MAX", 4 * kMaxBlocks);
+static const int kBnApplyMax = env_int("DPT_BN_APPLY_MAX", 32768);
+static const int kBnBwdApplyMax = env_int("DPT_BN_BWD_APPLY_MAX", 4 * kMaxBlocks);
 
 BnGeometry bn_geometry(int64_t M, int64_t C) {
   BnGeometry g;
@@ -507,7 +510,7 @@ static void bwd_dispatch(bool relu, const void* dy, const void* dy2, const void*
   }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p2, g.chunks, C, M, gamma,
                      invstd, dgamma, dbeta, k1, k2, k3);
-  dim3 ga(g.apply_blocks * 2 > kBnApplyMax ? kBnApplyMax : g.apply_blocks * 2);
+  dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
   if (dz != nullptr) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, true>), ga, bl, 0, s, dz, y, x, mean, k1, k2, k3, dx, M, C);
   else if (relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false>), ga, bl, 0, s, dy, y, x, mean, k1, k2, k3, dx, M, C);
   else hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, false>), ga, bl, 0, s, dy, y, x, mean, k1, k2, k3, dx, M, C);
