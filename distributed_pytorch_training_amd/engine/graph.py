@@ -7,6 +7,13 @@ all-reduce on the comm stream) + optimizer can be captured once and replayed: on
 launch-bound (the reference's own ResNet-18 / 32x32 CIFAR workload), not for GPU-bound
 ResNet-50 at batch 256.
 
+Stream discipline: autograd runs each AccumulateGrad node on the stream that was current
+when the node was created, and the C++ reducer keeps those nodes alive from construction
+(on the default stream).  A capture on a side stream would then need a default-stream sync
+inside the capture (illegal).  So graph mode owns ONE stream: the reducer is rebuilt under
+it (recreating the accumulator nodes there), and the warmup steps, the capture and every
+replay run on it, ordered against the caller's stream with wait_stream.
+
 Rules (checked or documented):
 * ``warmup`` eager steps run first - MIOpen kernels get compiled/found, the reducer
   rebuilds its buckets, the optimizer allocates its state;
@@ -17,6 +24,7 @@ Rules (checked or documented):
 """
 from __future__ import annotations
 
+import contextlib
 import warnings
 
 import torch
@@ -30,25 +38,47 @@ class GraphedStep:
         self.failed = False
         self.calls = 0
         self.replays = 0
+        self.stream = None
         self.static_x = self.static_y = None
         self.out = self.loss = None
+
+    @contextlib.contextmanager
+    def _on_stream(self):
+        caller = torch.cuda.current_stream()
+        self.stream.wait_stream(caller)
+        with torch.cuda.stream(self.stream):
+            yield
+        caller.wait_stream(self.stream)
+
+    def _own_stream(self) -> None:
+        t = self.trainer
+        torch.cuda.synchronize()
+        self.stream = torch.cuda.Stream(device=t.device)
+        with torch.cuda.stream(self.stream):
+            t.ddp._build_reducer()      # accumulator nodes (re)created on the graph stream
 
     def __call__(self, x: torch.Tensor, y: torch.Tensor):
         t = self.trainer
         if self.failed or t.timeline.enabled:
             return t._native_step(x, y)
+        if self.stream is None:
+            self._own_stream()
         if self.graph is None:
             if self.calls < self.warmup:
                 self.calls += 1
-                return t._native_step(x, y)
+                with self._on_stream():
+                    return t._native_step(x, y)
             self._capture(x, y)
             if self.failed:
-                return t._native_step(x, y)
+                with self._on_stream():
+                    return t._native_step(x, y)
         if x.shape != self.static_x.shape or y.shape != self.static_y.shape:
-            return t._native_step(x, y)
-        self.static_x.copy_(x)
-        self.static_y.copy_(y)
-        self.graph.replay()
+            with self._on_stream():
+                return t._native_step(x, y)
+        with self._on_stream():
+            self.static_x.copy_(x)
+            self.static_y.copy_(y)
+            self.graph.replay()
         self.replays += 1
         t.global_step += 1
         return self.out, self.loss
@@ -60,7 +90,7 @@ class GraphedStep:
         self.static_y = y.clone()
         g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, stream=self.stream):
                 out, loss = t._native_step(self.static_x, self.static_y)
             t.global_step -= 1          # the captured call counted a step that did not run
             torch.cuda.synchronize()

@@ -178,13 +178,14 @@ class NativeDDP(nn.Module):
         n = len(self.arena.params)
         seen = set(order)
         order += [i for i in range(n) if i not in seen]   # unused params keep relative order
-        if order == list(range(n)):
-            return False
-        # Ranks must agree on the layout: use rank 0's observed order.
+        # Every rank must take the same decision on the same layout: adopt rank 0's order
+        # BEFORE deciding (a rank-local early return would strand the others in the broadcast).
         box = [order]
         if dist.is_initialized() and self.world_size > 1:
             dist.broadcast_object_list(box, src=0)
         order = box[0]
+        if order == list(range(n)):
+            return False
         state = optimizer.arena_state() if optimizer is not None and hasattr(optimizer, "arena_state") else []
         perm = self.arena.relayout(order, extra=state)
         if state:
