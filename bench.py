@@ -54,6 +54,8 @@ def parse(argv=None):
                          "immediate mode, which reads the find-db shipped in miopen_db/ (tuned on MI355X "
                          "for this config) and skips the search")
     ap.add_argument("--cuda-graph", action="store_true", help="replay the captured step as a hipGraph")
+    ap.add_argument("--no-weight-shadow", action="store_true",
+                    help="A/B: autocast casts fp32 weights every forward (no optimizer-kept bf16 copy)")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="extra steps after the timed window with the hipEvent sync timeline")
     ap.add_argument("--json-out", default=None)
@@ -76,6 +78,8 @@ def train_args(a):
         argv.append("--no-fused-bn")
     if a.cuda_graph:
         argv.append("--cuda-graph")
+    if a.no_weight_shadow:
+        argv.append("--no-weight-shadow")
     return parse_args(argv)
 
 
@@ -152,6 +156,7 @@ def main(argv=None) -> int:
                    "bucket_cap_mb": a.bucket_cap_mb, "grad_dtype": a.grad_dtype,
                    "fused_bn": bool(args.fused_bn and a.impl == "native" and args.channels_last),
                    "miopen": "find" if a.find else "immediate(find-db)",
+                   "weight_shadow": bool(trainer.ddp is not None and trainer.ddp.shadow_flat is not None),
                    "cuda_graph": bool(a.cuda_graph and trainer.graphed is not None
                                       and trainer.graphed.graph is not None)},
         "baseline": {"stock_torch_1gpu_img_s": base, "source": "BASELINE.md (MI355X, --impl torch)"},

@@ -41,9 +41,20 @@ void grad_check(Tensor g, c10::optional<Tensor> scale, double host_factor, Tenso
                          found_inf.data_ptr<float>(), cur_stream(g));
 }
 
+// Optional 16-bit parameter shadow (bf16 / fp16, same length as the arena).
+std::pair<uint16_t*, int> shadow_arg(const c10::optional<Tensor>& sh, int64_t n) {
+  if (!sh.has_value() || !sh->defined()) return {nullptr, 0};
+  TORCH_CHECK(sh->is_cuda() && sh->is_contiguous() && sh->numel() == n &&
+                  (sh->scalar_type() == at::kBFloat16 || sh->scalar_type() == at::kHalf),
+              "shadow must be a contiguous bf16/fp16 GPU tensor of the arena's size");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(sh->data_ptr()) % 8 == 0, "shadow must be 8-byte aligned");
+  return {reinterpret_cast<uint16_t*>(sh->data_ptr()), sh->scalar_type() == at::kBFloat16 ? 1 : 2};
+}
+
 void sgd_step(Tensor p, Tensor g, Tensor buf, double lr, double momentum, double dampening,
               double wd, bool nesterov, c10::optional<Tensor> scale, double host_factor,
-              c10::optional<Tensor> found_inf, c10::optional<Tensor> step, bool zero_grad) {
+              c10::optional<Tensor> found_inf, c10::optional<Tensor> step, bool zero_grad,
+              c10::optional<Tensor> shadow) {
   check_flat_f32(p, "param");
   check_flat_f32(g, "grad");
   TORCH_CHECK(g.numel() == p.numel(), "grad/param size mismatch");
@@ -51,28 +62,31 @@ void sgd_step(Tensor p, Tensor g, Tensor buf, double lr, double momentum, double
     check_flat_f32(buf, "momentum_buffer");
     TORCH_CHECK(buf.numel() == p.numel(), "momentum buffer size mismatch");
   }
+  auto [sp, sk] = shadow_arg(shadow, p.numel());
   c10::hip::HIPGuard guard(p.device().index());
   dpt::launch_sgd(p.data_ptr<float>(), g.data_ptr<float>(),
                   momentum != 0.0 ? buf.data_ptr<float>() : nullptr, p.numel(), (float)lr,
                   (float)momentum, (float)dampening, (float)wd, nesterov, opt_f32(scale, "scale"),
                   (float)host_factor, opt_f32(found_inf, "found_inf"), opt_f32(step, "step"),
-                  zero_grad, cur_stream(p));
+                  zero_grad, sp, sk, cur_stream(p));
 }
 
 void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, double lr, double beta1, double beta2,
                double eps, double wd, bool adamw, c10::optional<Tensor> scale, double host_factor,
-               c10::optional<Tensor> found_inf, c10::optional<Tensor> step, bool zero_grad) {
+               c10::optional<Tensor> found_inf, c10::optional<Tensor> step, bool zero_grad,
+               c10::optional<Tensor> shadow) {
   check_flat_f32(p, "param");
   check_flat_f32(g, "grad");
   check_flat_f32(m, "exp_avg");
   check_flat_f32(v, "exp_avg_sq");
   TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(),
               "adam arena size mismatch");
+  auto [sp, sk] = shadow_arg(shadow, p.numel());
   c10::hip::HIPGuard guard(p.device().index());
   dpt::launch_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                    p.numel(), lr, beta1, beta2, eps, wd, adamw,
                    opt_f32(scale, "scale"), (float)host_factor, opt_f32(found_inf, "found_inf"),
-                   opt_f32(step, "step"), zero_grad, cur_stream(p));
+                   opt_f32(step, "step"), zero_grad, sp, sk, cur_stream(p));
 }
 
 void optim_tail(c10::optional<Tensor> scale, c10::optional<Tensor> growth_tracker, Tensor found_inf,
@@ -317,10 +331,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_check", &grad_check, py::arg("grad"), py::arg("scale"), py::arg("host_factor"), py::arg("found_inf"));
   m.def("sgd_step", &sgd_step, py::arg("param"), py::arg("grad"), py::arg("momentum_buffer"), py::arg("lr"),
         py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"), py::arg("scale"),
-        py::arg("host_factor"), py::arg("found_inf"), py::arg("step"), py::arg("zero_grad"));
+        py::arg("host_factor"), py::arg("found_inf"), py::arg("step"), py::arg("zero_grad"),
+        py::arg("shadow") = py::none());
   m.def("adam_step", &adam_step, py::arg("param"), py::arg("grad"), py::arg("exp_avg"), py::arg("exp_avg_sq"),
         py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("adamw"),
-        py::arg("scale"), py::arg("host_factor"), py::arg("found_inf"), py::arg("step"), py::arg("zero_grad"));
+        py::arg("scale"), py::arg("host_factor"), py::arg("found_inf"), py::arg("step"), py::arg("zero_grad"),
+        py::arg("shadow") = py::none());
   m.def("optim_tail", &optim_tail, py::arg("scale"), py::arg("growth_tracker"), py::arg("found_inf"),
         py::arg("step"), py::arg("growth_factor"), py::arg("backoff_factor"), py::arg("growth_interval"));
   m.def("pack_bf16", &pack_bf16);

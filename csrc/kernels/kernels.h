@@ -15,12 +15,16 @@ struct AugNorm {
 // optim_kernels.hip
 void launch_grad_check(const float* g, int64_t n, const float* scale, float host_factor,
                        float* found_inf, hipStream_t s);
+// shadow (optional): a 16-bit copy of the updated parameters (bf16: kind 1, fp16: kind 2)
+// written in the same pass - the weights the convolutions read under autocast.
 void launch_sgd(float* p, float* g, float* buf, int64_t n, float lr, float momentum,
                 float dampening, float wd, bool nesterov, const float* scale, float host_factor,
-                const float* found_inf, const float* step, bool zero_grad, hipStream_t s);
+                const float* found_inf, const float* step, bool zero_grad, uint16_t* shadow,
+                int shadow_kind, hipStream_t s);
 void launch_adam(float* p, float* g, float* m, float* v, int64_t n, double lr, double beta1,
                  double beta2, double eps, double wd, bool adamw, const float* scale, float host_factor,
-                 const float* found_inf, const float* step, bool zero_grad, hipStream_t s);
+                 const float* found_inf, const float* step, bool zero_grad, uint16_t* shadow,
+                 int shadow_kind, hipStream_t s);
 void launch_optim_tail(float* scale, int* growth_tracker, float* found_inf, float* step,
                        float growth_factor, float backoff_factor, int growth_interval,
                        hipStream_t s);
@@ -67,9 +71,10 @@ void launch_maxpool_bwd(int dtype, const void* dy, const uint8_t* idx, void* dx,
 // gather_kernels.hip: up to kGatherMax tensors per launch (kernel-argument struct)
 constexpr int kGatherMax = 48;
 struct GatherBatch {
-  const float* src[kGatherMax];
+  const void* src[kGatherMax];
   float* dst[kGatherMax];
   int64_t numel[kGatherMax];
+  int8_t kind[kGatherMax];  // source dtype: 0 f32, 1 bf16, 2 f16
   int count;
 };
 void launch_gather(const GatherBatch& batch, bool accumulate, hipStream_t s);

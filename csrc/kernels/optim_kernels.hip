@@ -22,6 +22,17 @@
 
 namespace dpt {
 
+// 16-bit shadow of 4 updated parameters (bf16 kind 1, fp16 kind 2): one 8-byte store.
+__device__ __forceinline__ void store_shadow4(uint16_t* shadow, int kind, int64_t i, float4 v) {
+  auto cv = [kind](float f) -> uint32_t {
+    return kind == 1 ? (uint32_t)f32_to_bf16(f) : (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f);
+  };
+  uint2 w;
+  w.x = cv(v.x) | (cv(v.y) << 16);
+  w.y = cv(v.z) | (cv(v.w) << 16);
+  reinterpret_cast<uint2*>(shadow)[i] = w;
+}
+
 template <int UNROLL>
 __global__ __launch_bounds__(kBlock) void grad_check_kernel(const float4* __restrict__ g,
                                                             int64_t nvec, const float* scale,
@@ -51,7 +62,8 @@ __global__ __launch_bounds__(kBlock) void sgd_kernel(float4* __restrict__ p, flo
                                                      float momentum, float one_m_damp, float wd,
                                                      const float* scale, float host_factor,
                                                      const float* found_inf, const float* step,
-                                                     int zero_grad) {
+                                                     int zero_grad, uint16_t* __restrict__ shadow,
+                                                     int shadow_kind) {
   const bool skip = found_inf != nullptr && found_inf[0] != 0.0f;
   const int64_t stride = (int64_t)gridDim.x * kBlock * UNROLL;
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -95,6 +107,7 @@ __global__ __launch_bounds__(kBlock) void sgd_kernel(float4* __restrict__ p, flo
         pp[k] = pp[k] - lr * d;
       }
       p[i] = pv[u];
+      if (shadow) store_shadow4(shadow, shadow_kind, i, pv[u]);
       if (MOMENTUM) buf[i] = bv[u];
       if (zero_grad) g[i] = z;
     }
@@ -114,7 +127,8 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float4* __restrict__ p, fl
                                                       float4* __restrict__ m, float4* __restrict__ v,
                                                       int64_t nvec, AdamCoef co, const float* scale,
                                                       float host_factor, const float* found_inf,
-                                                      const float* step, int zero_grad) {
+                                                      const float* step, int zero_grad,
+                                                      uint16_t* __restrict__ shadow, int shadow_kind) {
   const bool skip = found_inf != nullptr && found_inf[0] != 0.0f;
   const int64_t stride = (int64_t)gridDim.x * kBlock * UNROLL;
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -160,6 +174,7 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float4* __restrict__ p, fl
         pp[k] = pp[k] - step_size * (mm[k] / denom);
       }
       p[i] = pv[u]; m[i] = mv[u]; v[i] = vv[u];
+      if (shadow) store_shadow4(shadow, shadow_kind, i, pv[u]);
       if (zero_grad) g[i] = z;
     }
   }
@@ -203,7 +218,8 @@ void launch_grad_check(const float* g, int64_t n, const float* scale, float host
 
 void launch_sgd(float* p, float* g, float* buf, int64_t n, float lr, float momentum,
                 float dampening, float wd, bool nesterov, const float* scale, float host_factor,
-                const float* found_inf, const float* step, bool zero_grad, hipStream_t s) {
+                const float* found_inf, const float* step, bool zero_grad, uint16_t* shadow,
+                int shadow_kind, hipStream_t s) {
   const float one_m_damp = (float)(1.0 - (double)dampening);  // formed in double, as torch does
   int64_t nvec = n / 4;
   if (nvec == 0) return;
@@ -213,19 +229,20 @@ void launch_sgd(float* p, float* g, float* buf, int64_t n, float lr, float momen
   auto B = reinterpret_cast<float4*>(buf);
   if (momentum == 0.0f) {
     hipLaunchKernelGGL((sgd_kernel<kUnroll, false, false>), grid, block, 0, s, P, G, B, nvec, lr,
-                       momentum, one_m_damp, wd, scale, host_factor, found_inf, step, (int)zero_grad);
+                       momentum, one_m_damp, wd, scale, host_factor, found_inf, step, (int)zero_grad, shadow, shadow_kind);
   } else if (nesterov) {
     hipLaunchKernelGGL((sgd_kernel<kUnroll, true, true>), grid, block, 0, s, P, G, B, nvec, lr,
-                       momentum, one_m_damp, wd, scale, host_factor, found_inf, step, (int)zero_grad);
+                       momentum, one_m_damp, wd, scale, host_factor, found_inf, step, (int)zero_grad, shadow, shadow_kind);
   } else {
     hipLaunchKernelGGL((sgd_kernel<kUnroll, true, false>), grid, block, 0, s, P, G, B, nvec, lr,
-                       momentum, one_m_damp, wd, scale, host_factor, found_inf, step, (int)zero_grad);
+                       momentum, one_m_damp, wd, scale, host_factor, found_inf, step, (int)zero_grad, shadow, shadow_kind);
   }
 }
 
 void launch_adam(float* p, float* g, float* m, float* v, int64_t n, double lr, double beta1,
                  double beta2, double eps, double wd, bool adamw, const float* scale, float host_factor,
-                 const float* found_inf, const float* step, bool zero_grad, hipStream_t s) {
+                 const float* found_inf, const float* step, bool zero_grad, uint16_t* shadow,
+                 int shadow_kind, hipStream_t s) {
   int64_t nvec = n / 4;
   if (nvec == 0) return;
   dim3 grid(grid_for(nvec, kUnroll)), block(kBlock);
@@ -246,10 +263,10 @@ void launch_adam(float* p, float* g, float* m, float* v, int64_t n, double lr, d
   co.beta2_d = beta2;
   if (adamw)
     hipLaunchKernelGGL((adam_kernel<kUnroll, true>), grid, block, 0, s, P, G, M, V, nvec, co, scale,
-                       host_factor, found_inf, step, (int)zero_grad);
+                       host_factor, found_inf, step, (int)zero_grad, shadow, shadow_kind);
   else
     hipLaunchKernelGGL((adam_kernel<kUnroll, false>), grid, block, 0, s, P, G, M, V, nvec, co, scale,
-                       host_factor, found_inf, step, (int)zero_grad);
+                       host_factor, found_inf, step, (int)zero_grad, shadow, shadow_kind);
 }
 
 void launch_optim_tail(float* scale, int* growth_tracker, float* found_inf, float* step,

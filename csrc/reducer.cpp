@@ -196,17 +196,20 @@ void Reducer::gather_bucket(int64_t b, hipStream_t s) {
       if (!accumulate_) DPT_HIP_OK(hipMemsetAsync(v.data_ptr<float>(), 0, v.numel() * sizeof(float), s));
       continue;
     }
-    const bool same = g.scalar_type() == at::kFloat && g.is_cuda() && g.strides() == v.strides() &&
-                      g.sizes() == v.sizes() && g.is_non_overlapping_and_dense();
+    const auto dt = g.scalar_type();
+    const int kind = dt == at::kFloat ? 0 : dt == at::kBFloat16 ? 1 : dt == at::kHalf ? 2 : -1;
+    const bool same = kind >= 0 && g.is_cuda() && g.strides() == v.strides() && g.sizes() == v.sizes() &&
+                      g.is_non_overlapping_and_dense();
     if (!same) {
-      at::Tensor vv = v;  // strided fallback on the current stream
-      if (accumulate_) vv.add_(g);
+      at::Tensor vv = v;  // strided / odd-dtype fallback on the current stream
+      if (accumulate_) vv.add_(g.to(at::kFloat));
       else vv.copy_(g);
       continue;
     }
-    batch.src[batch.count] = g.data_ptr<float>();
+    batch.src[batch.count] = g.data_ptr();
     batch.dst[batch.count] = v.data_ptr<float>();
     batch.numel[batch.count] = v.numel();
+    batch.kind[batch.count] = (int8_t)kind;
     if (++batch.count == kGatherMax) {
       launch_gather(batch, accumulate_, s);
       batch.count = 0;
@@ -288,7 +291,9 @@ void Reducer::finalize() {
     // Hand the arena views back as .grad and drop the stolen tensors (their memory returns to
     // the caching allocator stream-ordered behind the gather kernels).
     for (size_t i = 0; i < params_.size(); ++i) {
-      params_[i].mutable_grad() = grad_views_[i];
+      // fp32 parameters get their arena view back as .grad; 16-bit weight-shadow leaves
+      // keep an undefined .grad (their gradient lives, converted, in the fp32 arena).
+      if (params_[i].scalar_type() == at::kFloat) params_[i].mutable_grad() = grad_views_[i];
       stolen_[i].reset();
     }
   }

@@ -94,11 +94,16 @@ class Trainer:
             fuse_native_layers(model)
         params_in_order = [p for p in model.parameters() if p.requires_grad]
         self.scaler = DeviceGradScaler(self.device, enabled=self.amp)
+        shadow = None
+        if (self.amp and getattr(args, "weight_shadow", True) and self.grad_accum == 1
+                and self.device.type == "cuda"):
+            shadow = torch.bfloat16 if self.amp_dtype == "bf16" else torch.float16
         self.ddp = NativeDDP(model, rank=self.rank, world_size=self.world_size, device=self.device,
                              bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb,
                              broadcast_buffers=args.broadcast_buffers, grad_dtype=args.grad_dtype,
                              found_inf=self.scaler.found_inf, scale=self.scaler.scale_tensor,
-                             check_inf=self.amp, profile=self.timeline.enabled, comm=comm)
+                             check_inf=self.amp, profile=self.timeline.enabled, comm=comm,
+                             weight_shadow=shadow)
         self.model = self.ddp
         self.module = model
         self.optimizer = build_optimizer(args.optimizer, self.ddp.arena, args, params_in_order)
@@ -168,7 +173,7 @@ class Trainer:
             self.log(f"rebuilt buckets: {self.ddp.bucket_sizes_mib()}")
         with roctx_range("optimizer", rx):
             self.optimizer.step(self.scaler if self.amp else None, host_factor=self.ddp.grad_factor,
-                                grads_checked=self.ddp.grads_checked)
+                                grads_checked=self.ddp.grads_checked, shadow=self.ddp.shadow_flat)
         tl.mark("opt")
         ops.accumulate_metrics(outputs, targets, loss, self.metrics)
         tl.end_step(self.ddp.comm_profile() if tl.enabled else None)
@@ -293,6 +298,11 @@ class Trainer:
         if self.rank == 0 and t[2] > 0:
             return EpochStats(t[0] / t[2], 100.0 * t[1] / t[2], time.time() - t0)
         return EpochStats(None, None, time.time() - t0)
+
+    def sync_weights(self) -> None:
+        """After externally loading parameters: refresh the 16-bit weight shadows."""
+        if self.ddp is not None:
+            self.ddp.refresh_shadow()
 
     def close(self) -> None:
         if self.ddp is not None:

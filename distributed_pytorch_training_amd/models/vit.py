@@ -23,6 +23,8 @@ import torch.nn.functional as F
 
 
 class SelfAttention(nn.Module):
+    dpt_shadow_names = ("in_proj_weight", "in_proj_bias")  # 16-bit weight shadows (parallel/shadow.py)
+
     def __init__(self, dim: int, heads: int, dropout: float = 0.0) -> None:
         super().__init__()
         self.dim, self.heads, self.dropout = dim, heads, dropout
@@ -35,7 +37,8 @@ class SelfAttention(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         b, s, d = x.shape
-        qkv = F.linear(x, self.in_proj_weight, self.in_proj_bias)
+        from ..parallel.shadow import shadow_param
+        qkv = F.linear(x, shadow_param(self, "in_proj_weight", x), shadow_param(self, "in_proj_bias", x))
         qkv = qkv.view(b, s, 3, self.heads, d // self.heads).permute(2, 0, 3, 1, 4)
         y = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2],
                                            dropout_p=self.dropout if self.training else 0.0)

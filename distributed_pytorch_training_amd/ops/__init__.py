@@ -46,25 +46,30 @@ def grad_check(grad, scale, host_factor: float, found_inf) -> None:
 
 
 def sgd_step(param, grad, momentum_buffer, *, lr, momentum, dampening, weight_decay, nesterov,
-             scale=None, host_factor=1.0, found_inf=None, step=None, zero_grad=True) -> None:
+             scale=None, host_factor=1.0, found_inf=None, step=None, zero_grad=True, shadow=None) -> None:
     if _gpu(param):
         native().sgd_step(param, grad, momentum_buffer if momentum_buffer is not None else param,
                           float(lr), float(momentum), float(dampening), float(weight_decay),
-                          bool(nesterov), scale, float(host_factor), found_inf, step, bool(zero_grad))
+                          bool(nesterov), scale, float(host_factor), found_inf, step, bool(zero_grad),
+                          shadow)
     else:
         reference.sgd_step(param, grad, momentum_buffer, lr, momentum, dampening, weight_decay,
                            nesterov, scale, host_factor, found_inf, step, zero_grad)
+        if shadow is not None:
+            shadow.copy_(param)
 
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, *, lr, beta1, beta2, eps, weight_decay, adamw,
-              scale=None, host_factor=1.0, found_inf=None, step=None, zero_grad=True) -> None:
+              scale=None, host_factor=1.0, found_inf=None, step=None, zero_grad=True, shadow=None) -> None:
     if _gpu(param):
         native().adam_step(param, grad, exp_avg, exp_avg_sq, float(lr), float(beta1), float(beta2),
                            float(eps), float(weight_decay), bool(adamw), scale, float(host_factor),
-                           found_inf, step, bool(zero_grad))
+                           found_inf, step, bool(zero_grad), shadow)
     else:
         reference.adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
                             adamw, scale, host_factor, found_inf, step, zero_grad)
+        if shadow is not None:
+            shadow.copy_(param)
 
 
 def optim_tail(scale, growth_tracker, found_inf, step, growth_factor=2.0, backoff_factor=0.5,

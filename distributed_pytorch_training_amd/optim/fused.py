@@ -117,7 +117,7 @@ class FusedSGD(_FlatOptimizer):
             self.momentum_buffer = tensors[0]
 
     def step(self, scaler: Optional[DeviceGradScaler] = None, host_factor: float = 1.0,
-             grads_checked: bool = False) -> None:
+             grads_checked: bool = False, shadow: Optional[torch.Tensor] = None) -> None:
         g = self.group
         if g["momentum"] != 0 and self.momentum_buffer is None:
             self.momentum_buffer = self.arena.zeros_like_arena()
@@ -125,7 +125,8 @@ class FusedSGD(_FlatOptimizer):
         ops.sgd_step(self.arena.param_flat, self.arena.grad_flat, self.momentum_buffer,
                      lr=g["lr"], momentum=g["momentum"], dampening=g["dampening"],
                      weight_decay=g["weight_decay"], nesterov=g["nesterov"], scale=scale,
-                     host_factor=host_factor, found_inf=found_inf, step=self._step, zero_grad=True)
+                     host_factor=host_factor, found_inf=found_inf, step=self._step, zero_grad=True,
+                     shadow=shadow)
         self._epilogue(scaler, found_inf)
 
     def state_dict(self) -> Dict[str, Any]:
@@ -170,7 +171,7 @@ class FusedAdam(_FlatOptimizer):
             self.exp_avg, self.exp_avg_sq = tensors
 
     def step(self, scaler: Optional[DeviceGradScaler] = None, host_factor: float = 1.0,
-             grads_checked: bool = False) -> None:
+             grads_checked: bool = False, shadow: Optional[torch.Tensor] = None) -> None:
         g = self.group
         if self.exp_avg is None:
             self.exp_avg = self.arena.zeros_like_arena()
@@ -180,7 +181,7 @@ class FusedAdam(_FlatOptimizer):
         ops.adam_step(self.arena.param_flat, self.arena.grad_flat, self.exp_avg, self.exp_avg_sq,
                       lr=g["lr"], beta1=b1, beta2=b2, eps=g["eps"], weight_decay=g["weight_decay"],
                       adamw=self.adamw, scale=scale, host_factor=host_factor, found_inf=found_inf,
-                      step=self._step, zero_grad=True)
+                      step=self._step, zero_grad=True, shadow=shadow)
         self._epilogue(scaler, found_inf)
 
     def state_dict(self) -> Dict[str, Any]:

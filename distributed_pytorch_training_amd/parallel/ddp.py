@@ -43,7 +43,8 @@ class NativeDDP(nn.Module):
                  first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
                  grad_dtype: str = "fp32", found_inf: Optional[torch.Tensor] = None,
                  scale: Optional[torch.Tensor] = None, check_inf: bool = False,
-                 profile: bool = False, rebuild_buckets: bool = True, comm=None) -> None:
+                 profile: bool = False, rebuild_buckets: bool = True, comm=None,
+                 weight_shadow: Optional[torch.dtype] = None) -> None:
         super().__init__()
         self.module = module
         self.rank, self.world_size = rank, world_size
@@ -74,12 +75,29 @@ class NativeDDP(nn.Module):
             broadcast_(self.arena.param_flat, self.comm, 0)
             for t in self.buffers_arena.tensors():
                 broadcast_(t, self.comm, 0)
+        # 16-bit weight shadows (parallel/shadow.py): GPU only, written by the fused optimizer
+        self.weight_shadow = weight_shadow if self.device.type == "cuda" else None
+        self.shadow_flat: Optional[torch.Tensor] = None
+        self._shadow_leaves = {}
+        self._install_shadows()
         self.reducer = None
         self.plan: Optional[BucketPlan] = None
         self._wire_buf = None
         self._build_reducer()
 
     # ------------------------------------------------------------------ construction
+    def _install_shadows(self) -> None:
+        if self.weight_shadow is None:
+            return
+        from .shadow import install_shadows
+        self.shadow_flat, self._shadow_leaves = install_shadows(self.module, self.arena, self.weight_shadow)
+
+    def refresh_shadow(self) -> None:
+        """Re-derive the 16-bit shadows from the fp32 masters (after load_state_dict etc.)."""
+        if self.shadow_flat is not None:
+            with torch.no_grad():
+                self.shadow_flat.copy_(self.arena.param_flat)
+
     def _verify_shapes(self, params: List[torch.Tensor]) -> None:
         desc = ";".join(f"{tuple(p.shape)}:{p.dtype}" for p in params)
         digest = hashlib.sha1(desc.encode()).hexdigest()
@@ -105,8 +123,11 @@ class NativeDDP(nn.Module):
             self._wire_buf = torch.zeros(self.arena.numel, dtype=torch.bfloat16, device=self.device)
         wire_buf = self._wire_buf if self._wire_buf is not None else torch.empty(0)
         py_cb = None if gpu else self._cpu_allreduce
+        # gradient leaves: the 16-bit shadow where one exists (its gradient is what autograd
+        # produces), else the fp32 parameter itself
+        leaves = [self._shadow_leaves.get(i, p) for i, p in enumerate(self.arena.params)]
         self.reducer = C.Reducer(
-            list(self.arena.params), list(self.arena.grad_views), self.arena.grad_flat,
+            leaves, list(self.arena.grad_views), self.arena.grad_flat,
             self.plan.offsets, self.plan.numels, self.plan.param_bucket, self.comm, py_cb, wire,
             wire_buf, self.found_inf, self.scale if self.scale is not None else torch.empty(0),
             1.0 / self.world_size, bool(self.check_inf), bool(self.profile), gpu)
@@ -151,6 +172,9 @@ class NativeDDP(nn.Module):
 
     @contextlib.contextmanager
     def no_sync(self):
+        if self.shadow_flat is not None:
+            raise RuntimeError("no_sync/gradient accumulation is not supported with 16-bit weight "
+                               "shadows; construct NativeDDP with weight_shadow=None")
         old = self.require_backward_grad_sync
         self.require_backward_grad_sync = False
         self._pending_accum = True
@@ -190,6 +214,7 @@ class NativeDDP(nn.Module):
         perm = self.arena.relayout(order, extra=state)
         if state:
             optimizer.set_arena_state(perm.extra)
+        self._install_shadows()       # shadow arena follows the new layout
         if self._wire_buf is not None:
             self._wire_buf = torch.zeros(self.arena.numel, dtype=torch.bfloat16, device=self.device)
         self._build_reducer()

@@ -68,4 +68,6 @@ def load_checkpoint(path: str, trainer, map_location: Optional[str] = "cpu") -> 
     trainer.optimizer.load_state_dict(state["optimizer"])
     if state.get("scaler"):
         trainer.scaler.load_state_dict(state["scaler"])
+    if hasattr(trainer, "sync_weights"):
+        trainer.sync_weights()
     return int(state["epoch"])

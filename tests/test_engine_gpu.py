@@ -160,3 +160,39 @@ def test_cuda_graph_step_matches_eager(cuda):
     torch.testing.assert_close(graph.ddp.arena.param_flat, eager.ddp.arena.param_flat, rtol=1e-3, atol=1e-4)
     assert graph.metrics[2].item() == eager.metrics[2].item() == 7 * 32
     assert graph.scaler.get_scale() == eager.scaler.get_scale()
+
+
+@pytest.mark.parametrize("model_name,opt", [("resnet18", "sgd"), ("vit_b_16", "adamw")])
+def test_weight_shadow_matches_autocast_casts(cuda, model_name, opt):
+    """bf16 weight shadows (optimizer-maintained) give the same training trajectory as
+    autocast's per-forward weight casts, and stay equal to bf16(master) after every step."""
+    import copy
+
+    torch.manual_seed(0)
+    cl = model_name.startswith("resnet")
+    base = build_model(model_name, 10, cuda, image_size=32, channels_last=cl)
+    common = ["--model", model_name, "--dataset", "synthetic", "--amp", "--amp-dtype", "bf16",
+              "--optimizer", opt, "--lr", "0.1" if opt == "sgd" else "1e-3"] + (["--channels-last"] if cl else [])
+    sh = Trainer(copy.deepcopy(base), parse_args(common), 0, 1, cuda, log=lambda s: None)
+    no = Trainer(copy.deepcopy(base), parse_args(common + ["--no-weight-shadow"]), 0, 1, cuda, log=lambda s: None)
+    assert sh.ddp.shadow_flat is not None and no.ddp.shadow_flat is None
+    torch.backends.cudnn.deterministic = True
+    g = torch.Generator(device=cuda).manual_seed(5)
+    for _ in range(4):
+        x = torch.randn(16, 3, 32, 32, device=cuda, generator=g)
+        if cl:
+            x = x.contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 10, (16,), device=cuda, generator=g)
+        sh.train_step(x, y)
+        no.train_step(x, y)
+        torch.cuda.synchronize()
+        assert torch.equal(sh.ddp.shadow_flat, sh.ddp.arena.param_flat.to(torch.bfloat16))
+    atol = 1e-5 if opt == "sgd" else 2e-3
+    torch.testing.assert_close(sh.ddp.arena.param_flat, no.ddp.arena.param_flat, rtol=1e-4, atol=atol)
+    assert sh.scaler.get_scale() == no.scaler.get_scale()
+    # checkpoint-style reload refreshes the shadows
+    with torch.no_grad():
+        for p in sh.module.parameters():
+            p.add_(1.0)
+    sh.sync_weights()
+    assert torch.equal(sh.ddp.shadow_flat, sh.ddp.arena.param_flat.to(torch.bfloat16))
