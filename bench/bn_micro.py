@@ -41,7 +41,7 @@ def main():
         b = torch.zeros(c, device=dev)
         rm, rv = torch.zeros(c, device=dev), torch.ones(c, device=dev)
         nb = torch.zeros(1, dtype=torch.long, device=dev)
-        y, mean, invstd = C_.bn_fwd_train(x, r, wgt, b, rm, rv, nb, 0.1, 1e-5, True)
+        y, mean, invstd, _coef = C_.bn_fwd_train(x, r, wgt, b, rm, rv, nb, 0.1, 1e-5, True)
         bytes_pass = x.numel() * 2
         tf = t_ms(lambda: C_.bn_fwd_train(x, r, wgt, b, rm, rv, nb, 0.1, 1e-5, True))
         tb = t_ms(lambda: C_.bn_bwd(dy, dy2, y, x, wgt, mean, invstd, True, True, True))

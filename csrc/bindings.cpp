@@ -233,14 +233,15 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::
   auto y = at::empty_like(x);
   auto fopt = x.options().dtype(at::kFloat);
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  auto coef = at::empty({2 * C}, fopt);  // [a | b]: y = relu(x*a + b [+ r]); lets bn_bwd skip reading y
   auto ws = at::empty({dpt::bn_workspace_floats(M, C)}, fopt);
   c10::hip::HIPGuard guard(x.device().index());
   dpt::launch_bn_fwd_train(bn_dtype(x), x.data_ptr(), rp, y.data_ptr(), M, C, f32_param(weight, C, "weight"),
                            f32_param(bias, C, "bias"), (float)eps, (float)momentum,
                            f32_param(running_mean, C, "running_mean"), f32_param(running_var, C, "running_var"), nb,
-                           mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr<float>(), relu,
-                           cur_stream(x));
-  return {y, mean, invstd};
+                           mean.data_ptr<float>(), invstd.data_ptr<float>(), coef.data_ptr<float>(),
+                           ws.data_ptr<float>(), relu, cur_stream(x));
+  return {y, mean, invstd, coef};
 }
 
 Tensor bn_apply(Tensor x, c10::optional<Tensor> residual, Tensor a, Tensor b, bool relu) {
@@ -262,9 +263,11 @@ Tensor bn_apply(Tensor x, c10::optional<Tensor> residual, Tensor a, Tensor b, bo
 // Returns {dx, dgamma, dbeta, dz}.  dy2: gradient of the second (aliased) output, if the
 // forward exposed one.  dz (= the residual-path gradient) is materialised when want_dz or
 // dy2 is given.
+// coef: the forward's [a | b]; with ReLU and no residual-path output, the mask is recomputed
+// from x (y may then be None).
 std::vector<Tensor> bn_bwd(Tensor dy, c10::optional<Tensor> dy2, c10::optional<Tensor> y, Tensor x,
                            c10::optional<Tensor> weight, Tensor mean, Tensor invstd, bool relu, bool want_dz,
-                           bool want_dparams) {
+                           bool want_dparams, c10::optional<Tensor> coef) {
   auto [M, C] = bn_rows(x, "x");
   auto [Md, Cd] = bn_rows(dy, "grad_output");
   TORCH_CHECK(M == Md && C == Cd && dy.scalar_type() == x.scalar_type(), "grad_output mismatch");
@@ -274,22 +277,24 @@ std::vector<Tensor> bn_bwd(Tensor dy, c10::optional<Tensor> dy2, c10::optional<T
     TORCH_CHECK(M2 == M && C2 == C && dy2->scalar_type() == x.scalar_type(), "grad_output2 mismatch");
     d2 = dy2->data_ptr();
   }
+  const bool make_dz = want_dz || d2 != nullptr;
+  const float* cp = nullptr;
+  if (relu && !make_dz && coef.has_value() && coef->defined()) cp = f32_param(*coef, 2 * C, "coef");
   const void* yp = nullptr;
-  if (relu) {
-    TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the saved output");
+  if (relu && cp == nullptr) {
+    TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the saved output (or coef)");
     bn_rows(*y, "y");
     yp = y->data_ptr();
   }
   auto fopt = x.options().dtype(at::kFloat);
   auto dx = at::empty_like(x);
-  const bool make_dz = want_dz || d2 != nullptr;
   Tensor dz = make_dz ? at::empty_like(x) : Tensor();
   Tensor dg = want_dparams ? at::empty({C}, fopt) : Tensor();
   Tensor db = want_dparams ? at::empty({C}, fopt) : Tensor();
   auto ws = at::empty({dpt::bn_workspace_floats(M, C)}, fopt);
   c10::hip::HIPGuard guard(x.device().index());
   dpt::launch_bn_bwd(bn_dtype(x), dy.data_ptr(), d2, yp, x.data_ptr(), M, C, f32_param(weight, C, "weight"),
-                     f32_param(mean, C, "mean"), f32_param(invstd, C, "invstd"),
+                     f32_param(mean, C, "mean"), f32_param(invstd, C, "invstd"), cp,
                      want_dparams ? dg.data_ptr<float>() : nullptr, want_dparams ? db.data_ptr<float>() : nullptr,
                      dx.data_ptr(), make_dz ? dz.data_ptr() : nullptr, ws.data_ptr<float>(), relu, cur_stream(x));
   return {dx, dg, db, dz};
@@ -324,6 +329,137 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64
   return dx;
 }
 
+// ---- ViT block kernels (vit_kernels.hip) -----------------------------------------------------
+int act16_kind(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), name, " must be a contiguous GPU tensor");
+  if (t.scalar_type() == at::kBFloat16) return 1;
+  TORCH_CHECK(t.scalar_type() == at::kHalf, name, " must be bf16 or fp16");
+  return 2;
+}
+
+// A per-column parameter of any float dtype (the fp32 master or its 16-bit shadow).
+int param_kind(const Tensor& t, int64_t D, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.numel() == D, name, " must be a contiguous GPU tensor of ", D,
+              " elements");
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kHalf: return 2;
+    default: TORCH_CHECK(false, name, " must be f32/bf16/f16");
+  }
+  return 0;
+}
+
+at::ScalarType kind_dtype(int kind) { return kind == 1 ? at::kBFloat16 : at::kHalf; }
+
+// s = x + a + bias (only when a is given), h = LayerNorm(s) (16-bit), per-row mean / rstd.
+std::vector<Tensor> ln_fwd(Tensor x, c10::optional<Tensor> a, c10::optional<Tensor> bias,
+                           c10::optional<Tensor> gamma, c10::optional<Tensor> beta, double eps, int64_t out_kind) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), "ln: x must be contiguous fp32 GPU");
+  const int64_t D = x.size(-1), T = x.numel() / D;
+  TORCH_CHECK(dpt::ln_supported(D), "ln: width must be a multiple of 256 in [256, 2048], got ", D);
+  const bool add = a.has_value() && a->defined();
+  int kind = (int)out_kind;
+  const void* bp = nullptr;
+  int bk = 0;
+  if (add) {
+    kind = act16_kind(*a, "ln: a");
+    TORCH_CHECK(a->sizes() == x.sizes(), "ln: a must match x");
+    if (bias.has_value() && bias->defined()) {
+      bk = param_kind(*bias, D, "ln: bias");
+      bp = bias->data_ptr();
+    }
+  }
+  TORCH_CHECK(kind == 1 || kind == 2, "ln: output kind must be 1 (bf16) or 2 (fp16)");
+  Tensor sv = add ? at::empty_like(x) : Tensor();
+  auto h = at::empty(x.sizes(), x.options().dtype(kind_dtype(kind)));
+  auto fopt = x.options().dtype(at::kFloat);
+  auto mean = at::empty({T}, fopt), rstd = at::empty({T}, fopt);
+  c10::hip::HIPGuard guard(x.device().index());
+  dpt::launch_ln_fwd(kind, x.data_ptr<float>(), add ? static_cast<const uint16_t*>(a->data_ptr()) : nullptr, bp, bk,
+                     f32_param(gamma, D, "gamma"), f32_param(beta, D, "beta"), add ? sv.data_ptr<float>() : nullptr,
+                     static_cast<uint16_t*>(h.data_ptr()), mean.data_ptr<float>(), rstd.data_ptr<float>(), T, D,
+                     (float)eps, cur_stream(x));
+  return {sv, h, mean, rstd};
+}
+
+// Returns {gx, ga, dgamma, dbeta, dbias}: gx = gs + LN_bwd(gh) (fp32); with want_ga also
+// ga = 16-bit(gx) and, if bias_like is given, dbias = column sums of gx in bias_like's dtype.
+std::vector<Tensor> ln_bwd(c10::optional<Tensor> gs, Tensor gh, Tensor sv, Tensor mean, Tensor rstd,
+                           c10::optional<Tensor> gamma, bool want_ga, c10::optional<Tensor> bias_like,
+                           bool want_dparams) {
+  TORCH_CHECK(sv.is_cuda() && sv.scalar_type() == at::kFloat && sv.is_contiguous(), "ln_bwd: s must be fp32");
+  const int64_t D = sv.size(-1), T = sv.numel() / D;
+  TORCH_CHECK(dpt::ln_supported(D), "ln_bwd: unsupported width ", D);
+  const int kind = act16_kind(gh, "ln_bwd: grad_h");
+  TORCH_CHECK(gh.sizes() == sv.sizes(), "ln_bwd: grad_h must match s");
+  TORCH_CHECK(mean.numel() == T && rstd.numel() == T, "ln_bwd: mean/rstd must have one entry per row");
+  const float* gsp = nullptr;
+  if (gs.has_value() && gs->defined()) {
+    TORCH_CHECK(gs->scalar_type() == at::kFloat && gs->is_contiguous() && gs->sizes() == sv.sizes(),
+                "ln_bwd: grad_s must be contiguous fp32 like s");
+    gsp = gs->data_ptr<float>();
+  }
+  auto fopt = sv.options().dtype(at::kFloat);
+  auto gx = at::empty_like(sv);
+  Tensor ga = want_ga ? at::empty(sv.sizes(), sv.options().dtype(kind_dtype(kind))) : Tensor();
+  Tensor dg = want_dparams ? at::empty({D}, fopt) : Tensor();
+  Tensor db = want_dparams ? at::empty({D}, fopt) : Tensor();
+  Tensor dbias;
+  int dbk = 0;
+  if (want_ga && bias_like.has_value() && bias_like->defined()) {
+    dbk = param_kind(*bias_like, D, "ln_bwd: bias");
+    dbias = at::empty({D}, sv.options().dtype(bias_like->scalar_type()));
+  }
+  auto part = at::empty({3 * (int64_t)dpt::ln_bwd_blocks(T) * D}, fopt);
+  c10::hip::HIPGuard guard(sv.device().index());
+  dpt::launch_ln_bwd(kind, gsp, static_cast<const uint16_t*>(gh.data_ptr()), sv.data_ptr<float>(),
+                     mean.data_ptr<float>(), rstd.data_ptr<float>(), f32_param(gamma, D, "gamma"), gx.data_ptr<float>(),
+                     want_ga ? static_cast<uint16_t*>(ga.data_ptr()) : nullptr, part.data_ptr<float>(),
+                     want_dparams ? dg.data_ptr<float>() : nullptr, want_dparams ? db.data_ptr<float>() : nullptr,
+                     dbias.defined() ? dbias.data_ptr() : nullptr, dbk, T, D, cur_stream(sv));
+  return {gx, ga, dg, db, dbias};
+}
+
+Tensor gelu_fwd(Tensor u, c10::optional<Tensor> bias) {
+  const int kind = act16_kind(u, "gelu: u");
+  const int64_t F = u.size(-1), T = u.numel() / F;
+  TORCH_CHECK(F % 8 == 0, "gelu: width must be a multiple of 8");
+  const void* bp = nullptr;
+  int bk = 0;
+  if (bias.has_value() && bias->defined()) {
+    bk = param_kind(*bias, F, "gelu: bias");
+    bp = bias->data_ptr();
+  }
+  auto h = at::empty_like(u);
+  c10::hip::HIPGuard guard(u.device().index());
+  dpt::launch_gelu_fwd(kind, static_cast<const uint16_t*>(u.data_ptr()), bp, bk, static_cast<uint16_t*>(h.data_ptr()),
+                       T, F, cur_stream(u));
+  return h;
+}
+
+// Returns {gu, dbias}: gu = gh * gelu'(u + bias); dbias = column sums of gu (bias dtype).
+std::vector<Tensor> gelu_bwd(Tensor gh, Tensor u, c10::optional<Tensor> bias, bool want_dbias) {
+  const int kind = act16_kind(u, "gelu_bwd: u");
+  TORCH_CHECK(act16_kind(gh, "gelu_bwd: grad") == kind && gh.sizes() == u.sizes(), "gelu_bwd: grad must match u");
+  const int64_t F = u.size(-1), T = u.numel() / F;
+  TORCH_CHECK(F % 8 == 0, "gelu_bwd: width must be a multiple of 8");
+  const void* bp = nullptr;
+  int bk = 0;
+  if (bias.has_value() && bias->defined()) {
+    bk = param_kind(*bias, F, "gelu_bwd: bias");
+    bp = bias->data_ptr();
+  }
+  auto gu = at::empty_like(u);
+  Tensor db = (want_dbias && bp) ? at::empty({F}, u.options().dtype(bias->scalar_type())) : Tensor();
+  auto part = at::empty({(int64_t)dpt::gelu_bwd_chunks(T, F) * F}, u.options().dtype(at::kFloat));
+  c10::hip::HIPGuard guard(u.device().index());
+  dpt::launch_gelu_bwd(kind, static_cast<const uint16_t*>(gh.data_ptr()), static_cast<const uint16_t*>(u.data_ptr()),
+                       bp, bk, static_cast<uint16_t*>(gu.data_ptr()), part.data_ptr<float>(),
+                       db.defined() ? db.data_ptr() : nullptr, bk, T, F, cur_stream(u));
+  return {gu, db};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -351,7 +487,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("residual"), py::arg("a"), py::arg("b"), py::arg("relu"));
   m.def("bn_bwd", &bn_bwd, py::arg("grad_output"), py::arg("grad_output2"), py::arg("y"), py::arg("x"),
         py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("relu"), py::arg("want_dz"),
-        py::arg("want_dparams"));
+        py::arg("want_dparams"), py::arg("coef") = py::none());
+  m.def("ln_supported", &dpt::ln_supported, py::arg("D"));
+  m.def("ln_fwd", &ln_fwd, py::arg("x"), py::arg("a"), py::arg("bias"), py::arg("gamma"), py::arg("beta"),
+        py::arg("eps"), py::arg("out_kind") = 1);
+  m.def("ln_bwd", &ln_bwd, py::arg("grad_s"), py::arg("grad_h"), py::arg("s"), py::arg("mean"), py::arg("rstd"),
+        py::arg("gamma"), py::arg("want_ga"), py::arg("bias_like"), py::arg("want_dparams"));
+  m.def("gelu_fwd", &gelu_fwd, py::arg("u"), py::arg("bias"));
+  m.def("gelu_bwd", &gelu_bwd, py::arg("grad"), py::arg("u"), py::arg("bias"), py::arg("want_dbias"));
   m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("stride"), py::arg("pad"));
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("grad_output"), py::arg("idx"), py::arg("H"), py::arg("W"),
         py::arg("k"), py::arg("stride"), py::arg("pad"));

@@ -243,8 +243,8 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(const void* __rest
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float o0 = v0[k] * a[k] + b[k];
-      float o1 = v1[k] * a[k] + b[k];
+      float o0 = __builtin_fmaf(v0[k], a[k], b[k]);  // bwd mask-from-x recomputes exactly this
+      float o1 = __builtin_fmaf(v1[k], a[k], b[k]);
       if (RES) { o0 += q0[k]; o1 += q1[k]; }
       if (RELU) {  // NaN-propagating like torch.relu (a NaN must still reach the AMP check)
         o0 = o0 < 0.0f ? 0.0f : o0;
@@ -258,17 +258,33 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(const void* __rest
   }
 }
 
+// ReLU mask of one 8-channel vector: from the saved output (y > 0) or, MX, recomputed from
+// the BN input with the forward's own coefficients (fma(x, a, b) > 0 - the exact value the
+// forward apply clamped), which saves reading y in both backward passes.
+template <typename IO, bool MX>
+__device__ __forceinline__ void relu_mask8(const void* y, int64_t off, const float xv[8], const float a[8],
+                                           const float b[8], bool m[8]) {
+  if (MX) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[k] = __builtin_fmaf(xv[k], a[k], b[k]) > 0.0f;
+  } else {
+    IO::pos8(y, off, m);
+  }
+}
+
 // ---- backward statistics: s1 = sum dz, s2 = sum dz*(x-mean), dz = (dy [+ dy2]) * (y > 0) ------
 // TWO: the output had two consumers (conv path + identity path of the next residual block,
 // see ops/bn.py "pair" outputs); their gradients arrive separately and are summed here
 // instead of in an autograd add kernel.  WDZ: also store dz (it is the residual-path
-// gradient dres, and the apply pass then reads dz instead of dy, dy2 and y).
-template <typename IO, bool RELU, bool TWO, bool WDZ, int UNR>
+// gradient dres, and the apply pass then reads dz instead of dy, dy2 and y).  MX: ReLU mask
+// recomputed from x and the forward coefficients coef = [a | b] (non-residual BN+ReLU).
+template <typename IO, bool RELU, bool TWO, bool WDZ, int UNR, bool MX>
 __global__ __launch_bounds__(kBlock) void bn_bwd_stats_kernel(const void* __restrict__ dy,
                                                               const void* __restrict__ dy2,
                                                               const void* __restrict__ y,
                                                               const void* __restrict__ x,
-                                                              const float* __restrict__ mean, int64_t M,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ coef, int64_t M,
                                                               int C, int64_t rows_per_chunk, int chunks,
                                                               float* __restrict__ p1,
                                                               float* __restrict__ p2,
@@ -276,9 +292,13 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_stats_kernel(const void* __rest
   __shared__ float lds[2 * kBlock * 8];
   const int tpr = C >> 3, rpi = kBlock / tpr;
   const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
-  float mu[8];
+  float mu[8], fa[8], fb[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) mu[k] = mean[cg * 8 + k];
+  for (int k = 0; k < 8; ++k) {
+    mu[k] = mean[cg * 8 + k];
+    fa[k] = MX ? coef[cg * 8 + k] : 0.f;
+    fb[k] = MX ? coef[C + cg * 8 + k] : 0.f;
+  }
   const int64_t row0 = (int64_t)blockIdx.x * rows_per_chunk;
   const int64_t row1 = min(row0 + rows_per_chunk, M);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -292,7 +312,11 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_stats_kernel(const void* __rest
       IO::load8(dy, off, g[u]);
       if (TWO) IO::load8(dy2, off, g2[u]);
       IO::load8(x, off, xv[u]);
-      if (RELU) IO::pos8(y, off, m[u]);
+      if (RELU && !MX) IO::pos8(y, off, m[u]);
+    }
+    if (RELU && MX) {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) relu_mask8<IO, true>(y, 0, xv[u], fa, fb, m[u]);
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
@@ -314,7 +338,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_stats_kernel(const void* __rest
     IO::load8(dy, off, g);
     if (TWO) IO::load8(dy2, off, g2);
     IO::load8(x, off, xv);
-    if (RELU) IO::pos8(y, off, m);
+    if (RELU) relu_mask8<IO, MX>(y, off, xv, fa, fb, m);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float gk = TWO ? g[k] + g2[k] : g[k];
@@ -362,25 +386,29 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(
   k3[c] = (float)(-a * s1 / (double)M);
 }
 
-// dx = k1*dz + k2*(x - mean) + k3, dz = dy*(y>0) recomputed (RELU) or read back (FROM_DZ).
-template <typename IO, bool RELU, bool FROM_DZ>
+// dx = k1*dz + k2*(x - mean) + k3, dz = dy*(y>0) recomputed (RELU; mask from x if MX) or
+// read back (FROM_DZ).
+template <typename IO, bool RELU, bool FROM_DZ, bool MX>
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const void* __restrict__ dy,
                                                               const void* __restrict__ y,
                                                               const void* __restrict__ x,
                                                               const float* __restrict__ mean,
+                                                              const float* __restrict__ coef,
                                                               const float* __restrict__ k1,
                                                               const float* __restrict__ k2,
                                                               const float* __restrict__ k3, void* dx,
                                                               int64_t M, int C) {
   const int tpr = C >> 3, rpi = kBlock / tpr;
   const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
-  float mu[8], c1[8], c2[8], c3[8];
+  float mu[8], c1[8], c2[8], c3[8], fa[8], fb[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     mu[k] = mean[cg * 8 + k];
     c1[k] = k1[cg * 8 + k];
     c2[k] = k2[cg * 8 + k];
     c3[k] = k3[cg * 8 + k];
+    fa[k] = MX ? coef[cg * 8 + k] : 0.f;
+    fb[k] = MX ? coef[C + cg * 8 + k] : 0.f;
   }
   const int64_t stride = (int64_t)gridDim.x * rpi;
   for (int64_t r = (int64_t)blockIdx.x * rpi + rr; r < M; r += stride) {
@@ -388,7 +416,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const void* __rest
     bool m[8];
     IO::load8(dy, r * C + cg * 8, g);
     IO::load8(x, r * C + cg * 8, xv);
-    if (RELU && !FROM_DZ) IO::pos8(y, r * C + cg * 8, m);
+    if (RELU && !FROM_DZ) relu_mask8<IO, MX>(y, r * C + cg * 8, xv, fa, fb, m);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float dz = (FROM_DZ || !RELU || m[k]) ? g[k] : 0.0f;
@@ -449,11 +477,11 @@ static void fwd_apply_dispatch(bool relu, bool res, const void* x, const void* r
 void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                          const float* gamma, const float* beta, float eps, float momentum, float* run_mean,
                          float* run_var, int64_t* num_batches, float* save_mean, float* save_invstd,
-                         float* workspace, bool relu, hipStream_t s) {
+                         float* save_coef, float* workspace, bool relu, hipStream_t s) {
   BnGeometry g = bn_geometry(M, C);
   float* psum = workspace;
   float* psq = psum + (int64_t)C * g.chunks;
-  float* ca = psq + (int64_t)C * g.chunks;
+  float* ca = save_coef ? save_coef : psq + (int64_t)C * g.chunks;
   float* cb = ca + C;
   dim3 bl(kBlock);
   switch (dtype) {
@@ -482,45 +510,52 @@ void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t
 
 template <typename IO, int UNR>
 static void bwd_stats_dispatch(bool relu, const void* dy, const void* dy2, const void* y, const void* x,
-                               const float* mean, int64_t M, int C, const BnGeometry& g, float* p1, float* p2,
-                               void* dz, hipStream_t s) {
+                               const float* mean, const float* coef, int64_t M, int C, const BnGeometry& g,
+                               float* p1, float* p2, void* dz, hipStream_t s) {
   dim3 bl(kBlock), gs(g.chunks);
   const int64_t rpc = g.rows_per_chunk;
+#define DPT_BN_STATS(R, T, W, MXV) \
+  hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, R, T, W, UNR, MXV>), gs, bl, 0, s, dy, dy2, y, x, mean, coef, M, C, \
+                     rpc, g.chunks, p1, p2, dz)
   if (dz != nullptr) {  // dz written by the stats pass, read back by the apply pass
-    if (relu && dy2) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true, true, true, UNR>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
-    else if (relu) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true, false, true, UNR>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
-    else if (dy2) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false, true, true, UNR>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
-    else hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false, false, true, UNR>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+    if (relu && dy2) DPT_BN_STATS(true, true, true, false);
+    else if (relu) DPT_BN_STATS(true, false, true, false);
+    else if (dy2) DPT_BN_STATS(false, true, true, false);
+    else DPT_BN_STATS(false, false, true, false);
   } else {
-    if (relu) hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, true, false, false, UNR>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
-    else hipLaunchKernelGGL((bn_bwd_stats_kernel<IO, false, false, false, UNR>), gs, bl, 0, s, dy, dy2, y, x, mean, M, C, rpc, g.chunks, p1, p2, dz);
+    if (relu && coef) DPT_BN_STATS(true, false, false, true);
+    else if (relu) DPT_BN_STATS(true, false, false, false);
+    else DPT_BN_STATS(false, false, false, false);
   }
+#undef DPT_BN_STATS
 }
 
 template <typename IO>
 static void bwd_dispatch(bool relu, const void* dy, const void* dy2, const void* y, const void* x,
-                         const float* mean, int64_t M, int C, const BnGeometry& g, float* p1, float* p2,
-                         const float* gamma, const float* invstd, float* dgamma, float* dbeta, float* k1,
-                         float* k2, float* k3, void* dx, void* dz, hipStream_t s) {
+                         const float* mean, const float* coef, int64_t M, int C, const BnGeometry& g, float* p1,
+                         float* p2, const float* gamma, const float* invstd, float* dgamma, float* dbeta,
+                         float* k1, float* k2, float* k3, void* dx, void* dz, hipStream_t s) {
   dim3 bl(kBlock);
   if (kBnBwdUnroll == 4) {
-    bwd_stats_dispatch<IO, 4>(relu, dy, dy2, y, x, mean, M, C, g, p1, p2, dz, s);
+    bwd_stats_dispatch<IO, 4>(relu, dy, dy2, y, x, mean, coef, M, C, g, p1, p2, dz, s);
   } else {
-    bwd_stats_dispatch<IO, 2>(relu, dy, dy2, y, x, mean, M, C, g, p1, p2, dz, s);
+    bwd_stats_dispatch<IO, 2>(relu, dy, dy2, y, x, mean, coef, M, C, g, p1, p2, dz, s);
   }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p2, g.chunks, C, M, gamma,
                      invstd, dgamma, dbeta, k1, k2, k3);
   dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
-  if (dz != nullptr) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, true>), ga, bl, 0, s, dz, y, x, mean, k1, k2, k3, dx, M, C);
-  else if (relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false>), ga, bl, 0, s, dy, y, x, mean, k1, k2, k3, dx, M, C);
-  else hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, false>), ga, bl, 0, s, dy, y, x, mean, k1, k2, k3, dx, M, C);
+  if (dz != nullptr) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, true, false>), ga, bl, 0, s, dz, y, x, mean, coef, k1, k2, k3, dx, M, C);
+  else if (relu && coef) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false, true>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C);
+  else if (relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false, false>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C);
+  else hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, false, false>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C);
 }
 
 // dz: if non-null, receives dz = (dy [+ dy2]) * relu_mask (the residual-path gradient);
-// required when dy2 is given.
+// required when dy2 is given.  coef: the forward's [a | b] (2C floats); when given (and no dz),
+// the ReLU mask is recomputed from x and y is not read.
 void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, const void* x, int64_t M,
-                   int64_t C, const float* gamma, const float* mean, const float* invstd, float* dgamma,
-                   float* dbeta, void* dx, void* dz, float* workspace, bool relu, hipStream_t s) {
+                   int64_t C, const float* gamma, const float* mean, const float* invstd, const float* coef,
+                   float* dgamma, float* dbeta, void* dx, void* dz, float* workspace, bool relu, hipStream_t s) {
   BnGeometry g = bn_geometry(M, C);
   float* p1 = workspace;
   float* p2 = p1 + (int64_t)C * g.chunks;
@@ -528,9 +563,9 @@ void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, co
   float* k2 = k1 + C;
   float* k3 = k2 + C;
   switch (dtype) {
-    case 0: bwd_dispatch<F32>(relu, dy, dy2, y, x, mean, M, (int)C, g, p1, p2, gamma, invstd, dgamma, dbeta, k1, k2, k3, dx, dz, s); break;
-    case 1: bwd_dispatch<BF16>(relu, dy, dy2, y, x, mean, M, (int)C, g, p1, p2, gamma, invstd, dgamma, dbeta, k1, k2, k3, dx, dz, s); break;
-    default: bwd_dispatch<F16>(relu, dy, dy2, y, x, mean, M, (int)C, g, p1, p2, gamma, invstd, dgamma, dbeta, k1, k2, k3, dx, dz, s); break;
+    case 0: bwd_dispatch<F32>(relu, dy, dy2, y, x, mean, dz ? nullptr : coef, M, (int)C, g, p1, p2, gamma, invstd, dgamma, dbeta, k1, k2, k3, dx, dz, s); break;
+    case 1: bwd_dispatch<BF16>(relu, dy, dy2, y, x, mean, dz ? nullptr : coef, M, (int)C, g, p1, p2, gamma, invstd, dgamma, dbeta, k1, k2, k3, dx, dz, s); break;
+    default: bwd_dispatch<F16>(relu, dy, dy2, y, x, mean, dz ? nullptr : coef, M, (int)C, g, p1, p2, gamma, invstd, dgamma, dbeta, k1, k2, k3, dx, dz, s); break;
   }
 }
 

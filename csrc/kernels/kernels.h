@@ -55,12 +55,12 @@ int64_t bn_workspace_floats(int64_t M, int64_t C);
 void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                          const float* gamma, const float* beta, float eps, float momentum, float* run_mean,
                          float* run_var, int64_t* num_batches, float* save_mean, float* save_invstd,
-                         float* workspace, bool relu, hipStream_t s);
+                         float* save_coef, float* workspace, bool relu, hipStream_t s);
 void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                      const float* coef_a, const float* coef_b, bool relu, hipStream_t s);
 void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, const void* x, int64_t M,
-                   int64_t C, const float* gamma, const float* mean, const float* invstd, float* dgamma,
-                   float* dbeta, void* dx, void* dz, float* workspace, bool relu, hipStream_t s);
+                   int64_t C, const float* gamma, const float* mean, const float* invstd, const float* coef,
+                   float* dgamma, float* dbeta, void* dx, void* dz, float* workspace, bool relu, hipStream_t s);
 
 // pool_kernels.hip  (channels_last [B,H,W,C], C % 8 == 0; idx = window-local uint8 argmax)
 void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t B, int H, int W, int C, int Ho,
@@ -78,5 +78,23 @@ struct GatherBatch {
   int count;
 };
 void launch_gather(const GatherBatch& batch, bool accumulate, hipStream_t s);
+
+// vit_kernels.hip  (kind: 1 bf16, 2 fp16 for the 16-bit activations; param kinds 0 f32 / 1 bf16 /
+// 2 fp16; rows are tokens, LayerNorm width D % 256 == 0, GELU width F % 8 == 0)
+bool ln_supported(int64_t D);
+int ln_bwd_blocks(int64_t T);
+int gelu_bwd_chunks(int64_t T, int64_t F);
+void launch_ln_fwd(int kind, const float* x, const uint16_t* a, const void* bias, int bias_kind, const float* gamma,
+                   const float* beta, float* s_out, uint16_t* h_out, float* mean, float* rstd, int64_t T, int64_t D,
+                   float eps, hipStream_t s);
+// part: 3 * ln_bwd_blocks(T) * D floats of scratch
+void launch_ln_bwd(int kind, const float* gs, const uint16_t* gh, const float* sv, const float* mean,
+                   const float* rstd, const float* gamma, float* gx, uint16_t* ga, float* part, float* dgamma,
+                   float* dbeta, void* dbias, int dbias_kind, int64_t T, int64_t D, hipStream_t s);
+void launch_gelu_fwd(int kind, const uint16_t* u, const void* bias, int bias_kind, uint16_t* h, int64_t T, int64_t F,
+                     hipStream_t s);
+// part: gelu_bwd_chunks(T, F) * F floats of scratch
+void launch_gelu_bwd(int kind, const uint16_t* gh, const uint16_t* u, const void* bias, int bias_kind, uint16_t* gu,
+                     float* part, void* dbias, int dbias_kind, int64_t T, int64_t F, hipStream_t s);
 
 }  // namespace dpt

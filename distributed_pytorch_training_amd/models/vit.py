@@ -11,6 +11,11 @@ MI355X notes
   training path.  The parameters keep ``nn.MultiheadAttention``'s names (``in_proj_weight``,
   ``in_proj_bias``, ``out_proj.*``) so state dicts load into torchvision unchanged.
 * 197 tokens (14x14 patches + CLS): no sequence sharding is needed.
+* Under bf16/fp16 autocast on the GPU the encoder runs a fused path (ops/vit.py,
+  csrc/kernels/vit_kernels.hip): each residual add + branch bias + LayerNorm is one kernel
+  that writes the 16-bit GEMM operand directly, fc1's bias + GELU is one kernel, and the
+  backward passes fold the bias-gradient column sums and residual-gradient adds into the
+  same passes.  The branch GEMMs run bias-free; parameter names/shapes are unchanged.
 """
 from __future__ import annotations
 
@@ -20,6 +25,9 @@ from collections import OrderedDict
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from ..ops.vit import add_bias_layer_norm16, bias_gelu16, layer_norm16, ln_fusable
+from ..parallel.shadow import shadow_param
 
 
 class SelfAttention(nn.Module):
@@ -35,14 +43,22 @@ class SelfAttention(nn.Module):
         nn.init.xavier_uniform_(self.in_proj_weight)
         nn.init.zeros_(self.out_proj.bias)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def _context(self, x: torch.Tensor) -> torch.Tensor:
         b, s, d = x.shape
-        from ..parallel.shadow import shadow_param
         qkv = F.linear(x, shadow_param(self, "in_proj_weight", x), shadow_param(self, "in_proj_bias", x))
-        qkv = qkv.view(b, s, 3, self.heads, d // self.heads).permute(2, 0, 3, 1, 4)
-        y = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2],
-                                           dropout_p=self.dropout if self.training else 0.0)
-        return self.out_proj(y.transpose(1, 2).reshape(b, s, d))
+        # unbind (backward = one stack) instead of three selects (backward = zero-fill + 3 copies)
+        q, k, v = qkv.view(b, s, 3, self.heads, d // self.heads).permute(2, 0, 3, 1, 4).unbind(0)
+        y = F.scaled_dot_product_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0)
+        return y.transpose(1, 2).reshape(b, s, d)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.out_proj(self._context(x))
+
+    def attend_nobias(self, x: torch.Tensor):
+        """(out_proj(context) without its bias, the bias) - the fused path adds the bias in
+        the following add+LayerNorm kernel."""
+        y = self._context(x)
+        return F.linear(y, shadow_param(self.out_proj, "weight", y)), shadow_param(self.out_proj, "bias", y)
 
 
 class MLPBlock(nn.Sequential):
@@ -83,7 +99,37 @@ class Encoder(nn.Module):
         self.ln = nn.LayerNorm(dim, eps=1e-6)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self._fused_ok(x):
+            return self._forward_fused(x)
         return self.ln(self.layers(self.dropout(x + self.pos_embedding)))
+
+    def _fused_ok(self, x: torch.Tensor) -> bool:
+        if not (x.is_cuda and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16)):
+            return False
+        if not ln_fusable(x, x.shape[-1]):
+            return False
+        if self.training and any(isinstance(m, nn.Dropout) and m.p > 0 for m in self.modules()):
+            return False
+        blk = self.layers[0]
+        return (blk.mlp[0].out_features % 8 == 0 and not (self.training and blk.self_attention.dropout > 0))
+
+    def _forward_fused(self, x: torch.Tensor) -> torch.Tensor:
+        dt = torch.get_autocast_dtype("cuda")
+        x = (x + self.pos_embedding).float().contiguous()
+        pending = None                    # (branch GEMM output without bias, its bias)
+        for blk in self.layers:
+            if pending is None:
+                h = layer_norm16(x, blk.ln_1, dt)
+            else:
+                x, h = add_bias_layer_norm16(x, pending[0], pending[1], blk.ln_1)
+            a, ab = blk.self_attention.attend_nobias(h)
+            x, h2 = add_bias_layer_norm16(x, a, ab, blk.ln_2)
+            fc1, fc2 = blk.mlp[0], blk.mlp[3]
+            u = F.linear(h2, shadow_param(fc1, "weight", h2))
+            g = bias_gelu16(u, shadow_param(fc1, "bias", h2))
+            pending = (F.linear(g, shadow_param(fc2, "weight", g)), shadow_param(fc2, "bias", g))
+        return add_bias_layer_norm16(x, pending[0], pending[1], self.ln)[1]
 
 
 class VisionTransformer(nn.Module):

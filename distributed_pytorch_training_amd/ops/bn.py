@@ -6,9 +6,12 @@ statistics, biased variance for normalisation, unbiased for the running variance
 the running statistics in eval mode - the composition the reference's ResNet blocks run as
 separate MIOpen/ATen kernels (BN, in-place add, in-place ReLU).
 
-Saved for backward: the BN input ``x`` and (with ReLU) the output ``y`` - the same tensors
-the unfused graph keeps alive (BN saves its input, ReLU its output, and ``y`` is the next
-convolution's saved input anyway), so the fusion costs no extra activation memory.
+Saved for backward: the BN input ``x`` and, for BN+add+ReLU, the output ``y`` - tensors the
+unfused graph keeps alive anyway (BN saves its input, ReLU its output, and ``y`` is the next
+convolution's saved input), so the fusion costs no extra activation memory.  For BN+ReLU
+without a residual the ReLU mask is recomputed from ``x`` and the forward's per-channel
+coefficients (``fma(x, a, b) > 0``, bit-identical to the forward's decision), so the backward
+passes never read ``y``: 2 of 7 activation passes saved per such layer.
 """
 from __future__ import annotations
 
@@ -28,12 +31,7 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
 class _BNActTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu):
-        C = native()
-        y, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var, num_batches,
-                                         float(momentum), float(eps), bool(relu))
-        ctx.relu = bool(relu)
-        ctx.has_res = residual is not None
-        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        y = _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu)
         return y
 
     @staticmethod
@@ -50,12 +48,8 @@ class _BNActTrainPair(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu):
-        C = native()
-        y, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var, num_batches,
-                                         float(momentum), float(eps), bool(relu))
-        ctx.relu = bool(relu)
-        ctx.has_res = residual is not None
-        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        y = _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
+                 pair=True)
         ctx.set_materialize_grads(False)  # an unused alias (last block) gives None, not zeros
         return y, y.view_as(y)
 
@@ -64,8 +58,20 @@ class _BNActTrainPair(torch.autograd.Function):
         return _bwd(ctx, dy, dy2) + (None,) * 6
 
 
+def _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
+         pair=False):
+    y, mean, invstd, coef = native().bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
+                                                  num_batches, float(momentum), float(eps), bool(relu))
+    ctx.relu = bool(relu)
+    ctx.has_res = residual is not None
+    mask_from_x = ctx.relu and not ctx.has_res and not pair   # pair outputs always write dz
+    ctx.save_for_backward(x, y if (relu and not mask_from_x) else None, weight, mean, invstd,
+                          coef if mask_from_x else None)
+    return y
+
+
 def _bwd(ctx, dy, dy2):
-    x, y, weight, mean, invstd = ctx.saved_tensors
+    x, y, weight, mean, invstd, coef = ctx.saved_tensors
     if dy is None:
         dy, dy2 = dy2, None
     if dy is None:
@@ -73,7 +79,7 @@ def _bwd(ctx, dy, dy2):
     want_params = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
     want_dz = ctx.has_res and ctx.needs_input_grad[1]
     dx, dg, db, dz = native().bn_bwd(_cl(dy), None if dy2 is None else _cl(dy2), y, x, weight, mean, invstd,
-                                     ctx.relu, bool(want_dz), bool(want_params))
+                                     ctx.relu, bool(want_dz), bool(want_params), coef)
     return (dx, dz if want_dz else None, dg if want_params else None, db if want_params else None)
 
 

@@ -1,0 +1,112 @@
+"""Fused transformer-block ops for ViT on the gfx950 kernels (csrc/kernels/vit_kernels.hip).
+
+* ``layer_norm16(x, ln)``               h = LayerNorm(x) written directly in 16 bits
+* ``add_bias_layer_norm16(x, a, b, ln)`` s = x + a + b (fp32 residual stream), h = LayerNorm(s)
+                                        in 16 bits; backward gives the residual gradient,
+                                        the branch gradient (16-bit) and the branch bias
+                                        gradient in one pass
+* ``bias_gelu16(u, b)``                 gelu(u + b) (exact erf), backward with the bias-gradient
+                                        column sums fused
+
+``a`` / ``u`` are the outputs of bias-free GEMMs (``F.linear(h, W)``): the bias add moves into
+these kernels so the bias gradient falls out of the pass that already reads the gradient
+(no separate column-sum kernel per Linear).  Semantics equal the unfused PyTorch composition
+under autocast up to rounding order (the fused path adds the bias in fp32 before rounding,
+PyTorch rounds the GEMM+bias output to bf16 first); tests compare both against fp32.
+
+CPU tensors run the PyTorch composition (same function signatures) so the model code has
+one path.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import native, native_available
+
+_KIND = {torch.bfloat16: 1, torch.float16: 2}
+
+
+def ln_fusable(x: torch.Tensor, dim: int) -> bool:
+    return x.is_cuda and native_available() and native().ln_supported(dim)
+
+
+def _c(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    return None if t is None else t.contiguous()
+
+
+class _LayerNorm16(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, kind):
+        _, h, mean, rstd = native().ln_fwd(x, None, None, weight, bias, float(eps), int(kind))
+        ctx.save_for_backward(x, weight, mean, rstd)
+        return h
+
+    @staticmethod
+    def backward(ctx, gh):
+        x, weight, mean, rstd = ctx.saved_tensors
+        want_p = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        gx, _, dg, db, _ = native().ln_bwd(None, gh.contiguous(), x, mean, rstd, weight, False, None, want_p)
+        return gx, (dg if want_p else None), (db if want_p else None), None, None
+
+
+class _AddBiasLayerNorm16(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, a, abias, weight, bias, eps):
+        s, h, mean, rstd = native().ln_fwd(x, a, abias, weight, bias, float(eps), 1)
+        ctx.save_for_backward(s, weight, mean, rstd, abias)
+        ctx.a_dtype = a.dtype
+        ctx.set_materialize_grads(False)
+        return s, h
+
+    @staticmethod
+    def backward(ctx, gs, gh):
+        s, weight, mean, rstd, abias = ctx.saved_tensors
+        if gh is None:  # only the residual stream is used downstream: LN contributes nothing
+            ga = None if gs is None else gs.to(ctx.a_dtype)
+            return gs, ga, (None if gs is None or abias is None else gs.flatten(0, -2).sum(0).to(abias.dtype)), \
+                None, None, None
+        want_p = ctx.needs_input_grad[3] or ctx.needs_input_grad[4]
+        gx, ga, dg, db, dab = native().ln_bwd(_c(gs), gh.contiguous(), s, mean, rstd, weight, True,
+                                              abias, want_p)
+        return (gx, ga, dab if abias is not None else None, dg if want_p else None,
+                db if want_p else None, None)
+
+
+class _BiasGELU16(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, u, bias):
+        ctx.save_for_backward(u, bias)
+        return native().gelu_fwd(u, bias)
+
+    @staticmethod
+    def backward(ctx, gh):
+        u, bias = ctx.saved_tensors
+        gu, db = native().gelu_bwd(gh.contiguous(), u, bias, bias is not None and ctx.needs_input_grad[1])
+        return gu, (db if bias is not None and ctx.needs_input_grad[1] else None)
+
+
+# ---------------------------------------------------------------------------------------------
+def layer_norm16(x: torch.Tensor, ln: torch.nn.LayerNorm, dtype: torch.dtype) -> torch.Tensor:
+    """LayerNorm(x) (x fp32) returned in ``dtype`` (bf16/fp16)."""
+    if x.is_cuda:
+        return _LayerNorm16.apply(x.contiguous(), ln.weight, ln.bias, ln.eps, _KIND[dtype])
+    return F.layer_norm(x, ln.normalized_shape, ln.weight, ln.bias, ln.eps).to(dtype)
+
+
+def add_bias_layer_norm16(x: torch.Tensor, a: torch.Tensor, abias: Optional[torch.Tensor],
+                          ln: torch.nn.LayerNorm) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(s, h) with s = x + a + abias (fp32) and h = LayerNorm(s) in a's dtype."""
+    if x.is_cuda:
+        return _AddBiasLayerNorm16.apply(x.contiguous(), a.contiguous(), abias, ln.weight, ln.bias, ln.eps)
+    s = x + a.float() + (abias.float() if abias is not None else 0.0)
+    return s, F.layer_norm(s, ln.normalized_shape, ln.weight, ln.bias, ln.eps).to(a.dtype)
+
+
+def bias_gelu16(u: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    if u.is_cuda:
+        return _BiasGELU16.apply(u.contiguous(), bias)
+    z = u.float() + (bias.float() if bias is not None else 0.0)
+    return F.gelu(z).to(u.dtype)

@@ -21,7 +21,10 @@ def setup_miopen_env(scratch: str | None = None) -> str:
     """Point MIOpen's user find-db / kernel cache at writable dirs seeded from the repo."""
     if "MIOPEN_USER_DB_PATH" in os.environ:
         return os.environ["MIOPEN_USER_DB_PATH"]
-    base = Path(scratch or os.environ.get("DPT_SCRATCH", "/tmp")) / f"dpt_miopen_{os.getuid()}"
+    # one directory per local rank: N ranks starting together never read a database another
+    # rank is still copying, and never contend for MIOpen's sqlite kernel-cache lock
+    lr = os.environ.get("LOCAL_RANK", "0")
+    base = Path(scratch or os.environ.get("DPT_SCRATCH", "/tmp")) / f"dpt_miopen_{os.getuid()}_r{lr}"
     db = base / "db"
     cache = base / "cache"
     db.mkdir(parents=True, exist_ok=True)
@@ -34,7 +37,9 @@ def setup_miopen_env(scratch: str | None = None) -> str:
             # seeds the kernel cache so a fresh box does not recompile MIOpen's kernels.
             dst = (cache if f.suffix == ".ukdb" else db) / f.name
             if not dst.exists():
-                shutil.copy2(f, dst)
+                tmp = dst.with_name(f"{dst.name}.{os.getpid()}.tmp")
+                shutil.copy2(f, tmp)
+                os.replace(tmp, dst)       # atomic: readers see all or nothing
     os.environ["MIOPEN_USER_DB_PATH"] = str(db)
     os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", str(cache))
     return str(db)
