@@ -224,16 +224,19 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(const void* __rest
                                                               void* __restrict__ y,
                                                               const float* __restrict__ coef_a,
                                                               const float* __restrict__ coef_b,
-                                                              int64_t M, int C) {
+                                                              int64_t M, int C, int rev) {
   const int tpr = C >> 3, rpi = kBlock / tpr;
   const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
   float a[8], b[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { a[k] = coef_a[cg * 8 + k]; b[k] = coef_b[cg * 8 + k]; }
   const int64_t stride = (int64_t)gridDim.x * rpi;
-  for (int64_t r = (int64_t)blockIdx.x * rpi + rr; r < M; r += 2 * stride) {
-    const int64_t r2 = r + stride;
-    const bool two = r2 < M;
+  for (int64_t rf = (int64_t)blockIdx.x * rpi + rr; rf < M; rf += 2 * stride) {
+    const bool two = rf + stride < M;
+    // rev: walk the rows last-to-first so the first blocks re-read what the stats pass
+    // touched last (still resident in the 256 MB Infinity Cache / L2)
+    const int64_t r = rev ? M - 1 - rf : rf;
+    const int64_t r2 = rev ? r - stride : r + stride;
     float v0[8], v1[8], q0[8], q1[8];
     IO::load8(x, r * C + cg * 8, v0);
     if (two) IO::load8(x, r2 * C + cg * 8, v1);
@@ -397,7 +400,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const void* __rest
                                                               const float* __restrict__ k1,
                                                               const float* __restrict__ k2,
                                                               const float* __restrict__ k3, void* dx,
-                                                              int64_t M, int C) {
+                                                              int64_t M, int C, int rev) {
   const int tpr = C >> 3, rpi = kBlock / tpr;
   const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
   float mu[8], c1[8], c2[8], c3[8], fa[8], fb[8];
@@ -411,7 +414,8 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const void* __rest
     fb[k] = MX ? coef[C + cg * 8 + k] : 0.f;
   }
   const int64_t stride = (int64_t)gridDim.x * rpi;
-  for (int64_t r = (int64_t)blockIdx.x * rpi + rr; r < M; r += stride) {
+  for (int64_t rf = (int64_t)blockIdx.x * rpi + rr; rf < M; rf += stride) {
+    const int64_t r = rev ? M - 1 - rf : rf;  // see bn_fwd_apply_kernel
     float g[8], xv[8], o[8];
     bool m[8];
     IO::load8(dy, r * C + cg * 8, g);
@@ -446,6 +450,7 @@ static const int kBnMaxChunks = env_int("DPT_BN_MAX_CHUNKS", 512);
 static const int kBnBwdUnroll = env_int("DPT_BN_BWD_UNROLL", 2);
 static const int kBnApplyMax = env_int("DPT_BN_APPLY_MAX", 32768);
 static const int kBnBwdApplyMax = env_int("DPT_BN_BWD_APPLY_MAX", 4 * kMaxBlocks);
+static const int kBnReverse = env_int("DPT_BN_REVERSE", 1);  // apply passes walk rows last-to-first
 
 BnGeometry bn_geometry(int64_t M, int64_t C) {
   BnGeometry g;
@@ -468,10 +473,11 @@ template <typename IO>
 static void fwd_apply_dispatch(bool relu, bool res, const void* x, const void* r, void* y, const float* a,
                                const float* b, int64_t M, int C, int blocks, hipStream_t s) {
   dim3 gr(blocks), bl(kBlock);
-  if (relu && res) hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, true, true>), gr, bl, 0, s, x, r, y, a, b, M, C);
-  else if (relu) hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, true, false>), gr, bl, 0, s, x, r, y, a, b, M, C);
-  else if (res) hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, false, true>), gr, bl, 0, s, x, r, y, a, b, M, C);
-  else hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, false, false>), gr, bl, 0, s, x, r, y, a, b, M, C);
+  const int rev = kBnReverse;
+  if (relu && res) hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, true, true>), gr, bl, 0, s, x, r, y, a, b, M, C, rev);
+  else if (relu) hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, true, false>), gr, bl, 0, s, x, r, y, a, b, M, C, rev);
+  else if (res) hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, false, true>), gr, bl, 0, s, x, r, y, a, b, M, C, rev);
+  else hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, false, false>), gr, bl, 0, s, x, r, y, a, b, M, C, rev);
 }
 
 void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
@@ -544,10 +550,10 @@ static void bwd_dispatch(bool relu, const void* dy, const void* dy2, const void*
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p2, g.chunks, C, M, gamma,
                      invstd, dgamma, dbeta, k1, k2, k3);
   dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
-  if (dz != nullptr) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, true, false>), ga, bl, 0, s, dz, y, x, mean, coef, k1, k2, k3, dx, M, C);
-  else if (relu && coef) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false, true>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C);
-  else if (relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false, false>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C);
-  else hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, false, false>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C);
+  if (dz != nullptr) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, true, false>), ga, bl, 0, s, dz, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse);
+  else if (relu && coef) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false, true>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse);
+  else if (relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false, false>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse);
+  else hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, false, false>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse);
 }
 
 // dz: if non-null, receives dz = (dy [+ dy2]) * relu_mask (the residual-path gradient);

@@ -1,0 +1,153 @@
+"""Fused ViT block kernels (vit_kernels.hip) vs fp32 PyTorch references, and the fused ViT
+encoder vs the module-by-module path under bf16 autocast."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_pytorch_training_amd import ops
+from distributed_pytorch_training_amd.ops.vit import add_bias_layer_norm16, bias_gelu16, layer_norm16
+
+pytestmark = pytest.mark.gpu
+
+
+def _ln(D, dev):
+    ln = torch.nn.LayerNorm(D, eps=1e-6).to(dev)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    return ln
+
+
+def _close(a, b, rtol, atol, what):
+    torch.testing.assert_close(a.float(), b.float(), rtol=rtol, atol=atol, msg=what)
+
+
+@pytest.mark.parametrize("D", [256, 768, 1024])
+def test_layer_norm16_matches_fp32(cuda, D):
+    torch.manual_seed(0)
+    ln = _ln(D, cuda)
+    x = (torch.randn(3, 197, D, device=cuda) * 2 + 0.5).requires_grad_(True)
+    h = layer_norm16(x, ln, torch.bfloat16)
+    assert h.dtype == torch.bfloat16
+    gh = torch.randn_like(h)
+    h.backward(gh)
+    xr = x.detach().clone().requires_grad_(True)
+    lr = copy.deepcopy(ln)
+    hr = F.layer_norm(xr, (D,), lr.weight, lr.bias, lr.eps)
+    hr.backward(gh.float())
+    _close(h, hr, 1e-2, 2e-2, "h")
+    _close(x.grad, xr.grad, 1e-3, 1e-3, "dx")
+    _close(ln.weight.grad, lr.weight.grad, 1e-3, 1e-2, "dgamma")
+    _close(ln.bias.grad, lr.bias.grad, 1e-3, 1e-2, "dbeta")
+
+
+@pytest.mark.parametrize("bias_dtype", [torch.float32, torch.bfloat16, None])
+def test_add_bias_layer_norm16_matches_fp32(cuda, bias_dtype):
+    torch.manual_seed(1)
+    D = 768
+    ln = _ln(D, cuda)
+    x = torch.randn(2, 197, D, device=cuda).requires_grad_(True)
+    a = torch.randn(2, 197, D, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    b = None if bias_dtype is None else (torch.randn(D, device=cuda) * 0.1).to(bias_dtype).requires_grad_(True)
+    s, h = add_bias_layer_norm16(x, a, b, ln)
+    gs, gh = torch.randn_like(s), torch.randn_like(h)
+    torch.autograd.backward([s, h], [gs, gh])
+    # fp32 reference on the same (rounded) inputs
+    xr, ar = x.detach().clone().requires_grad_(True), a.detach().float().requires_grad_(True)
+    br = None if b is None else b.detach().float().requires_grad_(True)
+    lr = copy.deepcopy(ln)
+    for p in lr.parameters():
+        p.grad = None
+    sr = xr + ar + (br if br is not None else 0.0)
+    hr = F.layer_norm(sr, (D,), lr.weight, lr.bias, lr.eps)
+    torch.autograd.backward([sr, hr], [gs, gh.float()])
+    _close(s, sr, 1e-6, 1e-6, "s")
+    _close(h, hr, 1e-2, 2e-2, "h")
+    _close(x.grad, xr.grad, 1e-4, 1e-4, "dx")
+    assert a.grad.dtype == torch.bfloat16
+    _close(a.grad, ar.grad, 1e-2, 1e-2, "da")
+    if b is not None:
+        assert b.grad.dtype == bias_dtype
+        tol = 1e-4 if bias_dtype == torch.float32 else 1e-2
+        _close(b.grad, br.grad, tol, tol * 10, "dbias")
+    _close(ln.weight.grad, lr.weight.grad, 1e-3, 1e-2, "dgamma")
+    _close(ln.bias.grad, lr.bias.grad, 1e-3, 1e-2, "dbeta")
+
+
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_bias_gelu16_matches_fp32(cuda, with_bias):
+    torch.manual_seed(2)
+    u = (torch.randn(2 * 197, 3072, device=cuda) * 2).to(torch.bfloat16).requires_grad_(True)
+    b = (torch.randn(3072, device=cuda) * 0.5).requires_grad_(True) if with_bias else None
+    h = bias_gelu16(u, b)
+    gh = torch.randn_like(h)
+    h.backward(gh)
+    ur = u.detach().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True) if with_bias else None
+    hr = F.gelu(ur + (br if with_bias else 0.0))
+    hr.backward(gh.float())
+    _close(h, hr, 1e-2, 1e-2, "h")
+    _close(u.grad, ur.grad, 1e-2, 1e-2, "du")
+    if with_bias:
+        _close(b.grad, br.grad, 1e-3, 5e-2, "dbias")
+
+
+def test_vit_fused_encoder_matches_unfused(cuda):
+    """Fused encoder path vs the module-by-module path under bf16 autocast: both are compared
+    to an fp32 run and the fused error must be of the same order."""
+    from distributed_pytorch_training_amd.models import build_model
+    from distributed_pytorch_training_amd.models.vit import Encoder
+
+    torch.manual_seed(0)
+    base = build_model("vit_b_16", 10, cuda, image_size=64)
+    with torch.no_grad():      # torchvision zero-inits the head: give it values so grads flow
+        base.heads.head.weight.normal_(std=0.02)
+    x = torch.randn(4, 3, 64, 64, device=cuda)
+    y = torch.randint(0, 10, (4,), device=cuda)
+
+    def run(model, autocast, fused):
+        orig = Encoder._fused_ok
+        if not fused:
+            Encoder._fused_ok = lambda self, t: False
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+                loss = F.cross_entropy(model(x), y)
+            loss.backward()
+        finally:
+            Encoder._fused_ok = orig
+        return loss.detach(), {n: p.grad.detach().float().clone() for n, p in model.named_parameters()}
+
+    fused_m, unf_m, ref_m = (copy.deepcopy(base) for _ in range(3))
+    lf, gf = run(fused_m, True, True)
+    lu, gu = run(unf_m, True, False)
+    lr, gr = run(ref_m, False, False)
+    assert abs(lf - lr) < 2e-2 and abs(lu - lr) < 2e-2
+    for n in gr:
+        scale = gr[n].abs().max().item() + 1e-6
+        ef = (gf[n] - gr[n]).abs().max().item() / scale
+        eu = (gu[n] - gr[n]).abs().max().item() / scale
+        assert ef < max(3 * eu, 0.05), (n, ef, eu)
+
+
+def test_vit_trainer_fused_step(cuda):
+    """One native AdamW step of ViT through the fused path with weight shadows."""
+    from distributed_pytorch_training_amd.config import parse_args
+    from distributed_pytorch_training_amd.engine.trainer import Trainer
+    from distributed_pytorch_training_amd.models import build_model
+
+    torch.manual_seed(0)
+    m = build_model("vit_b_16", 10, cuda, image_size=32)
+    args = parse_args(["--model", "vit_b_16", "--dataset", "synthetic", "--amp", "--amp-dtype", "bf16",
+                       "--optimizer", "adamw", "--lr", "1e-3"])
+    tr = Trainer(m, args, 0, 1, cuda, log=lambda s: None)
+    before = tr.ddp.arena.param_flat.clone()
+    x = torch.randn(8, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (8,), device=cuda)
+    for _ in range(2):
+        tr.train_step(x, y)
+    torch.cuda.synchronize()
+    assert torch.isfinite(tr.ddp.arena.param_flat).all()
+    assert not torch.equal(before, tr.ddp.arena.param_flat)
+    assert ops.native_available()

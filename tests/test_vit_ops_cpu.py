@@ -1,0 +1,35 @@
+"""CPU composition of the fused ViT ops (ops/vit.py): same math the GPU kernels implement."""
+import torch
+import torch.nn.functional as F
+
+from distributed_pytorch_training_amd.ops.vit import add_bias_layer_norm16, bias_gelu16, layer_norm16
+
+
+def test_cpu_compositions():
+    torch.manual_seed(0)
+    ln = torch.nn.LayerNorm(256, eps=1e-6)
+    x = torch.randn(2, 5, 256)
+    a = torch.randn(2, 5, 256).to(torch.bfloat16)
+    b = torch.randn(256)
+    h = layer_norm16(x, ln, torch.bfloat16)
+    assert h.dtype == torch.bfloat16
+    torch.testing.assert_close(h.float(), F.layer_norm(x, (256,), ln.weight, ln.bias, 1e-6), rtol=1e-2, atol=2e-2)
+    s, h2 = add_bias_layer_norm16(x, a, b, ln)
+    torch.testing.assert_close(s, x + a.float() + b)
+    assert h2.dtype == torch.bfloat16
+    u = torch.randn(10, 64).to(torch.bfloat16)
+    g = bias_gelu16(u, torch.zeros(64))
+    torch.testing.assert_close(g.float(), F.gelu(u.float()), rtol=1e-2, atol=1e-2)
+
+
+def test_vit_cpu_forward_unchanged_by_fused_hooks():
+    """On CPU (no autocast) the encoder takes the module path: output equals a plain composition."""
+    from distributed_pytorch_training_amd.models import build_model
+
+    torch.manual_seed(0)
+    m = build_model("vit_b_16", 10, torch.device("cpu"), image_size=32)
+    x = torch.randn(2, 3, 32, 32)
+    enc = m.encoder
+    assert not enc._fused_ok(torch.randn(2, 5, 768))
+    out = m(x)
+    assert out.shape == (2, 10) and torch.isfinite(out).all()
