@@ -89,11 +89,12 @@ def main(argv=None) -> int:
     from distributed_pytorch_training_amd.engine.trainer import Trainer
     from distributed_pytorch_training_amd.models import build_model
     from distributed_pytorch_training_amd.utils.dist import init_distributed, set_seed
-    from distributed_pytorch_training_amd.utils.env import setup_miopen_env
+    from distributed_pytorch_training_amd.utils.env import setup_miopen_env, setup_tunableop
 
     setup_miopen_env()
     args = train_args(a)
     info = init_distributed("auto")
+    gemm_db = setup_tunableop() if (a.impl == "native" and info.device.type == "cuda") else False
     rank, ws, device = info.rank, info.world_size, info.device
     if ws != a.gpus and rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={ws}; reporting WORLD_SIZE", file=sys.stderr)
@@ -156,6 +157,7 @@ def main(argv=None) -> int:
                    "bucket_cap_mb": a.bucket_cap_mb, "grad_dtype": a.grad_dtype,
                    "fused_bn": bool(args.fused_bn and a.impl == "native" and args.channels_last),
                    "miopen": "find" if a.find else "immediate(find-db)",
+                   "gemm_db": bool(gemm_db),
                    "weight_shadow": bool(trainer.ddp is not None and trainer.ddp.shadow_flat is not None),
                    "cuda_graph": bool(a.cuda_graph and trainer.graphed is not None
                                       and trainer.graphed.graph is not None)},

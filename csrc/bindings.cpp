@@ -460,6 +460,33 @@ std::vector<Tensor> gelu_bwd(Tensor gh, Tensor u, c10::optional<Tensor> bias, bo
   return {gu, db};
 }
 
+// dst.copy_(src) for same-shape 16-bit tensors of <= 5 dims whose last dim is contiguous in
+// both (e.g. attention heads [b,h,s,dh] <-> [b,s,h,dh]): one vectorised strided-row kernel.
+void copy_rows16(Tensor src, Tensor dst) {
+  TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.device() == dst.device(), "copy_rows16: GPU tensors");
+  TORCH_CHECK(src.scalar_type() == dst.scalar_type() && src.element_size() == 2, "copy_rows16: same 16-bit dtype");
+  TORCH_CHECK(src.sizes() == dst.sizes() && src.dim() >= 1 && src.dim() <= 5, "copy_rows16: same shape, <= 5 dims");
+  const int nd = (int)src.dim();
+  const int64_t L = src.size(nd - 1);
+  TORCH_CHECK(src.stride(nd - 1) == 1 && dst.stride(nd - 1) == 1 && L % 8 == 0, "copy_rows16: rows must be contiguous, L % 8 == 0");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0,
+              "copy_rows16: 16-byte aligned data");
+  int n[4] = {1, 1, 1, 1};
+  int64_t ss[4] = {0, 0, 0, 0}, ds[4] = {0, 0, 0, 0};
+  for (int d = 0; d < nd - 1; ++d) {
+    const int slot = 4 - (nd - 1) + d;
+    TORCH_CHECK(src.size(d) < (1LL << 31), "copy_rows16: dim too large");
+    TORCH_CHECK(src.stride(d) % 8 == 0 && dst.stride(d) % 8 == 0, "copy_rows16: row starts must be 16-byte aligned");
+    n[slot] = (int)src.size(d);
+    ss[slot] = src.stride(d);
+    ds[slot] = dst.stride(d);
+  }
+  TORCH_CHECK((int64_t)n[0] * n[1] * n[2] * n[3] < (1LL << 32), "copy_rows16: too many rows");
+  c10::hip::HIPGuard guard(src.device().index());
+  dpt::launch_rows_copy16(static_cast<const uint16_t*>(src.data_ptr()), static_cast<uint16_t*>(dst.data_ptr()), n, ss,
+                          ds, (int)L, cur_stream(src));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -495,6 +522,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gamma"), py::arg("want_ga"), py::arg("bias_like"), py::arg("want_dparams"));
   m.def("gelu_fwd", &gelu_fwd, py::arg("u"), py::arg("bias"));
   m.def("gelu_bwd", &gelu_bwd, py::arg("grad"), py::arg("u"), py::arg("bias"), py::arg("want_dbias"));
+  m.def("copy_rows16", &copy_rows16, py::arg("src"), py::arg("dst"));
   m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("stride"), py::arg("pad"));
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("grad_output"), py::arg("idx"), py::arg("H"), py::arg("W"),
         py::arg("k"), py::arg("stride"), py::arg("pad"));

@@ -251,21 +251,44 @@ __device__ __forceinline__ float gelu_grad(float z) {
   return cdf + z * pdf;
 }
 
+// Column-stationary layout for both GELU passes: grid (ceil(F/8 / 128), chunks) of 128-thread
+// blocks; a thread owns one 8-column group (its 8 bias values stay in registers) and walks a
+// chunk of rows with 4 rows (8 x 16-byte accesses) in flight.
+constexpr int kGeluRows = 4;
+
 template <int KIND>
-__global__ __launch_bounds__(kBlock) void gelu_fwd_kernel(const uint16_t* __restrict__ u,
-                                                          const void* __restrict__ bias, int bias_kind,
-                                                          uint16_t* __restrict__ h, int64_t n8, int F) {
-  for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < n8; v += (int64_t)gridDim.x * kBlock) {
-    const int c0 = (int)((v * 8) % F);
-    float z[8];
-    load8h<KIND>(u + v * 8, z);
+__global__ __launch_bounds__(128) void gelu_fwd_kernel(const uint16_t* __restrict__ u,
+                                                       const void* __restrict__ bias, int bias_kind,
+                                                       uint16_t* __restrict__ h, int64_t T, int F,
+                                                       int64_t rows_per_chunk) {
+  const int cg = blockIdx.x * 128 + threadIdx.x;
+  if (cg * 8 >= F) return;
+  float b[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) z[k] = gelu_f(z[k] + load_param(bias, bias_kind, c0 + k));
-    store8h<KIND>(h + v * 8, z);
+  for (int k = 0; k < 8; ++k) b[k] = load_param(bias, bias_kind, cg * 8 + k);
+  const int64_t row0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t row1 = min(row0 + rows_per_chunk, T);
+  int64_t r = row0;
+  for (; r + kGeluRows <= row1; r += kGeluRows) {
+    float z[kGeluRows][8];
+#pragma unroll
+    for (int q = 0; q < kGeluRows; ++q) load8h<KIND>(u + (r + q) * F + cg * 8, z[q]);
+#pragma unroll
+    for (int q = 0; q < kGeluRows; ++q) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) z[q][k] = gelu_f(z[q][k] + b[k]);
+      store8h<KIND>(h + (r + q) * F + cg * 8, z[q]);
+    }
+  }
+  for (; r < row1; ++r) {
+    float z[8];
+    load8h<KIND>(u + r * F + cg * 8, z);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) z[k] = gelu_f(z[k] + b[k]);
+    store8h<KIND>(h + r * F + cg * 8, z);
   }
 }
 
-// grid (ceil(F/8 / 128), chunks); 128-thread blocks; thread = one 8-column group over a row chunk
 template <int KIND>
 __global__ __launch_bounds__(128) void gelu_bwd_kernel(const uint16_t* __restrict__ gh,
                                                        const uint16_t* __restrict__ u,
@@ -283,63 +306,112 @@ __global__ __launch_bounds__(128) void gelu_bwd_kernel(const uint16_t* __restric
   const int64_t row0 = (int64_t)blockIdx.y * rows_per_chunk;
   const int64_t row1 = min(row0 + rows_per_chunk, T);
   int64_t r = row0;
-  for (; r + 1 < row1; r += 2) {  // two rows in flight
-    float g0[8], z0[8], g1[8], z1[8];
-    const int64_t o0 = r * F + cg * 8, o1 = o0 + F;
-    load8h<KIND>(gh + o0, g0);
-    load8h<KIND>(u + o0, z0);
-    load8h<KIND>(gh + o1, g1);
-    load8h<KIND>(u + o1, z1);
+  for (; r + kGeluRows <= row1; r += kGeluRows) {
+    float g[kGeluRows][8], z[kGeluRows][8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      g0[k] *= gelu_grad(z0[k] + b[k]);
-      g1[k] *= gelu_grad(z1[k] + b[k]);
-      acc[k] += g0[k] + g1[k];
+    for (int q = 0; q < kGeluRows; ++q) {
+      load8h<KIND>(gh + (r + q) * F + cg * 8, g[q]);
+      load8h<KIND>(u + (r + q) * F + cg * 8, z[q]);
     }
-    store8h<KIND>(gu + o0, g0);
-    store8h<KIND>(gu + o1, g1);
+#pragma unroll
+    for (int q = 0; q < kGeluRows; ++q) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        g[q][k] *= gelu_grad(z[q][k] + b[k]);
+        acc[k] += g[q][k];
+      }
+      store8h<KIND>(gu + (r + q) * F + cg * 8, g[q]);
+    }
   }
-  if (r < row1) {
-    float g0[8], z0[8];
-    const int64_t o0 = r * F + cg * 8;
-    load8h<KIND>(gh + o0, g0);
-    load8h<KIND>(u + o0, z0);
+  for (; r < row1; ++r) {
+    float g[8], z[8];
+    load8h<KIND>(gh + r * F + cg * 8, g);
+    load8h<KIND>(u + r * F + cg * 8, z);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      g0[k] *= gelu_grad(z0[k] + b[k]);
-      acc[k] += g0[k];
+      g[k] *= gelu_grad(z[k] + b[k]);
+      acc[k] += g[k];
     }
-    store8h<KIND>(gu + o0, g0);
+    store8h<KIND>(gu + r * F + cg * 8, g);
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) part[(int64_t)blockIdx.y * F + cg * 8 + k] = acc[k];
 }
 
+// ---- 16-bit strided row copy (attention head split/merge) ------------------------------------
+// dst[i0,i1,i2,i3,:L] = src[i0,i1,i2,i3,:L]; the L-element rows are contiguous in both, every
+// row start is 16-byte aligned (host-checked); one 16-byte vector per thread iteration.
+struct Rows4 {
+  int n[4];
+  int64_t ss[4], ds[4];
+};
+
+__global__ __launch_bounds__(kBlock) void rows_copy16_kernel(const uint16_t* __restrict__ src,
+                                                             uint16_t* __restrict__ dst, Rows4 g, int L) {
+  const int vpr = L >> 3;
+  const int64_t total = (int64_t)g.n[0] * g.n[1] * g.n[2] * g.n[3] * vpr;
+  for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < total; v += (int64_t)gridDim.x * kBlock) {
+    unsigned row = (unsigned)(v / vpr);
+    const int k = (int)(v - (int64_t)row * vpr);
+    const unsigned i3 = row % (unsigned)g.n[3];
+    row /= (unsigned)g.n[3];
+    const unsigned i2 = row % (unsigned)g.n[2];
+    row /= (unsigned)g.n[2];
+    const unsigned i1 = row % (unsigned)g.n[1];
+    const unsigned i0 = row / (unsigned)g.n[1];
+    const int64_t so = i0 * g.ss[0] + i1 * g.ss[1] + i2 * g.ss[2] + i3 * g.ss[3] + k * 8;
+    const int64_t d0 = i0 * g.ds[0] + i1 * g.ds[1] + i2 * g.ds[2] + i3 * g.ds[3] + k * 8;
+    *reinterpret_cast<uint4*>(dst + d0) = *reinterpret_cast<const uint4*>(src + so);
+  }
+}
+
 // ---- deterministic column sums of [n, D] partials -> out (kind 0 f32 / 1 bf16 / 2 f16) -----
-// grid (ceil(D/64)), 256 threads: 4 waves split the n rows, lane = column; fp64 accumulation.
-__global__ __launch_bounds__(kBlock) void colsum_kernel(const float* __restrict__ part, int64_t n, int64_t D,
-                                                        void* __restrict__ out, int out_kind) {
-  __shared__ double red[4][64];
+// grid (ceil(D/64), sets), 1024 threads: 16 waves split the n rows (4 loads in flight each),
+// lane = column; fp64 accumulation, fixed combine order.  Set s reads part + s*set_stride.
+struct ColsumOut {
+  void* out[3];
+  int kind[3];
+};
+
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ part, int64_t n, int64_t D,
+                                                      int64_t set_stride, ColsumOut o) {
+  __shared__ double red[16][64];
+  void* out = o.out[blockIdx.y];
+  if (out == nullptr) return;  // whole block: uniform
+  const float* p = part + blockIdx.y * set_stride;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t c = (int64_t)blockIdx.x * 64 + lane;
   double acc = 0.0;
   if (c < D) {
     int64_t r = wave;
-    for (; r + 12 < n; r += 16) {
-      const float a0 = part[r * D + c], a1 = part[(r + 4) * D + c];
-      const float a2 = part[(r + 8) * D + c], a3 = part[(r + 12) * D + c];
+    for (; r + 48 < n; r += 64) {
+      const float a0 = p[r * D + c], a1 = p[(r + 16) * D + c];
+      const float a2 = p[(r + 32) * D + c], a3 = p[(r + 48) * D + c];
       acc += ((double)a0 + (double)a1) + ((double)a2 + (double)a3);
     }
-    for (; r < n; r += 4) acc += (double)part[r * D + c];
+    for (; r < n; r += 16) acc += (double)p[r * D + c];
   }
   red[wave][lane] = acc;
   __syncthreads();
   if (wave == 0 && c < D) {
-    const float v = (float)((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]));
-    if (out_kind == 0) static_cast<float*>(out)[c] = v;
-    else if (out_kind == 1) static_cast<uint16_t*>(out)[c] = f32_to_bf16(v);
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w][lane];
+    const float v = (float)t;
+    const int kind = o.kind[blockIdx.y];
+    if (kind == 0) static_cast<float*>(out)[c] = v;
+    else if (kind == 1) static_cast<uint16_t*>(out)[c] = f32_to_bf16(v);
     else static_cast<uint16_t*>(out)[c] = __builtin_bit_cast(uint16_t, (_Float16)v);
   }
+}
+
+static void launch_colsum(const float* part, int64_t n, int64_t D, int sets, void* o0, int k0, void* o1, int k1,
+                          void* o2, int k2, hipStream_t s) {
+  ColsumOut o;
+  o.out[0] = o0; o.out[1] = o1; o.out[2] = o2;
+  o.kind[0] = k0; o.kind[1] = k1; o.kind[2] = k2;
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((D + 63) / 64), (unsigned)sets), dim3(1024), 0, s, part, n, D,
+                     n * D, o);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -425,18 +497,9 @@ void launch_ln_bwd(int kind, const float* gs, const uint16_t* gh, const float* s
   if (kind == 1) ln_bwd_kind<1>(D, gs, gh, sv, mean, rstd, gamma, gx, ga, part, T, s);
   else ln_bwd_kind<2>(D, gs, gh, sv, mean, rstd, gamma, gx, ga, part, T, s);
   const int64_t nb = ln_bwd_blocks(T);
-  dim3 gr((unsigned)((D + 63) / 64)), bl(kBlock);
-  if (dgamma) hipLaunchKernelGGL(colsum_kernel, gr, bl, 0, s, part, nb, D, (void*)dgamma, 0);
-  if (dbeta) hipLaunchKernelGGL(colsum_kernel, gr, bl, 0, s, part + nb * D, nb, D, (void*)dbeta, 0);
-  if (dbias && ga) hipLaunchKernelGGL(colsum_kernel, gr, bl, 0, s, part + 2 * nb * D, nb, D, dbias, dbias_kind);
-}
-
-void launch_gelu_fwd(int kind, const uint16_t* u, const void* bias, int bias_kind, uint16_t* h, int64_t T, int64_t F,
-                     hipStream_t s) {
-  const int64_t n8 = T * F / 8;
-  dim3 gr(grid_for(n8, 2)), bl(kBlock);
-  if (kind == 1) hipLaunchKernelGGL(gelu_fwd_kernel<1>, gr, bl, 0, s, u, bias, bias_kind, h, n8, (int)F);
-  else hipLaunchKernelGGL(gelu_fwd_kernel<2>, gr, bl, 0, s, u, bias, bias_kind, h, n8, (int)F);
+  void* db = (dbias && ga) ? dbias : nullptr;
+  if (dgamma || dbeta || db)
+    launch_colsum(part, nb, D, db ? 3 : 2, dgamma, 0, dbeta, 0, db, dbias_kind, s);
 }
 
 int gelu_bwd_chunks(int64_t T, int64_t F) {
@@ -447,6 +510,15 @@ int gelu_bwd_chunks(int64_t T, int64_t F) {
   return (int)(c < 1 ? 1 : c);
 }
 
+void launch_gelu_fwd(int kind, const uint16_t* u, const void* bias, int bias_kind, uint16_t* h, int64_t T, int64_t F,
+                     hipStream_t s) {
+  const int chunks = gelu_bwd_chunks(T, F);
+  const int64_t rpc = (T + chunks - 1) / chunks;
+  dim3 gr((unsigned)((F / 8 + 127) / 128), (unsigned)chunks), bl(128);
+  if (kind == 1) hipLaunchKernelGGL(gelu_fwd_kernel<1>, gr, bl, 0, s, u, bias, bias_kind, h, T, (int)F, rpc);
+  else hipLaunchKernelGGL(gelu_fwd_kernel<2>, gr, bl, 0, s, u, bias, bias_kind, h, T, (int)F, rpc);
+}
+
 void launch_gelu_bwd(int kind, const uint16_t* gh, const uint16_t* u, const void* bias, int bias_kind, uint16_t* gu,
                      float* part, void* dbias, int dbias_kind, int64_t T, int64_t F, hipStream_t s) {
   const int chunks = gelu_bwd_chunks(T, F);
@@ -454,8 +526,20 @@ void launch_gelu_bwd(int kind, const uint16_t* gh, const uint16_t* u, const void
   dim3 gr((unsigned)((F / 8 + 127) / 128), (unsigned)chunks), bl(128);
   if (kind == 1) hipLaunchKernelGGL(gelu_bwd_kernel<1>, gr, bl, 0, s, gh, u, bias, bias_kind, gu, part, T, (int)F, rpc);
   else hipLaunchKernelGGL(gelu_bwd_kernel<2>, gr, bl, 0, s, gh, u, bias, bias_kind, gu, part, T, (int)F, rpc);
-  if (dbias) hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((F + 63) / 64)), dim3(kBlock), 0, s, part, (int64_t)chunks, F,
-                                dbias, dbias_kind);
+  if (dbias) launch_colsum(part, chunks, F, 1, dbias, dbias_kind, nullptr, 0, nullptr, 0, s);
+}
+
+void launch_rows_copy16(const uint16_t* src, uint16_t* dst, const int n[4], const int64_t ss[4], const int64_t ds[4],
+                        int L, hipStream_t s) {
+  Rows4 g;
+  for (int i = 0; i < 4; ++i) {
+    g.n[i] = n[i];
+    g.ss[i] = ss[i];
+    g.ds[i] = ds[i];
+  }
+  const int64_t total = (int64_t)n[0] * n[1] * n[2] * n[3] * (L / 8);
+  if (total == 0) return;
+  hipLaunchKernelGGL(rows_copy16_kernel, dim3(grid_for(total, 2)), dim3(kBlock), 0, s, src, dst, g, L);
 }
 
 }  // namespace dpt

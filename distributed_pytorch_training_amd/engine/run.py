@@ -21,7 +21,7 @@ from ..data import get_dataloaders
 from ..models import build_model
 from ..utils.checkpoint import load_checkpoint, save_checkpoint
 from ..utils.dist import cleanup_distributed, init_distributed, set_seed
-from ..utils.env import setup_miopen_env
+from ..utils.env import setup_miopen_env, setup_tunableop
 from .trainer import Trainer, format_epoch_line
 
 CSV_HEADER = "epoch,train_loss,train_acc,val_loss,val_acc,epoch_time_seconds\n"
@@ -56,6 +56,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     setup_miopen_env()
     info = init_distributed(args.backend, args.dist_timeout)
     rank, world_size, device = info.rank, info.world_size, info.device
+    if args.impl == "native" and device.type == "cuda":
+        setup_tunableop()
     set_seed(args.seed, rank)
 
     if rank == 0:

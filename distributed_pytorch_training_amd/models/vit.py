@@ -26,7 +26,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.vit import add_bias_layer_norm16, bias_gelu16, layer_norm16, ln_fusable
+from ..ops.vit import add_bias_layer_norm16, bias_gelu16, layer_norm16, ln_fusable, merge_heads, split_heads
 from ..parallel.shadow import shadow_param
 
 
@@ -46,10 +46,9 @@ class SelfAttention(nn.Module):
     def _context(self, x: torch.Tensor) -> torch.Tensor:
         b, s, d = x.shape
         qkv = F.linear(x, shadow_param(self, "in_proj_weight", x), shadow_param(self, "in_proj_bias", x))
-        # unbind (backward = one stack) instead of three selects (backward = zero-fill + 3 copies)
-        q, k, v = qkv.view(b, s, 3, self.heads, d // self.heads).permute(2, 0, 3, 1, 4).unbind(0)
+        q, k, v = split_heads(qkv, self.heads)
         y = F.scaled_dot_product_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0)
-        return y.transpose(1, 2).reshape(b, s, d)
+        return merge_heads(y)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.out_proj(self._context(x))

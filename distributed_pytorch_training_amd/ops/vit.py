@@ -7,6 +7,10 @@
                                         gradient in one pass
 * ``bias_gelu16(u, b)``                 gelu(u + b) (exact erf), backward with the bias-gradient
                                         column sums fused
+* ``split_heads(qkv, h)`` / ``merge_heads(y)``  attention head layout changes: the backward of
+                                        the split writes dq/dk/dv straight into one [b, s, 3D]
+                                        gradient (no stack + transpose copy), the merge is one
+                                        vectorised strided copy
 
 ``a`` / ``u`` are the outputs of bias-free GEMMs (``F.linear(h, W)``): the bias add moves into
 these kernels so the bias gradient falls out of the pass that already reads the gradient
@@ -86,6 +90,65 @@ class _BiasGELU16(torch.autograd.Function):
         u, bias = ctx.saved_tensors
         gu, db = native().gelu_bwd(gh.contiguous(), u, bias, bias is not None and ctx.needs_input_grad[1])
         return gu, (db if bias is not None and ctx.needs_input_grad[1] else None)
+
+
+class _SplitHeads(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, heads):
+        b, s, d3 = qkv.shape
+        dh = d3 // 3 // heads
+        ctx.shape = (b, s, heads, dh)
+        v5 = qkv.view(b, s, 3, heads, dh).permute(2, 0, 3, 1, 4)
+        return v5[0], v5[1], v5[2]
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        b, s, h, dh = ctx.shape
+        ref = next(g for g in (dq, dk, dv) if g is not None)
+        out = torch.empty(b, s, 3, h, dh, dtype=ref.dtype, device=ref.device)
+        o5 = out.permute(2, 0, 3, 1, 4)
+        C = native()
+        for i, g in enumerate((dq, dk, dv)):
+            if g is None:
+                o5[i].zero_()
+            else:
+                C.copy_rows16(g if g.stride(-1) == 1 else g.contiguous(), o5[i])
+        return out.view(b, s, 3 * h * dh), None
+
+
+class _MergeHeads(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y):
+        b, h, s, dh = y.shape
+        ctx.shape = (b, h, s, dh)
+        out = torch.empty(b, s, h, dh, dtype=y.dtype, device=y.device)
+        native().copy_rows16(y if y.stride(-1) == 1 else y.contiguous(), out.permute(0, 2, 1, 3))
+        return out.view(b, s, h * dh)
+
+    @staticmethod
+    def backward(ctx, g):
+        b, h, s, dh = ctx.shape
+        return g.view(b, s, h, dh).permute(0, 2, 1, 3)
+
+
+def heads_fusable(t: torch.Tensor, head_dim: int) -> bool:
+    return (t.is_cuda and t.dtype in _KIND and head_dim % 8 == 0 and native_available())
+
+
+def split_heads(qkv: torch.Tensor, heads: int):
+    """[b, s, 3*D] -> q, k, v [b, heads, s, D/heads] (views)."""
+    if heads_fusable(qkv, qkv.shape[-1] // 3 // heads):
+        return _SplitHeads.apply(qkv, heads)
+    b, s, d3 = qkv.shape
+    return qkv.view(b, s, 3, heads, d3 // 3 // heads).permute(2, 0, 3, 1, 4).unbind(0)
+
+
+def merge_heads(y: torch.Tensor) -> torch.Tensor:
+    """[b, h, s, dh] -> [b, s, h*dh] contiguous."""
+    b, h, s, dh = y.shape
+    if heads_fusable(y, dh):
+        return _MergeHeads.apply(y)
+    return y.transpose(1, 2).reshape(b, s, h * dh)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -15,6 +15,7 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[2]
 SHIPPED_DB = REPO / "miopen_db"
+SHIPPED_GEMM_DB = REPO / "gemm_db" / "tunableop_results.csv"
 
 
 def setup_miopen_env(scratch: str | None = None) -> str:
@@ -63,3 +64,29 @@ def export_miopen_db(dest: str | None = None) -> int:
             shutil.copy2(f, out / f.name)
             n += 1
     return n
+
+
+def setup_tunableop() -> bool:
+    """Use the shipped MI355X GEMM tunings (PyTorch TunableOp over hipBLASLt/rocBLAS).
+
+    hipBLASLt's default heuristic picks non-split-K kernels for the long-K weight-gradient
+    GEMMs of ViT ([3072 x 768] outputs with K = tokens = 25,216): 36 workgroups on a 256-CU
+    chip.  ``gemm_db/tunableop_results.csv`` holds the measured-fastest solution per GEMM
+    shape (tuned on MI355X by ``bench/gpu_tune_gemm.sh``); TunableOp looks shapes up there and
+    falls back to the default heuristic for unknown ones.  Read-only: tuning stays off unless
+    the caller set ``PYTORCH_TUNABLEOP_*`` itself.  ``DPT_TUNABLEOP=0`` disables.
+    """
+    if os.environ.get("DPT_TUNABLEOP", "1") == "0" or "PYTORCH_TUNABLEOP_ENABLED" in os.environ:
+        return False
+    if not SHIPPED_GEMM_DB.is_file():
+        return False
+    import torch
+
+    if not torch.cuda.is_available():
+        return False
+    t = torch.cuda.tunable
+    t.enable(True)
+    t.tuning_enable(False)
+    t.record_untuned_enable(False)
+    t.set_filename(str(SHIPPED_GEMM_DB), False)
+    return True

@@ -151,3 +151,24 @@ def test_vit_trainer_fused_step(cuda):
     assert torch.isfinite(tr.ddp.arena.param_flat).all()
     assert not torch.equal(before, tr.ddp.arena.param_flat)
     assert ops.native_available()
+
+
+def test_split_merge_heads_match_torch(cuda):
+    from distributed_pytorch_training_amd.ops.vit import merge_heads, split_heads
+
+    torch.manual_seed(3)
+    b, s, h, dh = 3, 197, 12, 64
+    qkv = torch.randn(b, s, 3 * h * dh, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    q, k, v = split_heads(qkv, h)
+    ref = qkv.detach().view(b, s, 3, h, dh).permute(2, 0, 3, 1, 4)
+    assert torch.equal(q, ref[0]) and torch.equal(k, ref[1]) and torch.equal(v, ref[2])
+    y = F.scaled_dot_product_attention(q, k, v)
+    m = merge_heads(y)
+    assert m.is_contiguous() and torch.equal(m, y.detach().transpose(1, 2).reshape(b, s, h * dh))
+    g = torch.randn_like(m)
+    m.backward(g)
+    qkv2 = qkv.detach().clone().requires_grad_(True)
+    r = qkv2.view(b, s, 3, h, dh).permute(2, 0, 3, 1, 4)
+    y2 = F.scaled_dot_product_attention(r[0], r[1], r[2])
+    y2.transpose(1, 2).reshape(b, s, h * dh).backward(g)
+    torch.testing.assert_close(qkv.grad.float(), qkv2.grad.float(), rtol=1e-3, atol=1e-3)
