@@ -7,6 +7,10 @@ mkdir -p gpurun_out
 export DPT_SCRATCH=$PWD/gpurun_out/scratch_gemm
 ( while sleep 45; do echo "hb $(date +%T) $(cat gpurun_out/tunableop_results*.csv 2>/dev/null | wc -l) tuned"; done ) &
 HB=$!
+# start from the shipped tunings: TunableOp reads the file (device ordinal appended) and
+# writes it back with the new shapes added
+cp gemm_db/tunableop_results.csv gpurun_out/tunableop_results0.csv 2>/dev/null
+timeout -k 10 600 python -m pytest tests/test_vit_gpu.py -q -x > gpurun_out/pytest_gemm.txt 2>&1 || exit 3
 export PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_FILENAME=$PWD/gpurun_out/tunableop_results.csv
 timeout -k 10 700 python bench.py --find --model vit_b_16 --batch-size 128 --no-channels-last --steps 2 --warmup 2 --optimizer adamw > gpurun_out/tune_gemm_vit.txt 2>&1
 rc1=$?

@@ -26,7 +26,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.vit import add_bias_layer_norm16, bias_gelu16, layer_norm16, ln_fusable, merge_heads, split_heads
+from ..ops.vit import (add_bias_layer_norm16, bias_gelu16, layer_norm16, linear16, ln_fusable, merge_heads,
+                       split_heads)
 from ..parallel.shadow import shadow_param
 
 
@@ -45,7 +46,7 @@ class SelfAttention(nn.Module):
 
     def _context(self, x: torch.Tensor) -> torch.Tensor:
         b, s, d = x.shape
-        qkv = F.linear(x, shadow_param(self, "in_proj_weight", x), shadow_param(self, "in_proj_bias", x))
+        qkv = linear16(x, shadow_param(self, "in_proj_weight", x), shadow_param(self, "in_proj_bias", x))
         q, k, v = split_heads(qkv, self.heads)
         y = F.scaled_dot_product_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0)
         return merge_heads(y)
@@ -57,7 +58,7 @@ class SelfAttention(nn.Module):
         """(out_proj(context) without its bias, the bias) - the fused path adds the bias in
         the following add+LayerNorm kernel."""
         y = self._context(x)
-        return F.linear(y, shadow_param(self.out_proj, "weight", y)), shadow_param(self.out_proj, "bias", y)
+        return linear16(y, shadow_param(self.out_proj, "weight", y)), shadow_param(self.out_proj, "bias", y)
 
 
 class MLPBlock(nn.Sequential):
@@ -125,9 +126,9 @@ class Encoder(nn.Module):
             a, ab = blk.self_attention.attend_nobias(h)
             x, h2 = add_bias_layer_norm16(x, a, ab, blk.ln_2)
             fc1, fc2 = blk.mlp[0], blk.mlp[3]
-            u = F.linear(h2, shadow_param(fc1, "weight", h2))
+            u = linear16(h2, shadow_param(fc1, "weight", h2))
             g = bias_gelu16(u, shadow_param(fc1, "bias", h2))
-            pending = (F.linear(g, shadow_param(fc2, "weight", g)), shadow_param(fc2, "bias", g))
+            pending = (linear16(g, shadow_param(fc2, "weight", g)), shadow_param(fc2, "bias", g))
         return add_bias_layer_norm16(x, pending[0], pending[1], self.ln)[1]
 
 

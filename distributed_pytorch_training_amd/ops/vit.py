@@ -173,3 +173,61 @@ def bias_gelu16(u: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
         return _BiasGELU16.apply(u.contiguous(), bias)
     z = u.float() + (bias.float() if bias is not None else 0.0)
     return F.gelu(z).to(u.dtype)
+
+
+# ---- Linear with split-K weight gradient ------------------------------------------------------
+def _wgrad_splits(n_out: int, n_in: int, T: int) -> int:
+    """Batch-split count for dW = dY^T X with K = T tokens.  One [n_out x n_in] output has only
+    ceil(n_out/256)*ceil(n_in/256) macro tiles (9..36 for ViT-B) for 256 CUs; splitting K into
+    S batched GEMMs multiplies the tile count.  Measured on MI355X (bench/wgrad_splitk.py,
+    T = 25,216): best S = 4 for 36 tiles, 8 for 27, 16 for 9."""
+    tiles = -(-n_out // 256) * -(-n_in // 256)
+    s = 4 if tiles >= 32 else (8 if tiles >= 16 else 16)
+    while s > 1 and (T % s or T // s < 1024):
+        s //= 2
+    return s
+
+
+def wgrad_splitk(dy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+    """dY^T X ([T, n_out], [T, n_in] -> [n_out, n_in]) as split-K with fp32 partials."""
+    T, n_out = dy.shape
+    n_in = x.shape[1]
+    s = _wgrad_splits(n_out, n_in, T)
+    if s == 1:
+        return (dy.t() @ x).to(out_dtype)
+    part = torch.bmm(dy.view(s, T // s, n_out).transpose(1, 2), x.view(s, T // s, n_in),
+                     out_dtype=torch.float32)
+    return part.sum(0).to(out_dtype)
+
+
+class _Linear16(torch.autograd.Function):
+    """y = x W^T (+ b) on 16-bit operands; backward computes dW as a split-K batched GEMM
+    (hipBLASLt's single-GEMM choice leaves most CUs idle on these long-K shapes)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        w16 = w if w.dtype == x.dtype else w.to(x.dtype)
+        b16 = None if b is None else (b if b.dtype == x.dtype else b.to(x.dtype))
+        ctx.save_for_backward(x, w16)
+        ctx.w_dtype = w.dtype
+        ctx.b_dtype = None if b is None else b.dtype
+        return F.linear(x, w16, b16)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w16 = ctx.saved_tensors
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).contiguous()
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dx = (dy2 @ w16).view(shp) if ctx.needs_input_grad[0] else None
+        dw = wgrad_splitk(dy2, x2, ctx.w_dtype) if ctx.needs_input_grad[1] else None
+        db = dy2.sum(0, dtype=torch.float32).to(ctx.b_dtype) if (ctx.b_dtype is not None
+                                                                 and ctx.needs_input_grad[2]) else None
+        return dx, dw, db
+
+
+def linear16(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """F.linear for 16-bit activations (autocast region) with the split-K weight gradient."""
+    if x.is_cuda and x.dtype in _KIND and x.is_contiguous():
+        return _Linear16.apply(x, w, b)
+    return F.linear(x, w, b)

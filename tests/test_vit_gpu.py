@@ -172,3 +172,26 @@ def test_split_merge_heads_match_torch(cuda):
     y2 = F.scaled_dot_product_attention(r[0], r[1], r[2])
     y2.transpose(1, 2).reshape(b, s, h * dh).backward(g)
     torch.testing.assert_close(qkv.grad.float(), qkv2.grad.float(), rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("n_out,n_in,bias", [(3072, 768, False), (768, 768, False), (2304, 768, True)])
+def test_linear16_splitk_wgrad(cuda, n_out, n_in, bias):
+    from distributed_pytorch_training_amd.ops.vit import _wgrad_splits, linear16
+
+    torch.manual_seed(4)
+    T = 8 * 197 * 4
+    assert _wgrad_splits(n_out, n_in, T) > 1
+    x = torch.randn(T, n_in, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    w = (torch.randn(n_out, n_in, device=cuda) * 0.02).to(torch.bfloat16).requires_grad_(True)
+    b = torch.randn(n_out, device=cuda).requires_grad_(True) if bias else None
+    y = linear16(x, w, b)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr, wr = x.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True) if bias else None
+    F.linear(xr, wr, br).backward(g.float())
+    assert w.grad.dtype == torch.bfloat16
+    _close(w.grad, wr.grad, 1e-2, 1e-1, "dW")
+    _close(x.grad, xr.grad, 1e-2, 1e-2, "dx")
+    if bias:
+        _close(b.grad, br.grad, 1e-3, 1e-1, "db")

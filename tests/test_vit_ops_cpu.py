@@ -33,3 +33,14 @@ def test_vit_cpu_forward_unchanged_by_fused_hooks():
     assert not enc._fused_ok(torch.randn(2, 5, 768))
     out = m(x)
     assert out.shape == (2, 10) and torch.isfinite(out).all()
+
+
+def test_wgrad_split_choice():
+    from distributed_pytorch_training_amd.ops.vit import _wgrad_splits
+
+    T = 128 * 197
+    assert _wgrad_splits(3072, 768, T) == 4
+    assert _wgrad_splits(2304, 768, T) == 8
+    assert _wgrad_splits(768, 768, T) == 16
+    assert _wgrad_splits(768, 768, 1000) == 1          # too few rows per split
+    assert _wgrad_splits(768, 768, 197 * 3) == 1       # odd token count: no even split
