@@ -460,6 +460,32 @@ std::vector<Tensor> gelu_bwd(Tensor gh, Tensor u, c10::optional<Tensor> bias, bo
   return {gu, db};
 }
 
+// Column sums of a 16-bit [.., F] gradient (a Linear's bias gradient) in out_dtype's kind.
+Tensor bias_grad16(Tensor gy, int64_t out_kind) {
+  const int kind = act16_kind(gy, "bias_grad16: grad");
+  const int64_t F = gy.size(-1), T = gy.numel() / F;
+  TORCH_CHECK(F % 8 == 0 && (out_kind >= 0 && out_kind <= 2), "bias_grad16: F % 8 == 0, kind 0..2");
+  auto db = at::empty({F}, gy.options().dtype(out_kind == 0 ? at::kFloat : kind_dtype((int)out_kind)));
+  auto part = at::empty({(int64_t)dpt::gelu_bwd_chunks(T, F) * F}, gy.options().dtype(at::kFloat));
+  c10::hip::HIPGuard guard(gy.device().index());
+  dpt::launch_bias_grad16(kind, static_cast<const uint16_t*>(gy.data_ptr()), part.data_ptr<float>(), db.data_ptr(),
+                          (int)out_kind, T, F, cur_stream(gy));
+  return db;
+}
+
+// Sum of split-K partials [S, ...] (fp32) into a new tensor of out_kind (0 f32, 1 bf16, 2 f16).
+Tensor sum_partials(Tensor part, int64_t out_kind) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() >= 2,
+              "sum_partials: contiguous fp32 [S, ...]");
+  const int64_t S = part.size(0), n = part.numel() / S;
+  TORCH_CHECK(n % 4 == 0 && out_kind >= 0 && out_kind <= 2, "sum_partials: n % 4 == 0, kind 0..2");
+  auto out = at::empty(part.sizes().slice(1),
+                       part.options().dtype(out_kind == 0 ? at::kFloat : kind_dtype((int)out_kind)));
+  c10::hip::HIPGuard guard(part.device().index());
+  dpt::launch_sum_partials(part.data_ptr<float>(), n, (int)S, out.data_ptr(), (int)out_kind, cur_stream(part));
+  return out;
+}
+
 // dst.copy_(src) for same-shape 16-bit tensors of <= 5 dims whose last dim is contiguous in
 // both (e.g. attention heads [b,h,s,dh] <-> [b,s,h,dh]): one vectorised strided-row kernel.
 void copy_rows16(Tensor src, Tensor dst) {
@@ -523,6 +549,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_fwd", &gelu_fwd, py::arg("u"), py::arg("bias"));
   m.def("gelu_bwd", &gelu_bwd, py::arg("grad"), py::arg("u"), py::arg("bias"), py::arg("want_dbias"));
   m.def("copy_rows16", &copy_rows16, py::arg("src"), py::arg("dst"));
+  m.def("bias_grad16", &bias_grad16, py::arg("grad"), py::arg("out_kind"));
+  m.def("sum_partials", &sum_partials, py::arg("part"), py::arg("out_kind"));
   m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("stride"), py::arg("pad"));
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("grad_output"), py::arg("idx"), py::arg("H"), py::arg("W"),
         py::arg("k"), py::arg("stride"), py::arg("pad"));

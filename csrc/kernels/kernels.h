@@ -96,6 +96,11 @@ void launch_gelu_fwd(int kind, const uint16_t* u, const void* bias, int bias_kin
 // part: gelu_bwd_chunks(T, F) * F floats of scratch
 void launch_gelu_bwd(int kind, const uint16_t* gh, const uint16_t* u, const void* bias, int bias_kind, uint16_t* gu,
                      float* part, void* dbias, int dbias_kind, int64_t T, int64_t F, hipStream_t s);
+// dbias = column sums of gy [T, F] (F % 8 == 0); part: gelu_bwd_chunks(T, F) * F floats
+void launch_bias_grad16(int kind, const uint16_t* gy, float* part, void* dbias, int dbias_kind, int64_t T, int64_t F,
+                        hipStream_t s);
+// out[i] = sum over S of part[s][i], n % 4 == 0; out kind 0 f32 / 1 bf16 / 2 f16
+void launch_sum_partials(const float* part, int64_t n, int S, void* out, int out_kind, hipStream_t s);
 // dst[i0..i3, :L] = src[i0..i3, :L] (16-bit elements, strides in elements, L % 8 == 0, rows 16-B aligned)
 void launch_rows_copy16(const uint16_t* src, uint16_t* dst, const int n[4], const int64_t ss[4], const int64_t ds[4],
                         int L, hipStream_t s);

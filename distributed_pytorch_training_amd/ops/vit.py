@@ -31,6 +31,7 @@ import torch.nn.functional as F
 from . import native, native_available
 
 _KIND = {torch.bfloat16: 1, torch.float16: 2}
+_PKIND = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 
 
 def ln_fusable(x: torch.Tensor, dim: int) -> bool:
@@ -197,6 +198,8 @@ def wgrad_splitk(dy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype) -> t
         return (dy.t() @ x).to(out_dtype)
     part = torch.bmm(dy.view(s, T // s, n_out).transpose(1, 2), x.view(s, T // s, n_in),
                      out_dtype=torch.float32)
+    if native_available() and (n_out * n_in) % 4 == 0:
+        return native().sum_partials(part, _PKIND[out_dtype])   # sum + cast in one pass
     return part.sum(0).to(out_dtype)
 
 
@@ -221,8 +224,12 @@ class _Linear16(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         dx = (dy2 @ w16).view(shp) if ctx.needs_input_grad[0] else None
         dw = wgrad_splitk(dy2, x2, ctx.w_dtype) if ctx.needs_input_grad[1] else None
-        db = dy2.sum(0, dtype=torch.float32).to(ctx.b_dtype) if (ctx.b_dtype is not None
-                                                                 and ctx.needs_input_grad[2]) else None
+        db = None
+        if ctx.b_dtype is not None and ctx.needs_input_grad[2]:
+            if dy2.shape[1] % 8 == 0 and dy2.dtype in _KIND:
+                db = native().bias_grad16(dy2, _PKIND[ctx.b_dtype])
+            else:
+                db = dy2.sum(0, dtype=torch.float32).to(ctx.b_dtype)
         return dx, dw, db
 
 
