@@ -17,7 +17,9 @@ from collections import defaultdict
 
 FAMILIES = [
     ("native: optimizer (fused SGD/Adam, grad_check, tail)", r"dpt::(sgd|adam|grad_check|optim_tail)"),
-    ("native: metrics/augment/comm kernels", r"dpt::"),
+    ("native: fused BatchNorm(+add)(+ReLU)", r"dpt::bn_"),
+    ("native: ViT block kernels", r"dpt::(ln_|gelu|rows_copy|colsum|sum_partials)"),
+    ("native: metrics/augment/comm/pool kernels", r"dpt::"),
     ("RCCL", r"nccl|rccl|AllReduce|Broadcast"),
     ("conv (MIOpen/CK igemm, xdlops)", r"igemm|Conv|conv|xdlops|gridwise_gemm|DeviceGroupedConv|naive_conv|ImplicitGemm|kernel_grouped_conv"),
     ("batch-norm", r"batch_norm|batchnorm|BatchNorm|MIOpenBatchNorm|bn_"),

@@ -26,6 +26,7 @@ def test_native_matches_torch_fp32(cuda, opt):
     lr = "0.1" if opt == "sgd" else "1e-3"
     nat, ref = _pair(cuda, "resnet18", ["--optimizer", opt, "--lr", lr])
     torch.backends.cudnn.deterministic = True
+    p0 = [p.detach().clone() for p in ref.module.parameters()]
     g = torch.Generator(device=cuda).manual_seed(1)
     for _ in range(3):
         x = torch.randn(16, 3, 32, 32, device=cuda, generator=g)
@@ -34,8 +35,15 @@ def test_native_matches_torch_fp32(cuda, opt):
         ref.train_step(x, y)
     # Adam moves every weight by ~lr*sign(m/sqrt(v)); near-zero gradients flip sign on fp noise
     # between two conv algorithm runs, so its parity bound is a few lr steps.
-    atol = 2e-4 if opt == "sgd" else 4e-3
-    for (n, p), (_, q) in zip(nat.module.named_parameters(), ref.module.named_parameters()):
+    # Each parameter's 3-step update must agree with stock torch's to 1% of the update's norm
+    # (conv1 sits at the end of backward, so it carries every upstream fp32 rounding difference
+    # of two different conv-algorithm choices), and elementwise within an absolute bound.
+    atol = 1e-3 if opt == "sgd" else 4e-3
+    for (n, p), (_, q), w0 in zip(nat.module.named_parameters(), ref.module.named_parameters(), p0):
+        if opt == "sgd":
+            du_ref = (q - w0).double()
+            rel = ((p - q).double().norm() / du_ref.norm().clamp_min(1e-12)).item()
+            assert rel < 1e-2, f"{n}: |native-torch|/|torch update| = {rel:.3e}"
         torch.testing.assert_close(p, q, rtol=2e-3, atol=atol, msg=n)
 
 
@@ -187,8 +195,16 @@ def test_weight_shadow_matches_autocast_casts(cuda, model_name, opt):
         no.train_step(x, y)
         torch.cuda.synchronize()
         assert torch.equal(sh.ddp.shadow_flat, sh.ddp.arena.param_flat.to(torch.bfloat16))
-    atol = 1e-5 if opt == "sgd" else 2e-3
-    torch.testing.assert_close(sh.ddp.arena.param_flat, no.ddp.arena.param_flat, rtol=1e-4, atol=atol)
+    if opt == "sgd":
+        torch.testing.assert_close(sh.ddp.arena.param_flat, no.ddp.arena.param_flat, rtol=1e-4, atol=1e-5)
+    else:
+        # Adam's update is ~lr*sign(m/sqrt(v)) per step: a near-zero gradient whose sign flips on
+        # GEMM-algorithm rounding noise moves that weight by up to 2*lr per step.  Bound the worst
+        # element by that and require the bulk to agree.
+        d = (sh.ddp.arena.param_flat - no.ddp.arena.param_flat).abs()
+        assert d.max().item() <= 2 * 1e-3 * 4 + 1e-4
+        assert d.mean().item() < 2e-6
+        assert (d > 1e-4).float().mean().item() < 1e-2
     assert sh.scaler.get_scale() == no.scaler.get_scale()
     # checkpoint-style reload refreshes the shadows
     with torch.no_grad():
