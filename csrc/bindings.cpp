@@ -213,6 +213,85 @@ float* f32_param(const c10::optional<Tensor>& t, int64_t C, const char* name) {
   return t->data_ptr<float>();
 }
 
+// ---- channels_last bf16 implicit-GEMM convolutions ----------------------------------------
+void check_cl_bf16(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4, name,
+              " must be a 4-d bf16 GPU tensor");
+  TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name, " must be channels_last contiguous");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+// Returns {y, psum, psq} (psum/psq empty unless want_stats): y = conv2d(x, w, stride, pad).
+std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bool want_stats) {
+  check_cl_bf16(x, "x");
+  check_cl_bf16(w, "w");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int Cout = w.size(0), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(w.size(1) == C, "conv_fwd: channel mismatch");
+  TORCH_CHECK(dpt::conv_supported(C, Cout), "conv_fwd: needs C % 64 == 0 and Cout % 64 == 0");
+  TORCH_CHECK(stride >= 1 && pad >= 0, "conv_fwd: bad stride/pad");
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "conv_fwd: empty output");
+  auto y = at::empty({N, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor ps, pq;
+  if (want_stats) {
+    const int mt = dpt::conv_m_tiles((int64_t)N * Ho * Wo);
+    ps = at::empty({Cout, mt}, x.options().dtype(at::kFloat));
+    pq = at::empty({Cout, mt}, x.options().dtype(at::kFloat));
+  }
+  c10::hip::HIPGuard guard(x.device().index());
+  dpt::launch_conv_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                       reinterpret_cast<uint16_t*>(y.data_ptr()), N, H, W, C, Cout, R, S, (int)stride, (int)pad,
+                       want_stats ? ps.data_ptr<float>() : nullptr, want_stats ? pq.data_ptr<float>() : nullptr,
+                       cur_stream(x));
+  return {y, ps, pq};
+}
+
+// dx = conv2d backward-data for a stride-1 conv: the forward kernel on dy with the flipped,
+// transposed weight (returned too, so a caller can reuse it).
+std::vector<Tensor> conv_dgrad(Tensor dy, Tensor w, int64_t pad) {
+  check_cl_bf16(dy, "grad_output");
+  check_cl_bf16(w, "w");
+  const int Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(dy.size(1) == Cout, "conv_dgrad: channel mismatch");
+  TORCH_CHECK(dpt::conv_supported(Cout, C), "conv_dgrad: needs C % 64 == 0 and Cout % 64 == 0");
+  TORCH_CHECK(R - 1 - pad >= 0 && S == R, "conv_dgrad: needs square kernel and pad <= R-1");
+  auto wt = at::empty({C, Cout, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(dy.device().index());
+  auto st = cur_stream(dy);
+  dpt::launch_conv_wt_flip(reinterpret_cast<const uint16_t*>(w.data_ptr()), reinterpret_cast<uint16_t*>(wt.data_ptr()),
+                           Cout, R, S, C, st);
+  const int N = dy.size(0), Ho = dy.size(2), Wo = dy.size(3);
+  auto dx = at::empty({N, C, Ho, Wo}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dpt::launch_conv_fwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(wt.data_ptr()),
+                       reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, 1, (int)(R - 1 - pad),
+                       nullptr, nullptr, st);
+  return {dx, wt};
+}
+
+// dw = conv2d backward-weight (fp32 or bf16 output, KRSC = channels_last [Cout, C, R, S]).
+Tensor conv_wgrad(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stride, int64_t pad, bool fp32_out) {
+  check_cl_bf16(dy, "grad_output");
+  check_cl_bf16(x, "x");
+  TORCH_CHECK(wshape.size() == 4, "conv_wgrad: weight shape must be [Cout, C, R, S]");
+  const int Cout = wshape[0], C = wshape[1], R = wshape[2], S = wshape[3];
+  const int N = x.size(0), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(x.size(1) == C && dy.size(1) == Cout && dy.size(0) == N, "conv_wgrad: shape mismatch");
+  TORCH_CHECK(dpt::conv_supported(C, Cout), "conv_wgrad: needs C % 64 == 0 and Cout % 64 == 0");
+  auto pl = dpt::conv_wgrad_plan(N, H, W, C, Cout, R, S, (int)stride, (int)pad);
+  TORCH_CHECK(dy.size(2) == pl.Ho && dy.size(3) == pl.Wo, "conv_wgrad: grad_output spatial mismatch");
+  TORCH_CHECK((int64_t)N * pl.Ho * pl.Wo < (1ll << 31), "conv_wgrad: too many pixels");
+  auto dw = at::empty({Cout, C, R, S}, x.options().dtype(fp32_out ? at::kFloat : at::kBFloat16)
+                                          .memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t pf = pl.splits == 1 && !fp32_out ? (int64_t)Cout * C * R * S : pl.part_floats;
+  auto part = at::empty({std::max<int64_t>(pf, 4)}, x.options().dtype(at::kFloat));
+  c10::hip::HIPGuard guard(x.device().index());
+  dpt::launch_conv_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                         part.data_ptr<float>(), dw.data_ptr(), fp32_out ? 0 : 1, N, H, W, C, Cout, R, S, (int)stride,
+                         (int)pad, pl, cur_stream(x));
+  return dw;
+}
+
 std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::optional<Tensor> weight,
                                  c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
                                  c10::optional<Tensor> running_var, c10::optional<Tensor> num_batches,
@@ -554,6 +633,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("stride"), py::arg("pad"));
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("grad_output"), py::arg("idx"), py::arg("H"), py::arg("W"),
         py::arg("k"), py::arg("stride"), py::arg("pad"));
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"));
+  m.def("conv_wgrad", &conv_wgrad, py::arg("grad_output"), py::arg("x"), py::arg("weight_shape"), py::arg("stride"),
+        py::arg("pad"), py::arg("fp32_out"));
+  m.def("conv_set_variant", &dpt::conv_set_variant, py::arg("variant"));
+  m.def("conv_dgrad", &conv_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
 
   py::class_<dpt::RcclComm, std::shared_ptr<dpt::RcclComm>>(m, "RcclComm")

@@ -1,0 +1,663 @@
+// Channels-last bf16 convolutions as implicit GEMMs on the gfx950 matrix cores.
+//
+// Why: in a ResNet-50 bf16 step on MI355X the MIOpen/CK convolutions run at ~430 TFLOP/s
+// averaged over forward, backward-data and backward-weight (17% of the 2.5 PF dense peak),
+// and every conv output is re-read by a separate BatchNorm statistics pass.  Owning the conv
+// lets the epilogue emit the BatchNorm partial sums (sum, sum of squares per output channel)
+// while the tile is still on chip, so the BN statistics pass disappears.
+//
+// GEMM view (channels_last activations are row-major [pixels, channels]):
+//   forward   y[m, co]  = sum_{r,s,ci} x[pix(m) + (r,s), ci] * w[co, r, s, ci]
+//             M = N*Ho*Wo, N = Cout, K = R*S*Cin; A rows gathered per (r, s) tap (zero padding
+//             = rows outside the image), B = the KRSC weight itself (K-contiguous rows).
+//   dgrad     (stride 1) the same kernel on dy with the flipped/transposed weight
+//             wt[ci, r', s', co] = w[co, R-1-r', S-1-s', ci] and pad' = R-1-pad.
+//
+// Tile: 128 (pixels) x BN (channels) x 64 (K), 256 threads = 4 waves, each wave a 32*MI x 64
+// sub-tile of v_mfma_f32_32x32x16_bf16 accumulators.  Operands are register-staged into a
+// double-buffered LDS image with 128-byte rows whose 16-byte chunks are XOR-swizzled by
+// (row>>1)&7, so the 16 rows one ds_read_b128 quarter-wave touches land on distinct banks.
+// One barrier per K-step: tile t+1's global loads are in flight while tile t is multiplied.
+// Epilogue: accumulators -> bf16 -> LDS (row-padded image) -> coalesced 16-byte row stores;
+// the optional BN statistics are summed from the bf16-rounded values (exactly what a BN
+// pass over y would read) and written as per-M-tile partials [Cout][m_tiles], the layout
+// bn_fwd_finalize_kernel consumes.
+//
+// Blocks are numbered so the BN-tiles of one M-tile (which share the same A rows) are
+// consecutive and land on the same XCD (bijective XCD remap, cdna_hip_programming.md T1).
+#include <algorithm>
+#include <cstdlib>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace dpt {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+namespace conv {
+
+constexpr int BM = 128;
+constexpr int BK = 64;
+constexpr int kThreads = 256;
+constexpr int kRowBytes = BK * 2;  // 128 B per staged row
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// Bijective XCD remap: consecutive logical ids share an XCD (MI355X: 8 XCDs, dispatch is
+// round-robin over them by hardware block id).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace conv
+
+struct ConvFwdArgs {
+  const uint16_t* x;  // [N, H, W, C]
+  const uint16_t* w;  // [Cout, R, S, C]
+  uint16_t* y;        // [N, Ho, Wo, Cout]
+  float* psum;        // optional BN partials [Cout][m_tiles]
+  float* psq;
+  int N, H, W, C, Ho, Wo, Cout, R, S, stride, pad;
+  int64_t M;
+  int m_tiles, n_tiles;
+};
+
+// 16 zero bytes: the global source of glds lanes whose A row falls in the zero padding.
+__device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
+
+// STAGES: LDS buffers of the K loop (2 = tile t+1 streams in while tile t is multiplied; 1 =
+// half the LDS, twice the resident blocks - for K <= 2 steps, where there is nothing to
+// overlap inside a block).  LDSEPI: stage the output tile through LDS for 16-byte row
+// stores; otherwise each lane stores its accumulator column straight from registers.
+template <int BN, int STAGES, bool LDSEPI>
+__global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs p) {
+  using namespace conv;
+  constexpr int WN = BN / 64;         // waves along N (each wave owns 64 output channels)
+  constexpr int WM = 4 / WN;          // waves along M
+  constexpr int MI = BM / (WM * 32);  // 32-row MFMA tiles per wave
+  constexpr int NI = 2;               // 32-col MFMA tiles per wave
+  constexpr int A_PER_T = BM * 8 / kThreads;  // glds instructions per wave per K-step (A)
+  constexpr int B_PER_T = BN * 8 / kThreads;  // (B)
+  constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int C_STRIDE = BN * 2 + 16;  // epilogue image row stride (bytes), padded
+  constexpr int RED = 2 * WM * BN * 4;   // BN-statistics cross-wave scratch
+  constexpr int LDS_MAIN = STAGES * STAGE;
+  constexpr int LDS_EPI = (LDSEPI ? BM * C_STRIDE : 0) + RED;
+  constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int nwg = p.m_tiles * p.n_tiles;
+  const int bid = conv::xcd_remap(blockIdx.x, nwg);
+  const int mt = bid / p.n_tiles, nt = bid % p.n_tiles;
+  const int64_t m0 = (int64_t)mt * BM;
+  const int n0 = nt * BN;
+
+  // ---- per-lane A rows, pixel coordinates fixed for the whole K loop ----
+  // One glds wave instruction fills 8 whole LDS rows lane-linearly: lane L of wave w owns
+  // LDS slot L&7 of row (A_PER_T*w + i)*8 + L/8 and loads the chunk the swizzle puts there
+  // (slot ^ ((row>>1)&7): the XOR is its own inverse).
+  int hi0[A_PER_T], wi0[A_PER_T];
+  int64_t abase[A_PER_T];
+  const int64_t HoWo = (int64_t)p.Ho * p.Wo;
+#pragma unroll
+  for (int i = 0; i < A_PER_T; ++i) {
+    const int arow = (wid * A_PER_T + i) * 8 + (lane >> 3);
+    const int achunk = (lane & 7) ^ ((arow >> 1) & 7);
+    const int64_t m = m0 + arow;
+    if (m < p.M) {
+      const int64_t n = m / HoWo;
+      const int rem = (int)(m - n * HoWo);
+      const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+      hi0[i] = ho * p.stride - p.pad;
+      wi0[i] = wo * p.stride - p.pad;
+      abase[i] = ((n * p.H + hi0[i]) * (int64_t)p.W + wi0[i]) * p.C + achunk * 8;
+    } else {
+      hi0[i] = -(1 << 28);  // never in bounds
+      wi0[i] = 0;
+      abase[i] = 0;
+    }
+  }
+  const int64_t Kg = (int64_t)p.R * p.S * p.C;
+  const uint16_t* wrow[B_PER_T];
+#pragma unroll
+  for (int i = 0; i < B_PER_T; ++i) {
+    const int brow = (wid * B_PER_T + i) * 8 + (lane >> 3);
+    const int bchunk = (lane & 7) ^ ((brow >> 1) & 7);
+    wrow[i] = p.w + (int64_t)(n0 + brow) * Kg + bchunk * 8;
+  }
+
+  const int cblocks = p.C / BK;
+  const int nk = p.R * p.S * cblocks;
+
+  // global -> LDS directly (no staging registers); wave-uniform LDS base per 1 KiB.
+  auto stage = [&](int ks, int buf) {
+    const int rs = ks / cblocks, cb = ks - rs * cblocks;
+    const int r = rs / p.S, s = rs - r * p.S;
+    const int64_t koff = ((int64_t)r * p.W + s) * p.C + cb * BK;
+    unsigned char* a = lds + buf * STAGE;
+    unsigned char* b = a + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_PER_T; ++i) {
+      const int hi = hi0[i] + r, wi = wi0[i] + s;
+      const bool ok = (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
+      const void* src = ok ? (const void*)(p.x + abase[i] + koff) : (const void*)g_conv_zero16;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(a + (wid * A_PER_T + i) * 1024),
+                                       16, 0, 0);
+    }
+    const int64_t wk = (int64_t)rs * p.C + cb * BK;
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(wrow[i] + wk),
+                                       (__attribute__((address_space(3))) void*)(b + (wid * B_PER_T + i) * 1024),
+                                       16, 0, 0);
+  };
+
+  f32x16_t acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int lr = lane & 31, lh = lane >> 5;
+  auto mma = [&](int buf) {
+    const unsigned char* a = lds + buf * STAGE;
+    const unsigned char* b = a + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const int ch = kk * 2 + lh;
+      bf16x8_t fa[MI], fb[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wm * (MI * 32) + i * 32 + lr;
+        fa[i] = *reinterpret_cast<const bf16x8_t*>(a + row * kRowBytes + conv::swz(row, ch) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int row = wn * 64 + j * 32 + lr;
+        fb[j] = *reinterpret_cast<const bf16x8_t*>(b + row * kRowBytes + conv::swz(row, ch) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (STAGES == 2) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ks = 0; ks < nk; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < nk) stage(ks + 1, cur ^ 1);
+      mma(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    for (int ks = 0; ks < nk; ++ks) {
+      stage(ks, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      mma(0);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: bf16 rounding, BN partial sums, stores ----
+  // accumulator map (32x32x16): column = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5)
+  const bool stats = p.psum != nullptr;
+  float cs[NI], cq[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) { cs[j] = 0.f; cq[j] = 0.f; }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = wn * 64 + j * 32 + lr;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = wm * (MI * 32) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        const uint16_t h = f32_to_bf16(acc[i][j][e]);
+        if (LDSEPI) {
+          *reinterpret_cast<uint16_t*>(lds + row * C_STRIDE + col * 2) = h;
+        } else if (m0 + row < p.M) {
+          p.y[(m0 + row) * p.Cout + n0 + col] = h;
+        }
+        const float v = bf16_to_f32(h);
+        // rows past M hold exact zeros (their A rows were zero-filled): no effect on the sums
+        cs[j] += v;
+        cq[j] += v * v;
+      }
+    }
+  float* red = reinterpret_cast<float*>(lds + (LDSEPI ? BM * C_STRIDE : 0));  // [2][WM][BN]
+  if (stats) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+      cq[j] += __shfl_xor(cq[j], 32, 64);
+      if (lh == 0) {
+        const int col = wn * 64 + j * 32 + lr;
+        red[wm * BN + col] = cs[j];
+        red[WM * BN + wm * BN + col] = cq[j];
+      }
+    }
+  }
+  if (!LDSEPI && !stats) return;
+  __syncthreads();
+  if (stats && tid < BN) {
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
+    p.psum[(int64_t)(n0 + tid) * p.m_tiles + mt] = s;
+    p.psq[(int64_t)(n0 + tid) * p.m_tiles + mt] = q;
+  }
+  if (LDSEPI) {
+    constexpr int CPR = BN / 8;          // 16-byte chunks per output row
+    constexpr int RPP = kThreads / CPR;  // rows per pass
+    const int oc = tid % CPR, orow = tid / CPR;
+#pragma unroll
+    for (int r0 = 0; r0 < BM; r0 += RPP) {
+      const int row = r0 + orow;
+      const int64_t m = m0 + row;
+      if (m < p.M) {
+        const uint4 v = *reinterpret_cast<const uint4*>(lds + row * C_STRIDE + oc * 16);
+        *reinterpret_cast<uint4*>(p.y + m * p.Cout + n0 + oc * 8) = v;
+      }
+    }
+  }
+}
+
+// ---- backward-weight: dW[co, (r,s,ci)] = sum_m dy[m, co] * x[pix(m) + (r,s), ci] -------------
+//
+// The reduction runs over pixels, the ROW index of both channels_last operands, so both are
+// staged into LDS exactly as they sit in memory ([pixel][channel] rows, filled by glds) and
+// the MFMA fragments (8 consecutive pixels of one channel per lane) are taken with the gfx950
+// transposing read ds_read_b64_tr_b16 (cdna_hip_programming.md T10).  Row chunks are
+// XOR-swizzled (256-B rows: ch ^ ((row&3)<<2 | (row>>2)&3); 128-B rows: ch ^ ((row>>1)&1)<<2
+// | (row>>2)&3) so the 4 rows x 32 columns one 32-lane half reads hit 64 distinct banks.
+// Output tiles: BMW output channels x BNW input channels of one tap (r,s); the pixel range is
+// split over `splits` blocks per tile (split-K), each writing an fp32 partial
+// [split][Cout][R*S*Cin] summed by conv_wgrad_reduce_kernel (deterministic, no atomics).
+struct FastDiv {  // n / d for 0 <= n < 2^31 via a 32-bit multiply-high
+  uint32_t d, mul, shr;
+};
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return f.d == 1 ? n : (__umulhi(n, f.mul) >> f.shr);
+}
+
+struct ConvWgradArgs {
+  const uint16_t* dy;  // [N, Ho, Wo, Cout]
+  const uint16_t* x;   // [N, H, W, C]
+  float* part;         // [splits][Cout][R*S*C]
+  int N, H, W, C, Ho, Wo, Cout, R, S, stride, pad;
+  int M;               // N*Ho*Wo (< 2^31)
+  int co_tiles, n_tiles, splits, steps_per_split;
+  FastDiv div_wo, div_howo;
+  int direct;          // 1x1, stride 1, pad 0: x row = dy row
+};
+
+template <int RB>  // row bytes of the LDS image: 256 (128 channels) or 128 (64 channels)
+__device__ __forceinline__ int wg_slot(int row, int ch) {
+  if (RB == 256) return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
+  return ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
+}
+
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+
+// 4 consecutive rows (k) x this lane's column, two tr-reads -> one 8-element bf16 fragment
+template <int RB>
+__device__ __forceinline__ bf16x8_t wg_frag(const unsigned char* img, int krow0, int col0, int lane) {
+  // 16-lane group g reads rows krow0 + 8*(g>>1) + {0..3} (then +4) and columns col0 + 16*(g&1) + 0..15
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int colb = col0 + 16 * (g & 1) + 4 * pp;  // this lane's 4 columns
+  const int ch = colb >> 3, sub = (colb & 7) * 2;
+  const int r1 = krow0 + 8 * (g >> 1) + q, r2 = r1 + 4;
+  typedef __attribute__((address_space(3))) i16x4_t lds_v4;
+  const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(img + r1 * RB + wg_slot<RB>(r1, ch) * 16 + sub));
+  const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(img + r2 * RB + wg_slot<RB>(r2, ch) * 16 + sub));
+  typedef short i16x8_t __attribute__((ext_vector_type(8)));
+  i16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <int BMW, int BNW, int STAGES>
+__global__ __launch_bounds__(conv::kThreads, 2) void conv_wgrad_kernel(ConvWgradArgs p) {
+  using namespace conv;
+  constexpr int BKP = 64;                   // pixels per K-step
+  constexpr int RBA = BMW * 2, RBB = BNW * 2;  // LDS row bytes (dy image, x image)
+  constexpr int A_BYTES = BKP * RBA, B_BYTES = BKP * RBB;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = A_BYTES / 1024 / 4;  // glds instructions per wave per tile
+  constexpr int B_INSTR = B_BYTES / 1024 / 4;
+  constexpr int A_RPI = 1024 / RBA, B_RPI = 1024 / RBB;  // rows per glds instruction
+  constexpr int WTM = BMW / 2, WTN = BNW / 2;  // wave tile (2 x 2 waves)
+  constexpr int MI = WTM / 32, NI = WTN / 32;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[STAGES * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles = p.co_tiles * p.n_tiles;
+  const int bid = conv::xcd_remap(blockIdx.x, tiles * p.splits);
+  const int sp = bid / tiles, tile = bid - sp * tiles;
+  const int ct = tile / p.n_tiles, nt = tile - ct * p.n_tiles;
+  const int co0 = ct * BMW;
+  const int cblocks = p.C / BNW;
+  const int rs = nt / cblocks, cb = nt - rs * cblocks;
+  const int r = rs / p.S, s = rs - r * p.S;
+  const int ci0 = cb * BNW;
+  const int k0 = sp * p.steps_per_split;
+  const int k1 = min(k0 + p.steps_per_split, (p.M + BKP - 1) / BKP);
+
+  // per-lane glds rows/chunks (lane-linear images, source-side swizzle)
+  int arow[A_INSTR], achk[A_INSTR], brow[B_INSTR], bchk[B_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    arow[i] = (wid * A_INSTR + i) * A_RPI + lane / (RBA / 16);
+    achk[i] = wg_slot<RBA>(arow[i], lane % (RBA / 16));
+  }
+#pragma unroll
+  for (int i = 0; i < B_INSTR; ++i) {
+    brow[i] = (wid * B_INSTR + i) * B_RPI + lane / (RBB / 16);
+    bchk[i] = wg_slot<RBB>(brow[i], lane % (RBB / 16));
+  }
+
+  auto stage = [&](int ks, int buf) {
+    unsigned char* a = lds + buf * STAGE;
+    unsigned char* b = a + A_BYTES;
+    const int mb = ks * BKP;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i) {
+      const int m = mb + arow[i];
+      const void* src = m < p.M ? (const void*)(p.dy + (int64_t)m * p.Cout + co0 + achk[i] * 8)
+                                : (const void*)g_conv_zero16;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(a + (wid * A_INSTR + i) * 1024),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i) {
+      const int m = mb + brow[i];
+      const void* src = (const void*)g_conv_zero16;
+      if (m < p.M) {
+        if (p.direct) {
+          src = p.x + (int64_t)m * p.C + ci0 + bchk[i] * 8;
+        } else {
+          const uint32_t n = fdiv((uint32_t)m, p.div_howo);
+          const uint32_t rem = (uint32_t)m - n * (uint32_t)(p.Ho * p.Wo);
+          const uint32_t ho = fdiv(rem, p.div_wo), wo = rem - ho * (uint32_t)p.Wo;
+          const int hi = (int)ho * p.stride - p.pad + r, wi = (int)wo * p.stride - p.pad + s;
+          if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+            src = p.x + (((int64_t)n * p.H + hi) * p.W + wi) * p.C + ci0 + bchk[i] * 8;
+        }
+      }
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(b + (wid * B_INSTR + i) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x16_t acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  auto mma = [&](int buf) {
+    const unsigned char* a = lds + buf * STAGE;
+    const unsigned char* b = a + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BKP / 16; ++kk) {
+      bf16x8_t fa[MI], fb[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = wg_frag<RBA>(a, kk * 16, wm * WTM + i * 32, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) fb[j] = wg_frag<RBB>(b, kk * 16, wn * WTN + j * 32, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  if (STAGES == 2) {
+    if (k0 < k1) {
+      stage(k0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int ks = k0; ks < k1; ++ks) {
+        const int cur = (ks - k0) & 1;
+        if (ks + 1 < k1) stage(ks + 1, cur ^ 1);
+        mma(cur);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    }
+  } else {
+    for (int ks = k0; ks < k1; ++ks) {
+      stage(ks, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      mma(0);
+      __syncthreads();
+    }
+  }
+  // fp32 partial tile: rows = output channels, columns = (r, s, ci) of this tap
+  const int64_t Kg = (int64_t)p.R * p.S * p.C;
+  float* out = p.part + (int64_t)sp * p.Cout * Kg + (int64_t)rs * p.C + ci0;
+  const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = wn * WTN + j * 32 + lr;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = co0 + wm * WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        out[(int64_t)row * Kg + col] = acc[i][j][e];
+      }
+    }
+}
+
+// out[i] = sum_s part[s][i]: PH phases per block split the S loop, LDS combines them.
+template <int PH>
+__global__ __launch_bounds__(kBlock) void conv_wgrad_reduce_kernel(const float4* __restrict__ part, int64_t n4,
+                                                                   int S, void* __restrict__ out, int out_kind) {
+  constexpr int OUT = kBlock / PH;
+  __shared__ float4 red[kBlock];
+  const int o = threadIdx.x % OUT, ph = threadIdx.x / OUT;
+  const int64_t v = (int64_t)blockIdx.x * OUT + o;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (v < n4) {
+    int q = ph;
+    for (; q + 3 * PH < S; q += 4 * PH) {
+      const float4 b0 = part[(int64_t)q * n4 + v], b1 = part[(int64_t)(q + PH) * n4 + v];
+      const float4 b2 = part[(int64_t)(q + 2 * PH) * n4 + v], b3 = part[(int64_t)(q + 3 * PH) * n4 + v];
+      a.x += (b0.x + b1.x) + (b2.x + b3.x);
+      a.y += (b0.y + b1.y) + (b2.y + b3.y);
+      a.z += (b0.z + b1.z) + (b2.z + b3.z);
+      a.w += (b0.w + b1.w) + (b2.w + b3.w);
+    }
+    for (; q < S; q += PH) {
+      const float4 b = part[(int64_t)q * n4 + v];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+  }
+  red[threadIdx.x] = a;
+  __syncthreads();
+  if (ph != 0 || v >= n4) return;
+#pragma unroll
+  for (int k = 1; k < PH; ++k) {
+    const float4 b = red[k * OUT + o];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  if (out_kind == 0) {
+    static_cast<float4*>(out)[v] = a;
+  } else {
+    uint2 w;
+    w.x = (uint32_t)f32_to_bf16(a.x) | ((uint32_t)f32_to_bf16(a.y) << 16);
+    w.y = (uint32_t)f32_to_bf16(a.z) | ((uint32_t)f32_to_bf16(a.w) << 16);
+    static_cast<uint2*>(out)[v] = w;
+  }
+}
+
+// wt[ci, r', s', co] = w[co, R-1-r', S-1-s', ci]: the backward-data operand of a stride-1 conv.
+__global__ __launch_bounds__(kBlock) void conv_wt_flip_kernel(const uint16_t* __restrict__ w,
+                                                              uint16_t* __restrict__ wt, int Cout, int R,
+                                                              int S, int C) {
+  const int64_t n = (int64_t)Cout * R * S * C;
+  for (int64_t o = (int64_t)blockIdx.x * kBlock + threadIdx.x; o < n; o += (int64_t)gridDim.x * kBlock) {
+    // o indexes wt = [C][R][S][Cout]
+    const int co = (int)(o % Cout);
+    int64_t t = o / Cout;
+    const int s = (int)(t % S);
+    t /= S;
+    const int r = (int)(t % R);
+    const int ci = (int)(t / R);
+    wt[o] = w[(((int64_t)co * R + (R - 1 - r)) * S + (S - 1 - s)) * C + ci];
+  }
+}
+
+bool conv_supported(int C, int Cout) { return C % 64 == 0 && Cout % 64 == 0; }
+
+int conv_m_tiles(int64_t M) { return (int)((M + conv::BM - 1) / conv::BM); }
+
+// Kernel variant: 0 = default (1-stage + LDS epilogue), 1 = 2-stage + LDS epilogue, 2 = 2-stage +
+// register epilogue, 3 = 1-stage + register epilogue, 4 = 1-stage + LDS epilogue.
+// The backward-weight kernel takes 1-2 -> 2 stages, 0/3-4 -> 1 stage.
+// DPT_CONV_VARIANT overrides; conv_set_variant switches at run time (A/B tests, benchmarks).
+static int g_conv_variant = -1;
+static int conv_variant() {
+  if (g_conv_variant < 0) {
+    const char* e = std::getenv("DPT_CONV_VARIANT");
+    g_conv_variant = e ? std::atoi(e) : 0;
+  }
+  return g_conv_variant;
+}
+void conv_set_variant(int v) { g_conv_variant = v; }
+
+
+template <int BN>
+static void conv_fwd_dispatch(int variant, int nk, const ConvFwdArgs& a, dim3 grid, hipStream_t s) {
+  (void)nk;
+  if (variant == 0) variant = 4;  // measured best at every ResNet-50 shape but two (profiles/conv_*.md)
+  const dim3 block(conv::kThreads);
+  switch (variant) {
+    case 2: hipLaunchKernelGGL((conv_fwd_kernel<BN, 2, false>), grid, block, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((conv_fwd_kernel<BN, 1, false>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((conv_fwd_kernel<BN, 1, true>), grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL((conv_fwd_kernel<BN, 2, true>), grid, block, 0, s, a); break;
+  }
+}
+
+void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
+                     int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s) {
+  ConvFwdArgs a;
+  a.x = x; a.w = w; a.y = y; a.psum = psum; a.psq = psq;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S; a.stride = stride; a.pad = pad;
+  a.Ho = (H + 2 * pad - R) / stride + 1;
+  a.Wo = (W + 2 * pad - S) / stride + 1;
+  a.M = (int64_t)N * a.Ho * a.Wo;
+  a.m_tiles = conv_m_tiles(a.M);
+  const bool wide = Cout % 128 == 0;
+  a.n_tiles = Cout / (wide ? 128 : 64);
+  const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
+  const int nk = R * S * (C / conv::BK);
+  if (wide) conv_fwd_dispatch<128>(conv_variant(), nk, a, grid, s);
+  else conv_fwd_dispatch<64>(conv_variant(), nk, a, grid, s);
+}
+
+static FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  if (d <= 1) { f.mul = 0; f.shr = 0; return f; }
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;  // l = ceil(log2 d) >= 1
+  // mul = ceil(2^(31+l) / d) < 2^32; q = mulhi(n, mul) >> (l-1) is exact for n < 2^31
+  // (error term n * (mul - 2^(31+l)/d) / 2^(31+l) < 1/d).
+  f.mul = (uint32_t)(((1ull << (31 + l)) + d - 1) / d);
+  f.shr = l - 1;
+  return f;
+}
+
+ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad) {
+  ConvWgradPlan pl;
+  pl.Ho = (H + 2 * pad - R) / stride + 1;
+  pl.Wo = (W + 2 * pad - S) / stride + 1;
+  const int64_t M = (int64_t)N * pl.Ho * pl.Wo;
+  pl.bmw = Cout % 128 == 0 ? 128 : 64;
+  pl.bnw = C % 128 == 0 ? 128 : 64;
+  const int tiles = (Cout / pl.bmw) * (R * S * (C / pl.bnw));
+  const int steps = (int)((M + 63) / 64);
+  // ~768 blocks (3 per CU) and at least 32 K-steps per split: a split's fp32 partial tile
+  // (BMW x BNW x 4 B, written once and read once by the reduce) then costs < 1/8 of the
+  // operand bytes it streams.
+  int splits = (768 + tiles - 1) / tiles;
+  splits = std::max(1, std::min(splits, steps / 32));
+  pl.steps_per_split = (steps + splits - 1) / splits;
+  pl.splits = (steps + pl.steps_per_split - 1) / pl.steps_per_split;
+  pl.part_floats = pl.splits > 1 ? (int64_t)pl.splits * Cout * R * S * C : 0;
+  return pl;
+}
+
+void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void* dw, int dw_kind, int N, int H,
+                       int W, int C, int Cout, int R, int S, int stride, int pad, const ConvWgradPlan& pl,
+                       hipStream_t st) {
+  ConvWgradArgs a;
+  const bool direct_out = pl.splits == 1 && dw_kind == 0;  // fp32 result written in place
+  a.dy = dy; a.x = x; a.part = direct_out ? static_cast<float*>(dw) : part;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S; a.stride = stride; a.pad = pad;
+  a.Ho = pl.Ho; a.Wo = pl.Wo;
+  a.M = N * pl.Ho * pl.Wo;
+  a.co_tiles = Cout / pl.bmw;
+  a.n_tiles = R * S * (C / pl.bnw);
+  a.splits = pl.splits;
+  a.steps_per_split = pl.steps_per_split;
+  a.div_wo = make_fastdiv((uint32_t)pl.Wo);
+  a.div_howo = make_fastdiv((uint32_t)(pl.Ho * pl.Wo));
+  a.direct = (R == 1 && S == 1 && stride == 1 && pad == 0) ? 1 : 0;
+  const dim3 grid((unsigned)(a.co_tiles * a.n_tiles * a.splits)), block(conv::kThreads);
+  const int v = conv_variant();
+  if (v == 1 || v == 2) {
+    if (pl.bmw == 128 && pl.bnw == 128) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 2>), grid, block, 0, st, a);
+    else if (pl.bmw == 128) hipLaunchKernelGGL((conv_wgrad_kernel<128, 64, 2>), grid, block, 0, st, a);
+    else if (pl.bnw == 128) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 2>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<64, 64, 2>), grid, block, 0, st, a);
+  } else {
+    if (pl.bmw == 128 && pl.bnw == 128) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 1>), grid, block, 0, st, a);
+    else if (pl.bmw == 128) hipLaunchKernelGGL((conv_wgrad_kernel<128, 64, 1>), grid, block, 0, st, a);
+    else if (pl.bnw == 128) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 1>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<64, 64, 1>), grid, block, 0, st, a);
+  }
+  if (direct_out) return;
+  const int64_t n4 = (int64_t)Cout * R * S * C / 4;
+  if (pl.splits >= 16) {
+    hipLaunchKernelGGL(conv_wgrad_reduce_kernel<16>, dim3((unsigned)((n4 + 15) / 16)), dim3(kBlock), 0, st,
+                       reinterpret_cast<const float4*>(part), n4, pl.splits, dw, dw_kind);
+  } else if (pl.splits >= 4) {
+    hipLaunchKernelGGL(conv_wgrad_reduce_kernel<4>, dim3((unsigned)((n4 + 63) / 64)), dim3(kBlock), 0, st,
+                       reinterpret_cast<const float4*>(part), n4, pl.splits, dw, dw_kind);
+  } else {
+    hipLaunchKernelGGL(conv_wgrad_reduce_kernel<1>, dim3((unsigned)((n4 + 255) / 256)), dim3(kBlock), 0, st,
+                       reinterpret_cast<const float4*>(part), n4, pl.splits, dw, dw_kind);
+  }
+}
+
+void launch_conv_wt_flip(const uint16_t* w, uint16_t* wt, int Cout, int R, int S, int C, hipStream_t s) {
+  const int64_t n = (int64_t)Cout * R * S * C;
+  hipLaunchKernelGGL(conv_wt_flip_kernel, dim3((unsigned)grid_for(n, 4)), dim3(kBlock), 0, s, w, wt, Cout, R, S, C);
+}
+
+}  // namespace dpt

@@ -105,4 +105,25 @@ void launch_sum_partials(const float* part, int64_t n, int S, void* out, int out
 void launch_rows_copy16(const uint16_t* src, uint16_t* dst, const int n[4], const int64_t ss[4], const int64_t ds[4],
                         int L, hipStream_t s);
 
+// conv_kernels.hip: channels_last bf16 implicit-GEMM convolutions (MFMA).  x [N,H,W,C],
+// w [Cout,R,S,C], y [N,Ho,Wo,Cout]; C % 64 == 0, Cout % 64 == 0.  psum/psq (optional): BN
+// partial sums of y per (channel, M-tile), layout [Cout][conv_m_tiles(M)].
+bool conv_supported(int C, int Cout);
+int conv_m_tiles(int64_t M);
+void conv_set_variant(int v);
+void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
+                     int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s);
+// backward-weight: dw [Cout,R,S,C] (kind 0 f32 / 1 bf16) = sum over pixels of dy x x-shifted;
+// part: plan.part_floats floats of split-K scratch.  C % 64 == 0, Cout % 64 == 0.
+struct ConvWgradPlan {
+  int Ho, Wo, bmw, bnw, splits, steps_per_split;
+  int64_t part_floats;
+};
+ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad);
+void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void* dw, int dw_kind, int N, int H,
+                       int W, int C, int Cout, int R, int S, int stride, int pad, const ConvWgradPlan& plan,
+                       hipStream_t s);
+// wt[ci, r, s, co] = w[co, R-1-r, S-1-s, ci]
+void launch_conv_wt_flip(const uint16_t* w, uint16_t* wt, int Cout, int R, int S, int C, hipStream_t s);
+
 }  // namespace dpt
