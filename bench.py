@@ -54,6 +54,7 @@ def parse(argv=None):
                          "immediate mode, which reads the find-db shipped in miopen_db/ (tuned on MI355X "
                          "for this config) and skips the search")
     ap.add_argument("--cuda-graph", action="store_true", help="replay the captured step as a hipGraph")
+    ap.add_argument("--no-native-conv", action="store_true", help="A/B: MIOpen convolutions")
     ap.add_argument("--no-weight-shadow", action="store_true",
                     help="A/B: autocast casts fp32 weights every forward (no optimizer-kept bf16 copy)")
     ap.add_argument("--profile-steps", type=int, default=0,
@@ -80,6 +81,8 @@ def train_args(a):
         argv.append("--cuda-graph")
     if a.no_weight_shadow:
         argv.append("--no-weight-shadow")
+    if a.no_native_conv:
+        argv.append("--no-native-conv")
     return parse_args(argv)
 
 
@@ -156,6 +159,8 @@ def main(argv=None) -> int:
                    "impl": a.impl, "optimizer": a.optimizer, "channels_last": bool(args.channels_last),
                    "bucket_cap_mb": a.bucket_cap_mb, "grad_dtype": a.grad_dtype,
                    "fused_bn": bool(args.fused_bn and a.impl == "native" and args.channels_last),
+                   "native_conv": bool(args.native_conv and args.fused_bn and a.impl == "native"
+                                       and args.channels_last and args.amp and args.amp_dtype == "bf16"),
                    "miopen": "find" if a.find else "immediate(find-db)",
                    "gemm_db": bool(gemm_db),
                    "weight_shadow": bool(trainer.ddp is not None and trainer.ddp.shadow_flat is not None),

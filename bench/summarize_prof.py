@@ -17,6 +17,7 @@ from collections import defaultdict
 
 FAMILIES = [
     ("native: optimizer (fused SGD/Adam, grad_check, tail)", r"dpt::(sgd|adam|grad_check|optim_tail)"),
+    ("native: MFMA convolutions (fwd/dgrad/wgrad + reduce/flip)", r"dpt::conv_"),
     ("native: fused BatchNorm(+add)(+ReLU)", r"dpt::bn_"),
     ("native: ViT block kernels", r"dpt::(ln_|gelu|rows_copy|colsum|sum_partials)"),
     ("native: metrics/augment/comm/pool kernels", r"dpt::"),

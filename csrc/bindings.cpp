@@ -295,7 +295,8 @@ Tensor conv_wgrad(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stri
 std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::optional<Tensor> weight,
                                  c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
                                  c10::optional<Tensor> running_var, c10::optional<Tensor> num_batches,
-                                 double momentum, double eps, bool relu) {
+                                 double momentum, double eps, bool relu, c10::optional<Tensor> psum,
+                                 c10::optional<Tensor> psq) {
   auto [M, C] = bn_rows(x, "x");
   TORCH_CHECK(dpt::bn_supported(C), "fused BN: unsupported channel count ", C);
   const void* rp = nullptr;
@@ -313,8 +314,22 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::
   auto fopt = x.options().dtype(at::kFloat);
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
   auto coef = at::empty({2 * C}, fopt);  // [a | b]: y = relu(x*a + b [+ r]); lets bn_bwd skip reading y
-  auto ws = at::empty({dpt::bn_workspace_floats(M, C)}, fopt);
   c10::hip::HIPGuard guard(x.device().index());
+  if (psum.has_value() && psum->defined()) {
+    // statistics summed by the producing conv's epilogue: [C][chunks] fp32 partials
+    TORCH_CHECK(psq.has_value() && psq->defined(), "bn_fwd_train: psum without psq");
+    TORCH_CHECK(psum->is_cuda() && psum->scalar_type() == at::kFloat && psum->dim() == 2 && psum->size(0) == C &&
+                    psum->is_contiguous() && psq->sizes() == psum->sizes() && psq->is_contiguous(),
+                "bn_fwd_train: partials must be contiguous fp32 [C, chunks]");
+    dpt::launch_bn_fwd_from_partials(bn_dtype(x), x.data_ptr(), rp, y.data_ptr(), M, C, psum->data_ptr<float>(),
+                                     psq->data_ptr<float>(), (int)psum->size(1), f32_param(weight, C, "weight"),
+                                     f32_param(bias, C, "bias"), (float)eps, (float)momentum,
+                                     f32_param(running_mean, C, "running_mean"),
+                                     f32_param(running_var, C, "running_var"), nb, mean.data_ptr<float>(),
+                                     invstd.data_ptr<float>(), coef.data_ptr<float>(), relu, cur_stream(x));
+    return {y, mean, invstd, coef};
+  }
+  auto ws = at::empty({dpt::bn_workspace_floats(M, C)}, fopt);
   dpt::launch_bn_fwd_train(bn_dtype(x), x.data_ptr(), rp, y.data_ptr(), M, C, f32_param(weight, C, "weight"),
                            f32_param(bias, C, "bias"), (float)eps, (float)momentum,
                            f32_param(running_mean, C, "running_mean"), f32_param(running_var, C, "running_var"), nb,
@@ -615,7 +630,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_supported", [](int64_t C) { return dpt::bn_supported(C); });
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("residual"), py::arg("weight"), py::arg("bias"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches"), py::arg("momentum"), py::arg("eps"),
-        py::arg("relu"));
+        py::arg("relu"), py::arg("psum") = py::none(), py::arg("psq") = py::none());
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("residual"), py::arg("a"), py::arg("b"), py::arg("relu"));
   m.def("bn_bwd", &bn_bwd, py::arg("grad_output"), py::arg("grad_output2"), py::arg("y"), py::arg("x"),
         py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("relu"), py::arg("want_dz"),

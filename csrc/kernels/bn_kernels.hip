@@ -504,6 +504,26 @@ void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int
   }
 }
 
+// BN forward whose statistics were already summed by the producing convolution's epilogue
+// (conv_kernels.hip): psum/psq are [C][chunks] partials -> finalize -> apply.
+void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
+                                 const float* psum, const float* psq, int chunks, const float* gamma,
+                                 const float* beta, float eps, float momentum, float* run_mean, float* run_var,
+                                 int64_t* num_batches, float* save_mean, float* save_invstd, float* save_coef,
+                                 bool relu, hipStream_t s) {
+  BnGeometry g = bn_geometry(M, C);
+  float* ca = save_coef;
+  float* cb = ca + C;
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), dim3(kBlock), 0, s, psum, psq, chunks,
+                     (int)C, M, gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd,
+                     ca, cb);
+  switch (dtype) {
+    case 0: fwd_apply_dispatch<F32>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
+    case 1: fwd_apply_dispatch<BF16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
+    default: fwd_apply_dispatch<F16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
+  }
+}
+
 void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                      const float* coef_a, const float* coef_b, bool relu, hipStream_t s) {
   BnGeometry g = bn_geometry(M, C);

@@ -56,6 +56,11 @@ void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int
                          const float* gamma, const float* beta, float eps, float momentum, float* run_mean,
                          float* run_var, int64_t* num_batches, float* save_mean, float* save_invstd,
                          float* save_coef, float* workspace, bool relu, hipStream_t s);
+void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
+                                 const float* psum, const float* psq, int chunks, const float* gamma,
+                                 const float* beta, float eps, float momentum, float* run_mean, float* run_var,
+                                 int64_t* num_batches, float* save_mean, float* save_invstd, float* save_coef,
+                                 bool relu, hipStream_t s);
 void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                      const float* coef_a, const float* coef_b, bool relu, hipStream_t s);
 void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, const void* x, int64_t M,

@@ -79,6 +79,9 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--no-fused-bn", dest="fused_bn", action="store_false",
                    help="native impl: keep MIOpen BatchNorm + separate ReLU/add instead of the fused "
                         "gfx950 BN(+add)(+ReLU) kernels (channels_last GPU runs)")
+    g.add_argument("--no-native-conv", dest="native_conv", action="store_false",
+                   help="native impl: run convolutions on MIOpen instead of the hand-written MFMA "
+                        "implicit-GEMM kernels (which also fuse the BatchNorm statistics pass)")
     g.add_argument("--no-weight-shadow", dest="weight_shadow", action="store_false",
                    help="native impl: let autocast cast fp32 weights every forward instead of keeping "
                         "16-bit weight shadows updated by the fused optimizer")

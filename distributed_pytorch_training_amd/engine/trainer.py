@@ -91,7 +91,9 @@ class Trainer:
         if (getattr(args, "fused_bn", True) and self.device.type == "cuda"
                 and getattr(args, "channels_last", False)):
             from ..models.layers import fuse_native_layers
+            from ..ops import conv as native_conv
             fuse_native_layers(model)
+            native_conv.ENABLED = bool(getattr(args, "native_conv", True))
         params_in_order = [p for p in model.parameters() if p.requires_grad]
         self.scaler = DeviceGradScaler(self.device, enabled=self.amp)
         shadow = None

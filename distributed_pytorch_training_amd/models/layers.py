@@ -125,6 +125,29 @@ def fuse_native_layers(model: nn.Module, gemm_1x1: bool = False) -> int:
                 new.__dict__ = child.__dict__
                 setattr(parent, name, new)
                 n += 1
+    tag_conv_bn_pairs(model)
+    return n
+
+
+def tag_conv_bn_pairs(model: nn.Module) -> int:
+    """Mark convs whose output goes straight into a fused BatchNorm (``convK`` -> ``bnK`` in a
+    block, ``(Conv2d, BatchNorm2d)`` consecutive in a Sequential): the native conv's epilogue
+    then emits that BN's statistics (ops/conv.py) and the BN skips its statistics pass."""
+    n = 0
+    for parent in model.modules():
+        kids = dict(parent.named_children())
+        pairs = []
+        if isinstance(parent, nn.Sequential):
+            seq = list(parent)
+            pairs = [(a, b) for a, b in zip(seq, seq[1:])]
+        else:
+            for name, child in kids.items():
+                if name.startswith("conv") and ("bn" + name[4:]) in kids:
+                    pairs.append((child, kids["bn" + name[4:]]))
+        for conv, bn in pairs:
+            if isinstance(conv, nn.Conv2d) and isinstance(bn, FusedBatchNorm2d) and conv.bias is None:
+                conv.dpt_bn_stats = True
+                n += 1
     return n
 
 

@@ -30,13 +30,15 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
 
 class _BNActTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu):
-        y = _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu)
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
+                partials):
+        y = _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
+                 partials=partials)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        return _bwd(ctx, dy, None) + (None,) * 6
+        return _bwd(ctx, dy, None) + (None,) * 7
 
 
 class _BNActTrainPair(torch.autograd.Function):
@@ -47,21 +49,23 @@ class _BNActTrainPair(torch.autograd.Function):
     the residual-gradient adds were ~1.3 ms of a 33 ms step)."""
 
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu):
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
+                partials):
         y = _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
-                 pair=True)
+                 pair=True, partials=partials)
         ctx.set_materialize_grads(False)  # an unused alias (last block) gives None, not zeros
         return y, y.view_as(y)
 
     @staticmethod
     def backward(ctx, dy, dy2):
-        return _bwd(ctx, dy, dy2) + (None,) * 6
+        return _bwd(ctx, dy, dy2) + (None,) * 7
 
 
 def _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
-         pair=False):
+         pair=False, partials=None):
+    ps, pq = partials if partials is not None else (None, None)
     y, mean, invstd, coef = native().bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
-                                                  num_batches, float(momentum), float(eps), bool(relu))
+                                                  num_batches, float(momentum), float(eps), bool(relu), ps, pq)
     ctx.relu = bool(relu)
     ctx.has_res = residual is not None
     mask_from_x = ctx.relu and not ctx.has_res and not pair   # pair outputs always write dz
@@ -94,8 +98,11 @@ def bn_act_train(x: torch.Tensor, residual: Optional[torch.Tensor], weight, bias
                  num_batches, momentum: float, eps: float, relu: bool, pair: bool = False):
     if residual is not None:
         residual = _cl(residual.to(x.dtype))
+    # statistics already summed by the producing native conv's epilogue (ops/conv.py)
+    partials = x.__dict__.pop("_dpt_bn_partials", None)
     fn = _BNActTrainPair if pair else _BNActTrain
-    return fn.apply(x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu)
+    return fn.apply(x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
+                    partials)
 
 
 @torch.no_grad()

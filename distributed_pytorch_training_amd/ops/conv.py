@@ -1,0 +1,101 @@
+"""Channels-last bf16 convolution autograd op on the hand-written MFMA kernels
+(csrc/kernels/conv_kernels.hip).
+
+forward   implicit-GEMM conv; with ``bn_stats`` its epilogue also emits the per-channel
+          (sum, sum of squares) partials of the bf16 output, which the following fused
+          BatchNorm consumes instead of re-reading the activation (ops/bn.py picks them up
+          from the output tensor's ``_dpt_bn_partials`` attribute).
+backward  input gradient: the same kernel on dy with the flipped/transposed weight (stride 1)
+          or MIOpen's backward-data (strided convs); weight gradient: split-K MFMA kernel
+          with transposing LDS reads, bf16 (the shadow weight's dtype).
+
+Replaces the reference's cuDNN convolutions (reference
+``train_ddp.py:205,207`` -> torchvision ``resnet18`` convs); measured per shape against MIOpen
+in ``profiles/conv_kernels_vs_miopen_v1.md``.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import native, native_available
+
+_CL = torch.channels_last
+ENABLED = os.environ.get("DPT_NATIVE_CONV", "1") != "0"
+
+
+def supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups) -> bool:
+    if not (ENABLED and x.is_cuda and native_available() and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and x.dim() == 4 and groups == 1):
+        return False
+    if tuple(dilation) != (1, 1) or stride[0] != stride[1] or padding[0] != padding[1]:
+        return False
+    cout, cin, r, s = w.shape
+    return (cin % 64 == 0 and cout % 64 == 0 and r == s and x.shape[1] == cin
+            and x.is_contiguous(memory_format=_CL))
+
+
+def _cl(t: torch.Tensor) -> torch.Tensor:
+    return t if t.is_contiguous(memory_format=_CL) else t.contiguous(memory_format=_CL)
+
+
+def _backward(ctx, dy):
+    x, w = ctx.saved_tensors
+    dy = _cl(dy.to(torch.bfloat16))
+    s, p = ctx.stride, ctx.pad
+    dx = dw = None
+    if ctx.needs_input_grad[0]:
+        if s == 1:
+            dx = native().conv_dgrad(dy, w, p)[0]
+        else:
+            dx = torch.ops.aten.convolution_backward(dy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
+                                                     (True, False, False))[0]
+    if ctx.needs_input_grad[1]:
+        dw = native().conv_wgrad(dy, x, list(w.shape), s, p, False)
+    return dx, dw
+
+
+class _Conv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride: int, pad: int):
+        y = native().conv_fwd(x, w, stride, pad, False)[0]
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.pad = stride, pad
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _backward(ctx, dy) + (None, None)
+
+
+class _ConvStats(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride: int, pad: int):
+        y, ps, pq = native().conv_fwd(x, w, stride, pad, True)
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.pad = stride, pad
+        ctx.mark_non_differentiable(ps, pq)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the statistics outputs
+        return y, ps, pq
+
+    @staticmethod
+    def backward(ctx, dy, _dps, _dpq):
+        return _backward(ctx, dy) + (None, None)
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bool = False) -> torch.Tensor:
+    """y = conv2d(x, w, stride, pad) on the MFMA kernels; ``bn_stats`` attaches the output's
+    BatchNorm partial sums as ``y._dpt_bn_partials`` (consumed by ops/bn.py)."""
+    w = _cl(w)
+    if not bn_stats:
+        return _Conv.apply(x, w, int(stride), int(pad))
+    y, ps, pq = _ConvStats.apply(x, w, int(stride), int(pad))
+    y._dpt_bn_partials = (ps, pq)
+    return y
+
+
+def take_bn_partials(x: torch.Tensor):
+    """The (psum, psq) partials a native conv attached to ``x``, once (None otherwise)."""
+    part = x.__dict__.pop("_dpt_bn_partials", None)
+    return part

@@ -22,6 +22,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import conv as native_conv
+
 SHADOW_ATTR = "_dpt_shadow"
 
 
@@ -35,11 +37,18 @@ def active_shadow(mod: nn.Module, x: torch.Tensor):
 
 
 class ShadowConv2d(nn.Conv2d):
+    # set by fuse_native_layers on convs that feed a fused BatchNorm: the native conv's
+    # epilogue then also emits the BN statistics partials
+    dpt_bn_stats = False
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         sh = active_shadow(self, x)
         if sh is None:
             return super().forward(x)
-        return self._conv_forward(x, sh["weight"], sh.get("bias", self.bias))
+        w, b = sh["weight"], sh.get("bias", self.bias)
+        if b is None and native_conv.supported(x, w, self.stride, self.padding, self.dilation, self.groups):
+            return native_conv.conv2d(x, w, self.stride[0], self.padding[0], self.dpt_bn_stats)
+        return self._conv_forward(x, w, b)
 
 
 class ShadowLinear(nn.Linear):

@@ -87,3 +87,71 @@ def test_conv_wgrad_large_split(cuda):
     dw = ops.native().conv_wgrad(gy, x, list(w.shape), 1, 0, True)
     ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, gy.float())
     torch.testing.assert_close(dw, ref, rtol=1e-3, atol=1e-2)
+
+
+def test_bn_from_conv_partials_matches_stats_pass(cuda):
+    """Fused BN fed by the conv epilogue's partial sums == fused BN with its own stats pass."""
+    x, w = _operands(cuda, 4, 128, 14, 14, 256, 3, seed=4)
+    C_ = ops.native()
+    y, ps, pq = C_.conv_fwd(x, w, 1, 1, True)
+    g = torch.rand(256, device=cuda) + 0.5
+    b = torch.randn(256, device=cuda)
+    outs = []
+    for part in ((ps, pq), (None, None)):
+        rm, rv = torch.zeros(256, device=cuda), torch.ones(256, device=cuda)
+        nb = torch.zeros((), dtype=torch.long, device=cuda)
+        o, mean, invstd, coef = C_.bn_fwd_train(y, None, g, b, rm, rv, nb, 0.1, 1e-5, True, *part)
+        outs.append((o, mean, invstd, rm, rv, nb))
+    (o1, m1, i1, rm1, rv1, nb1), (o2, m2, i2, rm2, rv2, nb2) = outs
+    torch.testing.assert_close(m1, m2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(i1, i2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv1, rv2, rtol=1e-5, atol=1e-6)
+    assert nb1.item() == nb2.item() == 1
+    assert (o1.float() - o2.float()).abs().max().item() <= 2 ** -6
+
+
+def test_resnet50_native_conv_matches_miopen(cuda):
+    """Whole ResNet-50 training step: MFMA convs (+ BN statistics from the conv epilogue) vs
+    MIOpen convs, both bf16, each measured against an fp32 run of the same step.  A randomly
+    initialised deep ResNet amplifies any rounding difference layer by layer (MIOpen bf16 vs
+    fp32 differ by tens of percent at layer4 at this size), so the criterion is relative: the
+    native step must be no further from fp32 than MIOpen's bf16 step is."""
+    import copy
+
+    from distributed_pytorch_training_amd.config import parse_args
+    from distributed_pytorch_training_amd.engine.trainer import Trainer
+    from distributed_pytorch_training_amd.models import build_model
+    from distributed_pytorch_training_amd.ops import conv as native_conv
+
+    torch.manual_seed(0)
+    base = build_model("resnet50", 100, cuda, image_size=64, channels_last=True)
+    common = ["--model", "resnet50", "--dataset", "synthetic", "--channels-last", "--num-classes", "100",
+              "--lr", "0.05"]
+    amp = ["--amp", "--amp-dtype", "bf16"]
+    runs = {
+        "nat": (Trainer(copy.deepcopy(base), parse_args(common + amp), 0, 1, cuda, log=lambda s: None), True),
+        "mio": (Trainer(copy.deepcopy(base), parse_args(common + amp + ["--no-native-conv"]), 0, 1, cuda,
+                        log=lambda s: None), False),
+        "f32": (Trainer(copy.deepcopy(base), parse_args(common + ["--no-native-conv"]), 0, 1, cuda,
+                        log=lambda s: None), False),
+    }
+    n_native = sum(1 for m in runs["nat"][0].module.modules() if getattr(m, "dpt_bn_stats", False))
+    assert n_native >= 52  # every conv but the 3-channel stem feeds a fused BN
+    g = torch.Generator(device=cuda).manual_seed(7)
+    x = torch.randn(32, 3, 64, 64, device=cuda, generator=g).contiguous(memory_format=CL)
+    y = torch.randint(0, 100, (32,), device=cuda, generator=g)
+    loss = {}
+    for k, (tr, enabled) in runs.items():
+        native_conv.ENABLED = enabled
+        loss[k] = tr.train_step(x, y)[1].item()
+    native_conv.ENABLED = True
+    assert abs(loss["nat"] - loss["f32"]) <= 2 * abs(loss["mio"] - loss["f32"]) + 2e-3, loss
+
+    def upd(k):
+        return torch.cat([(a.detach() - b.detach()).double().reshape(-1)
+                          for a, b in zip(runs[k][0].module.parameters(), base.parameters())])
+
+    u32 = upd("f32")
+    e_nat = ((upd("nat") - u32).norm() / u32.norm()).item()
+    e_mio = ((upd("mio") - u32).norm() / u32.norm()).item()
+    assert e_nat <= 1.5 * e_mio + 0.02, (e_nat, e_mio)
