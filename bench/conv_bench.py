@@ -29,7 +29,7 @@ def main(argv=None):
     dev = torch.device("cuda")
     cl = torch.channels_last
     print(f"# conv_kernels.hip vs MIOpen, ResNet-50 convs, batch {a.batch}, bf16 channels_last\n")
-    print("| conv | x | pass | MIOpen ms | ours ms | ours+stats ms | speedup | ours TF/s | ours TB/s | v1 / v2 / v3 / v4 ms |")
+    print("| conv | x | pass | MIOpen ms | ours ms | ours+stats ms | speedup | ours TF/s | ours TB/s | v4 / v5(bm256 reg) / v6(bm256 lds) ms |")
     print("|---|---|---|---|---|---|---|---|---|---|")
     tot = {"fwd": [0.0, 0.0], "dgrad": [0.0, 0.0], "wgrad": [0.0, 0.0]}
     for (cin_hw, cout, k, s, p), count in resnet50_convs(a.batch, a.image).items():
@@ -46,7 +46,7 @@ def main(argv=None):
         t_o = time_ms(lambda: C_.conv_fwd(x, wt, s[0], p[0], False))
         t_os = time_ms(lambda: C_.conv_fwd(x, wt, s[0], p[0], True))
         tv = []
-        for v in (1, 2, 3, 4):
+        for v in (4, 5, 6):
             C_.conv_set_variant(v)
             tv.append(time_ms(lambda: C_.conv_fwd(x, wt, s[0], p[0], False)))
         C_.conv_set_variant(0)
@@ -71,8 +71,9 @@ def main(argv=None):
             t_m = time_ms(lambda: torch.ops.aten.convolution_backward(
                 gy, x, wt, None, s, p, (1, 1), False, (0, 0), 1, (True, False, False)))
             t_o = time_ms(lambda: C_.conv_dgrad(gy, wt, p[0]))
+            t_of = time_ms(lambda: C_.conv_dgrad_flip(gy, wt, p[0]))
             print(f"| {name} | {count} | dgrad | {t_m:.3f} | {t_o:.3f} | - | {t_m / t_o:.2f} | "
-                  f"{flops / t_o / 1e9:.0f} | {byts / t_o / 1e9:.2f} |", flush=True)
+                  f"{flops / t_o / 1e9:.0f} | {byts / t_o / 1e9:.2f} | flip-copy {t_of:.3f} |", flush=True)
             tot["dgrad"][0] += t_m * count
             tot["dgrad"][1] += min(t_m, t_o) * count
     for k_, (m, o) in tot.items():

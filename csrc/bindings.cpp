@@ -247,9 +247,28 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bo
   return {y, ps, pq};
 }
 
-// dx = conv2d backward-data for a stride-1 conv: the forward kernel on dy with the flipped,
-// transposed weight (returned too, so a caller can reuse it).
-std::vector<Tensor> conv_dgrad(Tensor dy, Tensor w, int64_t pad) {
+// dx = conv2d backward-data for a stride-1 conv (flip/transpose folded into the kernel's
+// weight addressing).
+Tensor conv_dgrad(Tensor dy, Tensor w, int64_t pad) {
+  check_cl_bf16(dy, "grad_output");
+  check_cl_bf16(w, "w");
+  const int Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(dy.size(1) == Cout, "conv_dgrad: channel mismatch");
+  TORCH_CHECK(dpt::conv_supported(Cout, C), "conv_dgrad: needs C % 64 == 0 and Cout % 64 == 0");
+  TORCH_CHECK(R - 1 - pad >= 0 && S == R, "conv_dgrad: needs square kernel and pad <= R-1");
+  const int N = dy.size(0), Ho = dy.size(2), Wo = dy.size(3);
+  // stride 1: H = Ho + R - 1 - 2*pad
+  auto dx = at::empty({N, C, Ho + R - 1 - 2 * (int)pad, Wo + S - 1 - 2 * (int)pad},
+                      dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(dy.device().index());
+  dpt::launch_conv_dgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                         reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, (int)pad, cur_stream(dy));
+  return dx;
+}
+
+// Same through an explicitly flipped/transposed weight copy (returned too): the reference
+// path the tests compare the folded addressing against.
+std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
   const int Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
@@ -653,6 +672,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pad"), py::arg("fp32_out"));
   m.def("conv_set_variant", &dpt::conv_set_variant, py::arg("variant"));
   m.def("conv_dgrad", &conv_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
+  m.def("conv_dgrad_flip", &conv_dgrad_flip, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
 
   py::class_<dpt::RcclComm, std::shared_ptr<dpt::RcclComm>>(m, "RcclComm")

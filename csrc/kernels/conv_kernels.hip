@@ -62,8 +62,42 @@ struct ConvFwdArgs {
   float* psq;
   int N, H, W, C, Ho, Wo, Cout, R, S, stride, pad;
   int64_t M;
-  int m_tiles, n_tiles;
+  int m_tiles, n_tiles;  // m_tiles: 128-row tiles (the BN-partials layout)
+  int mt256;             // 256-row tiles when BM = 256
 };
+
+// ---- transposed-operand LDS images (K along rows) -------------------------------------------
+// An operand staged as [k][n] rows (channels contiguous, the way a channels_last tensor or a
+// KRSC weight sits in memory when the GEMM reduces over its row index) is read with the gfx950
+// transposing read ds_read_b64_tr_b16 (cdna_hip_programming.md T10): 8 consecutive k of one
+// column per lane.  Row chunks are XOR-swizzled (256-B rows: ch ^ ((row&3)<<2 | (row>>2)&3);
+// 128-B rows: ch ^ ((row>>1)&1)<<2 | (row>>2)&3) so the 4 rows x 32 columns one 32-lane half
+// reads hit 64 distinct banks.
+template <int RB>  // row bytes of the LDS image: 256 (128 channels) or 128 (64 channels)
+__device__ __forceinline__ int wg_slot(int row, int ch) {
+  if (RB == 256) return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
+  return ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
+}
+
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+
+// 4 consecutive rows (k) x this lane's column, two tr-reads -> one 8-element bf16 fragment
+template <int RB>
+__device__ __forceinline__ bf16x8_t wg_frag(const unsigned char* img, int krow0, int col0, int lane) {
+  // 16-lane group g reads rows krow0 + 8*(g>>1) + {0..3} (then +4) and columns col0 + 16*(g&1) + 0..15
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int colb = col0 + 16 * (g & 1) + 4 * pp;  // this lane's 4 columns
+  const int ch = colb >> 3, sub = (colb & 7) * 2;
+  const int r1 = krow0 + 8 * (g >> 1) + q, r2 = r1 + 4;
+  typedef __attribute__((address_space(3))) i16x4_t lds_v4;
+  const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(img + r1 * RB + wg_slot<RB>(r1, ch) * 16 + sub));
+  const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(img + r2 * RB + wg_slot<RB>(r2, ch) * 16 + sub));
+  typedef short i16x8_t __attribute__((ext_vector_type(8)));
+  i16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
 
 // 16 zero bytes: the global source of glds lanes whose A row falls in the zero padding.
 __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
@@ -72,9 +106,14 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 // half the LDS, twice the resident blocks - for K <= 2 steps, where there is nothing to
 // overlap inside a block).  LDSEPI: stage the output tile through LDS for 16-byte row
 // stores; otherwise each lane stores its accumulator column straight from registers.
-template <int BN, int STAGES, bool LDSEPI>
+// BKN: the B operand is the ORIGINAL weight w[co][r][s][ci] read as [k = co][n = ci] with the
+// taps flipped - the backward-data GEMM without materialising a transposed weight copy - staged
+// as K-major rows and taken with transposing LDS reads.
+// BMT: block rows (128, or 256 = 4 MFMA row tiles per wave for more reuse per LDS byte).
+template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN>
 __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
+  constexpr int BM = BMT;
   constexpr int WN = BN / 64;         // waves along N (each wave owns 64 output channels)
   constexpr int WM = 4 / WN;          // waves along M
   constexpr int MI = BM / (WM * 32);  // 32-row MFMA tiles per wave
@@ -92,7 +131,7 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int nwg = p.m_tiles * p.n_tiles;
+  const int nwg = (BM == 256 ? p.mt256 : p.m_tiles) * p.n_tiles;
   const int bid = conv::xcd_remap(blockIdx.x, nwg);
   const int mt = bid / p.n_tiles, nt = bid % p.n_tiles;
   const int64_t m0 = (int64_t)mt * BM;
@@ -125,11 +164,21 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
   }
   const int64_t Kg = (int64_t)p.R * p.S * p.C;
   const uint16_t* wrow[B_PER_T];
+  constexpr int RBK = BN * 2;              // BKN image row bytes (BK rows of BN channels)
+  constexpr int KN_RPI = 1024 / RBK;       // rows per glds instruction
 #pragma unroll
   for (int i = 0; i < B_PER_T; ++i) {
-    const int brow = (wid * B_PER_T + i) * 8 + (lane >> 3);
-    const int bchunk = (lane & 7) ^ ((brow >> 1) & 7);
-    wrow[i] = p.w + (int64_t)(n0 + brow) * Kg + bchunk * 8;
+    if (BKN) {
+      // row k of the [BK][BN] image = output channel co of the original weight (this lane
+      // fills chunk wg_slot(row, lane % chunks) of it)
+      const int krow = (wid * B_PER_T + i) * KN_RPI + lane / (RBK / 16);
+      const int kchunk = wg_slot<RBK>(krow, lane % (RBK / 16));
+      wrow[i] = p.w + (int64_t)krow * p.R * p.S * p.Cout + n0 + kchunk * 8;
+    } else {
+      const int brow = (wid * B_PER_T + i) * 8 + (lane >> 3);
+      const int bchunk = (lane & 7) ^ ((brow >> 1) & 7);
+      wrow[i] = p.w + (int64_t)(n0 + brow) * Kg + bchunk * 8;
+    }
   }
 
   const int cblocks = p.C / BK;
@@ -150,7 +199,9 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(a + (wid * A_PER_T + i) * 1024),
                                        16, 0, 0);
     }
-    const int64_t wk = (int64_t)rs * p.C + cb * BK;
+    // BKN: rows co = cb*BK + krow, flipped tap (R-1-r, S-1-s)
+    const int64_t wk = BKN ? ((int64_t)cb * BK * p.R * p.S + (p.R - 1 - r) * p.S + (p.S - 1 - s)) * p.Cout
+                           : (int64_t)rs * p.C + cb * BK;
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(wrow[i] + wk),
@@ -181,8 +232,12 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int row = wn * 64 + j * 32 + lr;
-        fb[j] = *reinterpret_cast<const bf16x8_t*>(b + row * kRowBytes + conv::swz(row, ch) * 16);
+        if (BKN) {
+          fb[j] = wg_frag<RBK>(b, kk * 16, wn * 64 + j * 32, lane);
+        } else {
+          const int row = wn * 64 + j * 32 + lr;
+          fb[j] = *reinterpret_cast<const bf16x8_t*>(b + row * kRowBytes + conv::swz(row, ch) * 16);
+        }
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -255,11 +310,20 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
   if (!LDSEPI && !stats) return;
   __syncthreads();
   if (stats && tid < BN) {
-    float s = 0.f, q = 0.f;
+    // partials are per 128-row sub-tile (the layout is independent of BM): waves whose rows
+    // fall in the same sub-tile are combined
+    constexpr int SUB = BM / 128, WPS = WM / SUB;  // sub-tiles per block, waves per sub-tile
 #pragma unroll
-    for (int w = 0; w < WM; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
-    p.psum[(int64_t)(n0 + tid) * p.m_tiles + mt] = s;
-    p.psq[(int64_t)(n0 + tid) * p.m_tiles + mt] = q;
+    for (int st = 0; st < SUB; ++st) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = st * WPS; w < (st + 1) * WPS; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
+      const int sub = mt * SUB + st;
+      if ((int64_t)sub * 128 < p.M) {
+        p.psum[(int64_t)(n0 + tid) * p.m_tiles + sub] = s;
+        p.psq[(int64_t)(n0 + tid) * p.m_tiles + sub] = q;
+      }
+    }
   }
   if (LDSEPI) {
     constexpr int CPR = BN / 8;          // 16-byte chunks per output row
@@ -306,32 +370,6 @@ struct ConvWgradArgs {
   FastDiv div_wo, div_howo;
   int direct;          // 1x1, stride 1, pad 0: x row = dy row
 };
-
-template <int RB>  // row bytes of the LDS image: 256 (128 channels) or 128 (64 channels)
-__device__ __forceinline__ int wg_slot(int row, int ch) {
-  if (RB == 256) return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
-  return ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
-}
-
-typedef short i16x4_t __attribute__((ext_vector_type(4)));
-
-// 4 consecutive rows (k) x this lane's column, two tr-reads -> one 8-element bf16 fragment
-template <int RB>
-__device__ __forceinline__ bf16x8_t wg_frag(const unsigned char* img, int krow0, int col0, int lane) {
-  // 16-lane group g reads rows krow0 + 8*(g>>1) + {0..3} (then +4) and columns col0 + 16*(g&1) + 0..15
-  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  const int colb = col0 + 16 * (g & 1) + 4 * pp;  // this lane's 4 columns
-  const int ch = colb >> 3, sub = (colb & 7) * 2;
-  const int r1 = krow0 + 8 * (g >> 1) + q, r2 = r1 + 4;
-  typedef __attribute__((address_space(3))) i16x4_t lds_v4;
-  const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_v4*)(img + r1 * RB + wg_slot<RB>(r1, ch) * 16 + sub));
-  const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_v4*)(img + r2 * RB + wg_slot<RB>(r2, ch) * 16 + sub));
-  typedef short i16x8_t __attribute__((ext_vector_type(8)));
-  i16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8_t, v);
-}
 
 template <int BMW, int BNW, int STAGES>
 __global__ __launch_bounds__(conv::kThreads, 2) void conv_wgrad_kernel(ConvWgradArgs p) {
@@ -534,7 +572,8 @@ bool conv_supported(int C, int Cout) { return C % 64 == 0 && Cout % 64 == 0; }
 
 int conv_m_tiles(int64_t M) { return (int)((M + conv::BM - 1) / conv::BM); }
 
-// Kernel variant: 0 = default (1-stage + LDS epilogue), 1 = 2-stage + LDS epilogue, 2 = 2-stage +
+// Kernel variant: 0 = default (1-stage + LDS epilogue), 5/6 = 256-row blocks (register / LDS
+// epilogue), 1 = 2-stage + LDS epilogue, 2 = 2-stage +
 // register epilogue, 3 = 1-stage + register epilogue, 4 = 1-stage + LDS epilogue.
 // The backward-weight kernel takes 1-2 -> 2 stages, 0/3-4 -> 1 stage.
 // DPT_CONV_VARIANT overrides; conv_set_variant switches at run time (A/B tests, benchmarks).
@@ -550,20 +589,32 @@ void conv_set_variant(int v) { g_conv_variant = v; }
 
 
 template <int BN>
-static void conv_fwd_dispatch(int variant, int nk, const ConvFwdArgs& a, dim3 grid, hipStream_t s) {
-  (void)nk;
+static void conv_fwd_dispatch(int variant, bool bkn, ConvFwdArgs a, hipStream_t s) {
   if (variant == 0) variant = 4;  // measured best at every ResNet-50 shape but two (profiles/conv_*.md)
   const dim3 block(conv::kThreads);
+  const int mt128 = a.m_tiles;
+  if (variant >= 5 && !bkn) {  // 256-row blocks (4 row tiles per wave)
+    a.mt256 = (mt128 + 1) / 2;  // m_tiles stays the 128-row count: the BN-partials layout
+    const dim3 grid((unsigned)(a.mt256 * a.n_tiles));
+    if (variant == 5) hipLaunchKernelGGL((conv_fwd_kernel<256, BN, 1, false, false>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_fwd_kernel<256, BN, 1, true, false>), grid, block, 0, s, a);
+    return;
+  }
+  const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
+  if (bkn) {
+    hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, true>), grid, block, 0, s, a);
+    return;
+  }
   switch (variant) {
-    case 2: hipLaunchKernelGGL((conv_fwd_kernel<BN, 2, false>), grid, block, 0, s, a); break;
-    case 3: hipLaunchKernelGGL((conv_fwd_kernel<BN, 1, false>), grid, block, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((conv_fwd_kernel<BN, 1, true>), grid, block, 0, s, a); break;
-    default: hipLaunchKernelGGL((conv_fwd_kernel<BN, 2, true>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 2, false, false>), grid, block, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, false, false>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, false>), grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 2, true, false>), grid, block, 0, s, a); break;
   }
 }
 
-void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
-                     int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s) {
+static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
+                          int R, int S, int stride, int pad, float* psum, float* psq, bool bkn, hipStream_t s) {
   ConvFwdArgs a;
   a.x = x; a.w = w; a.y = y; a.psum = psum; a.psq = psq;
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S; a.stride = stride; a.pad = pad;
@@ -573,10 +624,21 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, i
   a.m_tiles = conv_m_tiles(a.M);
   const bool wide = Cout % 128 == 0;
   a.n_tiles = Cout / (wide ? 128 : 64);
-  const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
-  const int nk = R * S * (C / conv::BK);
-  if (wide) conv_fwd_dispatch<128>(conv_variant(), nk, a, grid, s);
-  else conv_fwd_dispatch<64>(conv_variant(), nk, a, grid, s);
+  a.mt256 = 0;
+  if (wide) conv_fwd_dispatch<128>(conv_variant(), bkn, a, s);
+  else conv_fwd_dispatch<64>(conv_variant(), bkn, a, s);
+}
+
+void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
+                     int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s) {
+  conv_fwd_impl(x, w, y, N, H, W, C, Cout, R, S, stride, pad, psum, psq, false, s);
+}
+
+// Stride-1 backward-data: dx[N,H,W,C] = conv(dy, flip(w)^T, pad' = R-1-pad) with the flip and
+// transpose done by the B-operand addressing (no weight copy).
+void launch_conv_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout, int C,
+                       int R, int S, int pad, hipStream_t s) {
+  conv_fwd_impl(dy, w, dx, N, Ho, Wo, Cout, C, R, S, 1, R - 1 - pad, nullptr, nullptr, true, s);
 }
 
 static FastDiv make_fastdiv(uint32_t d) {

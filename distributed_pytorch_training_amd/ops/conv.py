@@ -5,8 +5,8 @@ forward   implicit-GEMM conv; with ``bn_stats`` its epilogue also emits the per-
           (sum, sum of squares) partials of the bf16 output, which the following fused
           BatchNorm consumes instead of re-reading the activation (ops/bn.py picks them up
           from the output tensor's ``_dpt_bn_partials`` attribute).
-backward  input gradient: the same kernel on dy with the flipped/transposed weight (stride 1)
-          or MIOpen's backward-data (strided convs); weight gradient: split-K MFMA kernel
+backward  input gradient: the same kernel on dy reading the weight as [co][ci] with flipped taps
+          through transposing LDS reads (stride 1) or MIOpen's backward-data (strided convs); weight gradient: split-K MFMA kernel
           with transposing LDS reads, bf16 (the shadow weight's dtype).
 
 Replaces the reference's cuDNN convolutions (reference
@@ -47,7 +47,7 @@ def _backward(ctx, dy):
     dx = dw = None
     if ctx.needs_input_grad[0]:
         if s == 1:
-            dx = native().conv_dgrad(dy, w, p)[0]
+            dx = native().conv_dgrad_flip(dy, w, p)[0]
         else:
             dx = torch.ops.aten.convolution_backward(dy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
                                                      (True, False, False))[0]

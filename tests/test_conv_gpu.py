@@ -30,7 +30,8 @@ def _operands(cuda, N, C, H, W, Cout, k, seed=0):
     return x, w.contiguous(memory_format=CL)
 
 
-@pytest.fixture(params=[1, 2, 3, 4], ids=["2stage-ldsepi", "2stage-regepi", "1stage-regepi", "1stage-ldsepi"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6], ids=["2stage-ldsepi", "2stage-regepi", "1stage-regepi", "1stage-ldsepi",
+                                               "bm256-regepi", "bm256-ldsepi"])
 def variant(request):
     ops.native().conv_set_variant(request.param)
     yield request.param
@@ -56,10 +57,13 @@ def test_conv_dgrad_matches_fp32(cuda, shape):
     x, w = _operands(cuda, N, C, H, W, Cout, k, seed=1)
     Ho, Wo = H + 2 * p - k + 1, W + 2 * p - k + 1
     gy = torch.randn(N, Cout, Ho, Wo, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
-    dx, wt = ops.native().conv_dgrad(gy, w, p)
+    dx = ops.native().conv_dgrad(gy, w, p)
     ref = torch.nn.grad.conv2d_input(x.shape, w.float(), gy.float(), stride=1, padding=p)
+    assert dx.shape == ref.shape and dx.is_contiguous(memory_format=CL)
     torch.testing.assert_close(dx.float(), ref, rtol=1e-2, atol=2e-2)
+    dx2, wt = ops.native().conv_dgrad_flip(gy, w, p)
     assert torch.equal(wt, w.flip(2, 3).transpose(0, 1).contiguous(memory_format=CL))
+    torch.testing.assert_close(dx2.float(), ref, rtol=1e-2, atol=2e-2)
 
 
 @pytest.mark.parametrize("shape", SHAPES)
