@@ -311,6 +311,21 @@ Tensor conv_wgrad(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stri
   return dw;
 }
 
+// a = im2col(x) as a channels_last [N, Kp, Ho, Wo] bf16 tensor (x: channels_last fp32/bf16)
+Tensor im2col(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Kp) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
+              "im2col: x must be a 4-d fp32/bf16 GPU tensor");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "im2col: x must be channels_last");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(Kp % 64 == 0 && Kp >= R * S * C, "im2col: Kp must be a multiple of 64 covering R*S*C");
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  auto a = at::empty({N, Kp, Ho, Wo}, x.options().dtype(at::kBFloat16).memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(x.device().index());
+  dpt::launch_im2col(x.data_ptr(), x.scalar_type() == at::kBFloat16, reinterpret_cast<uint16_t*>(a.data_ptr()), N, H,
+                     W, C, (int)R, (int)S, (int)stride, (int)pad, (int)Kp, cur_stream(x));
+  return a;
+}
+
 std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::optional<Tensor> weight,
                                  c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
                                  c10::optional<Tensor> running_var, c10::optional<Tensor> num_batches,
@@ -670,6 +685,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"));
   m.def("conv_wgrad", &conv_wgrad, py::arg("grad_output"), py::arg("x"), py::arg("weight_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("fp32_out"));
+  m.def("im2col", &im2col, py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("Kp"));
   m.def("conv_set_variant", &dpt::conv_set_variant, py::arg("variant"));
   m.def("conv_dgrad", &conv_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("conv_dgrad_flip", &conv_dgrad_flip, py::arg("grad_output"), py::arg("w"), py::arg("pad"));

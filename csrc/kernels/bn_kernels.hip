@@ -217,6 +217,55 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_finalize_kernel(
   }
 }
 
+// Same finalize for MANY partials per channel (the conv epilogue writes one per 128 rows: up
+// to ~6k at ResNet-50's 56x56 layers): one 256-thread block per channel, fp64 block reduce.
+__global__ __launch_bounds__(kBlock) void bn_fwd_finalize_wide_kernel(
+    const float* __restrict__ psum, const float* __restrict__ psq, int chunks, int C, int64_t M,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    float* run_mean, float* run_var, int64_t* num_batches, float* save_mean, float* save_invstd,
+    float* coef_a, float* coef_b) {
+  __shared__ double red[2][kBlock / 64];
+  const int c = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (c == 0 && threadIdx.x == 0 && num_batches) num_batches[0] += 1;
+  const float* q1 = psum + (int64_t)c * chunks;
+  const float* q2 = psq + (int64_t)c * chunks;
+  double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+  int k = threadIdx.x;
+  for (; k + kBlock < chunks; k += 2 * kBlock) {
+    const float x0 = q1[k], x1 = q1[k + kBlock], y0 = q2[k], y1 = q2[k + kBlock];
+    a0 += (double)x0; a1 += (double)x1; b0 += (double)y0; b1 += (double)y1;
+  }
+  if (k < chunks) { a0 += (double)q1[k]; b0 += (double)q2[k]; }
+  double s = a0 + a1, q = b0 + b1;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off, 64);
+    q += __shfl_xor(q, off, 64);
+  }
+  if (lane == 0) { red[0][wave] = s; red[1][wave] = q; }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  s = 0.0;
+  q = 0.0;
+#pragma unroll
+  for (int w = 0; w < kBlock / 64; ++w) { s += red[0][w]; q += red[1][w]; }
+  const double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.0f, bt = beta ? beta[c] : 0.0f;
+  const float a = g * invstd;
+  save_mean[c] = (float)mean;
+  save_invstd[c] = invstd;
+  coef_a[c] = a;
+  coef_b[c] = bt - (float)mean * a;
+  if (run_mean) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    run_mean[c] = (1.0f - momentum) * run_mean[c] + momentum * (float)mean;
+    run_var[c] = (1.0f - momentum) * run_var[c] + momentum * (float)unbiased;
+  }
+}
+
 // ---- forward apply: y = relu(x*a + b [+ r]) --------------------------------------------------
 template <typename IO, bool RELU, bool RES>
 __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(const void* __restrict__ x,
@@ -514,9 +563,13 @@ void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void
   BnGeometry g = bn_geometry(M, C);
   float* ca = save_coef;
   float* cb = ca + C;
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), dim3(kBlock), 0, s, psum, psq, chunks,
-                     (int)C, M, gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd,
-                     ca, cb);
+  if (chunks > 256)
+    hipLaunchKernelGGL(bn_fwd_finalize_wide_kernel, dim3((unsigned)C), dim3(kBlock), 0, s, psum, psq, chunks, (int)C,
+                       M, gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd, ca, cb);
+  else
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), dim3(kBlock), 0, s, psum, psq, chunks,
+                       (int)C, M, gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd,
+                       ca, cb);
   switch (dtype) {
     case 0: fwd_apply_dispatch<F32>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
     case 1: fwd_apply_dispatch<BF16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;

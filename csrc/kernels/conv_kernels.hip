@@ -551,6 +551,63 @@ __global__ __launch_bounds__(kBlock) void conv_wgrad_reduce_kernel(const float4*
   }
 }
 
+// ---- narrow-input convs (the 3-channel stem): explicit im2col -> the 1x1 MFMA GEMM ---------------
+// a[m, k] (bf16, k padded to Kp, a multiple of 64) = x[pix(m) + tap(k)] for k < R*S*C, else 0;
+// k = (r*S + s)*C + c matches the KRSC weight flattened to [Cout, R*S*C].  x is fp32 or bf16
+// channels_last (the loader's dtype: the autocast cast of the input disappears with it).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void im2col_kernel(const T* __restrict__ x, uint16_t* __restrict__ a,
+                                                         int64_t M, int H, int W, int C, int Ho, int Wo, int R,
+                                                         int S, int stride, int pad, int Kp) {
+  const int cpr = Kp / 8;
+  const int64_t n_items = M * cpr;
+  const int K = R * S * C;
+  for (int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x; it < n_items; it += (int64_t)gridDim.x * kBlock) {
+    const int64_t m = it / cpr;
+    const int ch = (int)(it - m * cpr);
+    const int64_t n = m / ((int64_t)Ho * Wo);
+    const int rem = (int)(m - n * Ho * Wo);
+    const int ho = rem / Wo, wo = rem - ho * Wo;
+    uint32_t packed[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      uint16_t v[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k = ch * 8 + j + u;
+        float f = 0.f;
+        if (k < K) {
+          const int tap = k / C, c = k - tap * C;
+          const int r = tap / S, s = tap - r * S;
+          const int hi = ho * stride - pad + r, wi = wo * stride - pad + s;
+          if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W) {
+            const T raw = x[((n * H + hi) * (int64_t)W + wi) * C + c];
+            if constexpr (sizeof(T) == 4) f = (float)raw;
+            else f = bf16_to_f32((uint16_t)raw);
+          }
+        }
+        v[u] = f32_to_bf16(f);
+      }
+      packed[j / 2] = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
+    }
+    *reinterpret_cast<uint4*>(a + m * Kp + ch * 8) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+  }
+}
+
+void launch_im2col(const void* x, bool x_bf16, uint16_t* a, int N, int H, int W, int C, int R, int S, int stride,
+                   int pad, int Kp, hipStream_t st) {
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  const int64_t M = (int64_t)N * Ho * Wo;
+  const int64_t items = M * (Kp / 8);
+  const dim3 grid((unsigned)grid_for(items, 4));
+  if (x_bf16)
+    hipLaunchKernelGGL(im2col_kernel<uint16_t>, grid, dim3(kBlock), 0, st, static_cast<const uint16_t*>(x), a, M, H,
+                       W, C, Ho, Wo, R, S, stride, pad, Kp);
+  else
+    hipLaunchKernelGGL(im2col_kernel<float>, grid, dim3(kBlock), 0, st, static_cast<const float*>(x), a, M, H, W, C,
+                       Ho, Wo, R, S, stride, pad, Kp);
+}
+
 // wt[ci, r', s', co] = w[co, R-1-r', S-1-s', ci]: the backward-data operand of a stride-1 conv.
 __global__ __launch_bounds__(kBlock) void conv_wt_flip_kernel(const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ wt, int Cout, int R,

@@ -131,6 +131,9 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
 // stride-1 backward-data straight from the KRSC weight w [Cout,R,S,C]: dy [N,Ho,Wo,Cout] -> dx [N,Ho,Wo,C]
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout, int C,
                        int R, int S, int pad, hipStream_t s);
+// im2col for narrow-input convs: a [N*Ho*Wo, Kp] bf16 (k = (r*S+s)*C + c, zero past R*S*C)
+void launch_im2col(const void* x, bool x_bf16, uint16_t* a, int N, int H, int W, int C, int R, int S, int stride,
+                   int pad, int Kp, hipStream_t s);
 // wt[ci, r, s, co] = w[co, R-1-r, S-1-s, ci]
 void launch_conv_wt_flip(const uint16_t* w, uint16_t* wt, int Cout, int R, int S, int C, hipStream_t s);
 

@@ -23,6 +23,9 @@ from . import native, native_available
 
 _CL = torch.channels_last
 ENABLED = os.environ.get("DPT_NATIVE_CONV", "1") != "0"
+# The im2col stem path is correct but measured slower than MIOpen on ResNet-50's 7x7/2 stem at
+# batch 256 (the [3.2M x 192] bf16 patch matrix is 1.2 GB written and read twice): opt-in only.
+STEM_ENABLED = os.environ.get("DPT_NATIVE_STEM", "0") == "1"
 
 
 def supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups) -> bool:
@@ -99,3 +102,27 @@ def take_bn_partials(x: torch.Tensor):
     """The (psum, psq) partials a native conv attached to ``x``, once (None otherwise)."""
     part = x.__dict__.pop("_dpt_bn_partials", None)
     return part
+
+
+def stem_supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups) -> bool:
+    """Narrow-input conv (ResNet's 3-channel 7x7 stem) on the im2col + MFMA GEMM path."""
+    if not (ENABLED and x.is_cuda and native_available() and x.dim() == 4 and groups == 1
+            and x.dtype in (torch.float32, torch.bfloat16) and w.dtype == torch.bfloat16):
+        return False
+    cout, cin, r, s = w.shape
+    return (cin < 64 and cout % 64 == 0 and not x.requires_grad and tuple(dilation) == (1, 1)
+            and stride[0] == stride[1] and padding[0] == padding[1] and x.shape[1] == cin
+            and x.is_contiguous(memory_format=_CL))
+
+
+def stem_conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bool = False) -> torch.Tensor:
+    """conv2d for a narrow input that needs no input gradient: one im2col kernel writes the
+    [pixels, Kp] bf16 patch matrix (Kp = R*S*Cin rounded up to 64, zero-padded), then the 1x1
+    MFMA conv (GEMM) with the weight flattened to [Cout, R*S*Cin] (KRSC order) and zero-padded
+    - its backward-weight is the 1x1 split-K kernel on the saved patch matrix."""
+    cout, cin, r, s = w.shape
+    k = r * s * cin
+    kp = (k + 63) // 64 * 64
+    a = native().im2col(x, r, s, int(stride), int(pad), kp)
+    wf = torch.nn.functional.pad(w.permute(0, 2, 3, 1).reshape(cout, k), (0, kp - k))
+    return conv2d(a, wf.view(cout, kp, 1, 1), 1, 0, bn_stats)

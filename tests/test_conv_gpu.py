@@ -93,9 +93,10 @@ def test_conv_wgrad_large_split(cuda):
     torch.testing.assert_close(dw, ref, rtol=1e-3, atol=1e-2)
 
 
-def test_bn_from_conv_partials_matches_stats_pass(cuda):
+@pytest.mark.parametrize("n,hw", [(4, 14), (64, 28)])  # 7 and 392 partials per channel
+def test_bn_from_conv_partials_matches_stats_pass(cuda, n, hw):
     """Fused BN fed by the conv epilogue's partial sums == fused BN with its own stats pass."""
-    x, w = _operands(cuda, 4, 128, 14, 14, 256, 3, seed=4)
+    x, w = _operands(cuda, n, 128, hw, hw, 256, 3, seed=4)
     C_ = ops.native()
     y, ps, pq = C_.conv_fwd(x, w, 1, 1, True)
     g = torch.rand(256, device=cuda) + 0.5
@@ -159,3 +160,24 @@ def test_resnet50_native_conv_matches_miopen(cuda):
     e_nat = ((upd("nat") - u32).norm() / u32.norm()).item()
     e_mio = ((upd("mio") - u32).norm() / u32.norm()).item()
     assert e_nat <= 1.5 * e_mio + 0.02, (e_nat, e_mio)
+
+
+@pytest.mark.parametrize("xdtype", [torch.float32, torch.bfloat16])
+def test_stem_im2col_conv_matches_fp32(cuda, xdtype):
+    """3-channel 7x7/2 stem: im2col + 1x1 MFMA GEMM forward, and its weight gradient."""
+    from distributed_pytorch_training_amd.ops import conv as native_conv
+
+    g = torch.Generator(device=cuda).manual_seed(9)
+    x = torch.randn(2, 3, 40, 36, device=cuda, generator=g).to(xdtype).contiguous(memory_format=CL)
+    w = (torch.randn(64, 3, 7, 7, device=cuda, generator=g) * 0.05).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL).requires_grad_(True)
+    assert native_conv.stem_supported(x, w, (2, 2), (3, 3), (1, 1), 1)
+    y = native_conv.stem_conv2d(x, w, 2, 3, bn_stats=True)
+    ref = F.conv2d(x.float().to(torch.bfloat16).float(), w.detach().float(), stride=2, padding=3)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+    ps, pq = y._dpt_bn_partials
+    torch.testing.assert_close(ps.sum(1), y.float().sum((0, 2, 3)), rtol=1e-4, atol=1e-3)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    wref = torch.nn.grad.conv2d_weight(x.float().to(torch.bfloat16).float(), w.shape, gy.float(), stride=2, padding=3)
+    torch.testing.assert_close(w.grad.float(), wref, rtol=2e-2, atol=2e-2 * wref.abs().max().item())
