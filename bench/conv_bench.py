@@ -29,7 +29,7 @@ def main(argv=None):
     dev = torch.device("cuda")
     cl = torch.channels_last
     print(f"# conv_kernels.hip vs MIOpen, ResNet-50 convs, batch {a.batch}, bf16 channels_last\n")
-    print("| conv | x | pass | MIOpen ms | ours ms | ours+stats ms | speedup | ours TF/s | ours TB/s | v4 / v5(bm256 reg) / v6(bm256 lds) ms |")
+    print("| conv | x | pass | MIOpen ms | ours ms | ours+stats ms | speedup | ours TF/s | ours TB/s | v4 / v7(pipe3) / v8(pipe4) ms |")
     print("|---|---|---|---|---|---|---|---|---|---|")
     tot = {"fwd": [0.0, 0.0], "dgrad": [0.0, 0.0], "wgrad": [0.0, 0.0]}
     for (cin_hw, cout, k, s, p), count in resnet50_convs(a.batch, a.image).items():
@@ -46,7 +46,7 @@ def main(argv=None):
         t_o = time_ms(lambda: C_.conv_fwd(x, wt, s[0], p[0], False))
         t_os = time_ms(lambda: C_.conv_fwd(x, wt, s[0], p[0], True))
         tv = []
-        for v in (4, 5, 6):
+        for v in (4, 7, 8):
             C_.conv_set_variant(v)
             tv.append(time_ms(lambda: C_.conv_fwd(x, wt, s[0], p[0], False)))
         C_.conv_set_variant(0)

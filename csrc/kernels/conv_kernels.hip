@@ -35,6 +35,8 @@ namespace dpt {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 namespace conv {
 
@@ -110,7 +112,8 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 // taps flipped - the backward-data GEMM without materialising a transposed weight copy - staged
 // as K-major rows and taken with transposing LDS reads.
 // BMT: block rows (128, or 256 = 4 MFMA row tiles per wave for more reuse per LDS byte).
-template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN>
+// STATS: emit the BN partial sums (compiled out otherwise).
+template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true>
 __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
   constexpr int BM = BMT;
@@ -269,8 +272,9 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
   }
 
   // ---- epilogue: bf16 rounding, BN partial sums, stores ----
-  // accumulator map (32x32x16): column = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5)
-  const bool stats = p.psum != nullptr;
+  // accumulator map (32x32x16): column = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5); pairs of
+  // rows are rounded together by v_cvt_pk_bf16_f32
+  const bool stats = STATS && p.psum != nullptr;
   float cs[NI], cq[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) { cs[j] = 0.f; cq[j] = 0.f; }
@@ -279,19 +283,26 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int col = wn * 64 + j * 32 + lr;
+      const int rbase = wm * (MI * 32) + i * 32 + 4 * lh;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = wm * (MI * 32) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-        const uint16_t h = f32_to_bf16(acc[i][j][e]);
+      for (int e = 0; e < 16; e += 2) {
+        const int r0 = rbase + (e & 3) + 8 * (e >> 2);
+        const f32x2_t v = {acc[i][j][e], acc[i][j][e + 1]};
+        const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+        const uint16_t h0 = (uint16_t)u, h1 = (uint16_t)(u >> 16);
         if (LDSEPI) {
-          *reinterpret_cast<uint16_t*>(lds + row * C_STRIDE + col * 2) = h;
-        } else if (m0 + row < p.M) {
-          p.y[(m0 + row) * p.Cout + n0 + col] = h;
+          *reinterpret_cast<uint16_t*>(lds + r0 * C_STRIDE + col * 2) = h0;
+          *reinterpret_cast<uint16_t*>(lds + (r0 + 1) * C_STRIDE + col * 2) = h1;
+        } else {
+          if (m0 + r0 < p.M) p.y[(m0 + r0) * p.Cout + n0 + col] = h0;
+          if (m0 + r0 + 1 < p.M) p.y[(m0 + r0 + 1) * p.Cout + n0 + col] = h1;
         }
-        const float v = bf16_to_f32(h);
-        // rows past M hold exact zeros (their A rows were zero-filled): no effect on the sums
-        cs[j] += v;
-        cq[j] += v * v;
+        if (STATS) {
+          // rows past M hold exact zeros (their A rows were zero-filled): no effect on the sums
+          const float f0 = __uint_as_float(u << 16), f1 = __uint_as_float(u & 0xffff0000u);
+          cs[j] += f0 + f1;
+          cq[j] = __builtin_fmaf(f0, f0, __builtin_fmaf(f1, f1, cq[j]));
+        }
       }
     }
   float* red = reinterpret_cast<float*>(lds + (LDSEPI ? BM * C_STRIDE : 0));  // [2][WM][BN]
@@ -337,6 +348,211 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
         const uint4 v = *reinterpret_cast<const uint4*>(lds + row * C_STRIDE + oc * 16);
         *reinterpret_cast<uint4*>(p.y + m * p.Cout + n0 + oc * 8) = v;
       }
+    }
+  }
+}
+
+// ---- forward, software-pipelined: BK = 32 stages, NS-deep LDS ring, counted vmcnt -------------
+//
+// PMC on the 1-stage kernel (3x3 256->256 @14x14, batch 256) showed 30% MFMA busy with 36% of
+// wave cycles parked in s_waitcnt/barrier: each block waits a full HBM round trip per K-step.
+// Here a block keeps NS-1 K-tiles in flight: tile t+NS-1 is issued (global_load_lds) right
+// after the barrier that retires tile t, the barrier is a raw s_barrier (no vmcnt(0) fence),
+// and the wait before it is counted - vmcnt(G * tiles still allowed in flight), G = glds
+// instructions per wave per tile (cdna_hip_programming.md "Pipelining across barriers").
+// LDS rows are 64 B (32 bf16); 16-byte chunks are XOR-swizzled by (row>>2)&3 so the 16 rows a
+// ds_read_b128 quarter-wave touches (4 per 256-B bank row) land on distinct banks.
+// Epilogue: pairs of accumulators are rounded with v_cvt_pk_bf16_f32 and written to a padded
+// LDS image, then stored as 16-byte rows; BN statistics (STATS) from the rounded values.
+template <int N>
+__device__ __forceinline__ void vmcnt_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BN, int NS, bool STATS>
+__global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_pipe_kernel(ConvFwdArgs p) {
+  using namespace conv;
+  constexpr int BM = 128, BKP = 32, RB = BKP * 2;  // 64-byte LDS rows
+  constexpr int WN = BN / 64, WM = 4 / WN, MI = BM / (WM * 32), NI = 2;
+  constexpr int A_G = BM * RB / 1024 / 4, B_G = BN * RB / 1024 / 4;  // glds per wave per stage
+  constexpr int G = A_G + B_G;
+  constexpr int A_BYTES = BM * RB, STAGE = (BM + BN) * RB;
+  constexpr int C_STRIDE = BN * 2 + 16;
+  constexpr int RED = 2 * WM * BN * 4;
+  constexpr int LDS_MAIN = NS * STAGE, LDS_EPI = BM * C_STRIDE + RED;
+  constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+  static_assert(NS >= 2 && NS <= 4, "pipeline depth 2..4");
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int bid = conv::xcd_remap(blockIdx.x, p.m_tiles * p.n_tiles);
+  const int mt = bid / p.n_tiles, nt = bid % p.n_tiles;
+  const int64_t m0 = (int64_t)mt * BM;
+  const int n0 = nt * BN;
+
+  // glds lane-linear fill: one wave instruction = 16 rows of 64 B; lane L -> row base + L/4,
+  // slot L&3, loading the chunk the swizzle puts in that slot.
+  int hi0[A_G], wi0[A_G];
+  int64_t abase[A_G];
+  const int64_t HoWo = (int64_t)p.Ho * p.Wo;
+#pragma unroll
+  for (int i = 0; i < A_G; ++i) {
+    const int row = (wid * A_G + i) * 16 + (lane >> 2);
+    const int chunk = (lane & 3) ^ ((row >> 2) & 3);
+    const int64_t m = m0 + row;
+    if (m < p.M) {
+      const int64_t n = m / HoWo;
+      const int rem = (int)(m - n * HoWo);
+      const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+      hi0[i] = ho * p.stride - p.pad;
+      wi0[i] = wo * p.stride - p.pad;
+      abase[i] = ((n * p.H + hi0[i]) * (int64_t)p.W + wi0[i]) * p.C + chunk * 8;
+    } else {
+      hi0[i] = -(1 << 28);
+      wi0[i] = 0;
+      abase[i] = 0;
+    }
+  }
+  const int64_t Kg = (int64_t)p.R * p.S * p.C;
+  const uint16_t* wrow[B_G];
+#pragma unroll
+  for (int i = 0; i < B_G; ++i) {
+    const int row = (wid * B_G + i) * 16 + (lane >> 2);
+    const int chunk = (lane & 3) ^ ((row >> 2) & 3);
+    wrow[i] = p.w + (int64_t)(n0 + row) * Kg + chunk * 8;
+  }
+  const int cblocks = p.C / BKP;
+  const int nk = p.R * p.S * cblocks;
+
+  auto stage = [&](int ks, int buf) {
+    const int rs = ks / cblocks, cb = ks - rs * cblocks;
+    const int r = rs / p.S, s = rs - r * p.S;
+    const int64_t koff = ((int64_t)r * p.W + s) * p.C + cb * BKP;
+    unsigned char* a = lds + buf * STAGE;
+    unsigned char* b = a + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_G; ++i) {
+      const int hi = hi0[i] + r, wi = wi0[i] + s;
+      const bool ok = (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
+      const void* src = ok ? (const void*)(p.x + abase[i] + koff) : (const void*)g_conv_zero16;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(a + (wid * A_G + i) * 1024),
+                                       16, 0, 0);
+    }
+    const int64_t wk = (int64_t)rs * p.C + cb * BKP;
+#pragma unroll
+    for (int i = 0; i < B_G; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(wrow[i] + wk),
+                                       (__attribute__((address_space(3))) void*)(b + (wid * B_G + i) * 1024),
+                                       16, 0, 0);
+  };
+
+  f32x16_t acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  const int lr = lane & 31, lh = lane >> 5;
+  // fragment byte offsets inside a stage (loop-invariant)
+  int aoff[2][MI], boff[2][NI];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int ch = kk * 2 + lh;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * (MI * 32) + i * 32 + lr;
+      aoff[kk][i] = row * RB + ((ch ^ ((row >> 2) & 3)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int row = wn * 64 + j * 32 + lr;
+      boff[kk][j] = A_BYTES + row * RB + ((ch ^ ((row >> 2) & 3)) << 4);
+    }
+  }
+
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) stage(t, t);
+  for (int ks = 0; ks < nk; ++ks) {
+    const int ahead = min(NS - 2, nk - 1 - ks);  // tiles allowed to stay in flight
+    if (ahead >= 2) vmcnt_wait<2 * G>();
+    else if (ahead == 1) vmcnt_wait<G>();
+    else vmcnt_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (ks + NS - 1 < nk) stage(ks + NS - 1, (ks + NS - 1) % NS);
+    const unsigned char* base = lds + (ks % NS) * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t fa[MI], fb[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8_t*>(base + aoff[kk][i]);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const bf16x8_t*>(base + boff[kk][j]);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue ----
+  float cs[NI], cq[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) { cs[j] = 0.f; cq[j] = 0.f; }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      unsigned char* colp = lds + (wn * 64 + j * 32 + lr) * 2 + (wm * (MI * 32) + i * 32 + 4 * lh) * C_STRIDE;
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        const f32x2_t v = {acc[i][j][e], acc[i][j][e + 1]};
+        const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+        const int r0 = (e & 3) + 8 * (e >> 2);  // rows r0, r0+1 of this lane's column
+        *reinterpret_cast<uint16_t*>(colp + r0 * C_STRIDE) = (uint16_t)u;
+        *reinterpret_cast<uint16_t*>(colp + (r0 + 1) * C_STRIDE) = (uint16_t)(u >> 16);
+        if (STATS) {
+          const float f0 = __uint_as_float(u << 16), f1 = __uint_as_float(u & 0xffff0000u);
+          cs[j] += f0 + f1;
+          cq[j] = __builtin_fmaf(f0, f0, __builtin_fmaf(f1, f1, cq[j]));
+        }
+      }
+    }
+  float* red = reinterpret_cast<float*>(lds + BM * C_STRIDE);  // [2][WM][BN]
+  if (STATS) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+      cq[j] += __shfl_xor(cq[j], 32, 64);
+      if (lh == 0) {
+        const int col = wn * 64 + j * 32 + lr;
+        red[wm * BN + col] = cs[j];
+        red[WM * BN + wm * BN + col] = cq[j];
+      }
+    }
+  }
+  __syncthreads();
+  if (STATS && tid < BN) {
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
+    p.psum[(int64_t)(n0 + tid) * p.m_tiles + mt] = s;
+    p.psq[(int64_t)(n0 + tid) * p.m_tiles + mt] = q;
+  }
+  constexpr int CPR = BN / 8, RPP = kThreads / CPR;
+  const int oc = tid % CPR, orow = tid / CPR;
+#pragma unroll
+  for (int r0 = 0; r0 < BM; r0 += RPP) {
+    const int row = r0 + orow;
+    const int64_t m = m0 + row;
+    if (m < p.M) {
+      const uint4 v = *reinterpret_cast<const uint4*>(lds + row * C_STRIDE + oc * 16);
+      *reinterpret_cast<uint4*>(p.y + m * p.Cout + n0 + oc * 8) = v;
     }
   }
 }
@@ -658,6 +874,19 @@ static void conv_fwd_dispatch(int variant, bool bkn, ConvFwdArgs a, hipStream_t 
     return;
   }
   const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
+  const int nk32 = a.R * a.S * (a.C / 32);
+  if (!bkn && (variant == 7 || variant == 8)) {
+    const bool st = a.psum != nullptr;
+    if (variant == 7) {
+      if (st) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN, 3, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN, 3, false>), grid, block, 0, s, a);
+    } else {
+      if (st) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN, 4, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN, 4, false>), grid, block, 0, s, a);
+    }
+    return;
+  }
+  (void)nk32;
   if (bkn) {
     hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, true>), grid, block, 0, s, a);
     return;
@@ -665,7 +894,10 @@ static void conv_fwd_dispatch(int variant, bool bkn, ConvFwdArgs a, hipStream_t 
   switch (variant) {
     case 2: hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 2, false, false>), grid, block, 0, s, a); break;
     case 3: hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, false, false>), grid, block, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, false>), grid, block, 0, s, a); break;
+    case 4:
+      if (a.psum) hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, false, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, false, false>), grid, block, 0, s, a);
+      break;
     default: hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 2, true, false>), grid, block, 0, s, a); break;
   }
 }
