@@ -326,6 +326,44 @@ Tensor im2col(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64
   return a;
 }
 
+// ---- fused self-attention (ViT) ---------------------------------------------------------------
+void check_bf16_contig(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous(), name,
+              " must be a contiguous bf16 GPU tensor");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+// qkv [B, S, 3*H*64] -> {ctx [B, S, H*64], lse2 [B*H, stride]}
+std::vector<Tensor> attn_fwd(Tensor qkv, int64_t heads, double scale) {
+  check_bf16_contig(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) == 3 * heads * 64, "attn_fwd: qkv must be [B, S, 3*H*64]");
+  const int B = qkv.size(0), S = qkv.size(1), H = heads;
+  TORCH_CHECK(dpt::attn_supported(S, 64), "attn_fwd: needs S <= 256 and head dim 64");
+  auto ctx = at::empty({B, S, H * 64}, qkv.options());
+  auto lse = at::empty({(int64_t)B * H, dpt::attn_lse_stride(S)}, qkv.options().dtype(at::kFloat));
+  c10::hip::HIPGuard guard(qkv.device().index());
+  dpt::launch_attn_fwd(reinterpret_cast<const uint16_t*>(qkv.data_ptr()), reinterpret_cast<uint16_t*>(ctx.data_ptr()),
+                       lse.data_ptr<float>(), B, S, H, (float)scale, cur_stream(qkv));
+  return {ctx, lse};
+}
+
+Tensor attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, int64_t heads, double scale) {
+  check_bf16_contig(qkv, "qkv");
+  check_bf16_contig(out, "out");
+  check_bf16_contig(dout, "grad_output");
+  const int B = qkv.size(0), S = qkv.size(1), H = heads;
+  TORCH_CHECK(out.sizes() == dout.sizes() && out.dim() == 3 && out.size(0) == B && out.size(1) == S &&
+                  out.size(2) == H * 64 && qkv.size(2) == 3 * H * 64, "attn_bwd: shape mismatch");
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == at::kFloat && lse.is_contiguous() &&
+                  lse.numel() == (int64_t)B * H * dpt::attn_lse_stride(S), "attn_bwd: bad lse");
+  auto dqkv = at::empty_like(qkv);
+  c10::hip::HIPGuard guard(qkv.device().index());
+  dpt::launch_attn_bwd(reinterpret_cast<const uint16_t*>(qkv.data_ptr()), reinterpret_cast<const uint16_t*>(out.data_ptr()),
+                       reinterpret_cast<const uint16_t*>(dout.data_ptr()), lse.data_ptr<float>(),
+                       reinterpret_cast<uint16_t*>(dqkv.data_ptr()), B, S, H, (float)scale, cur_stream(qkv));
+  return dqkv;
+}
+
 std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::optional<Tensor> weight,
                                  c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
                                  c10::optional<Tensor> running_var, c10::optional<Tensor> num_batches,
@@ -686,6 +724,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad, py::arg("grad_output"), py::arg("x"), py::arg("weight_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("fp32_out"));
   m.def("im2col", &im2col, py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("Kp"));
+  m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("heads"), py::arg("scale"));
+  m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("grad_output"), py::arg("lse"),
+        py::arg("heads"), py::arg("scale"));
   m.def("conv_set_variant", &dpt::conv_set_variant, py::arg("variant"));
   m.def("conv_dgrad", &conv_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("conv_dgrad_flip", &conv_dgrad_flip, py::arg("grad_output"), py::arg("w"), py::arg("pad"));

@@ -30,13 +30,10 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "mfma.h"
 
 namespace dpt {
 
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x16_t __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 namespace conv {
 
@@ -68,37 +65,11 @@ struct ConvFwdArgs {
   int mt256;             // 256-row tiles when BM = 256
 };
 
-// ---- transposed-operand LDS images (K along rows) -------------------------------------------
-// An operand staged as [k][n] rows (channels contiguous, the way a channels_last tensor or a
-// KRSC weight sits in memory when the GEMM reduces over its row index) is read with the gfx950
-// transposing read ds_read_b64_tr_b16 (cdna_hip_programming.md T10): 8 consecutive k of one
-// column per lane.  Row chunks are XOR-swizzled (256-B rows: ch ^ ((row&3)<<2 | (row>>2)&3);
-// 128-B rows: ch ^ ((row>>1)&1)<<2 | (row>>2)&3) so the 4 rows x 32 columns one 32-lane half
-// reads hit 64 distinct banks.
-template <int RB>  // row bytes of the LDS image: 256 (128 channels) or 128 (64 channels)
-__device__ __forceinline__ int wg_slot(int row, int ch) {
-  if (RB == 256) return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
-  return ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
-}
-
-typedef short i16x4_t __attribute__((ext_vector_type(4)));
-
-// 4 consecutive rows (k) x this lane's column, two tr-reads -> one 8-element bf16 fragment
+// K-major operands (rows of the LDS image = k) use the transposing reads and the swizzle of
+// mfma.h: wg_frag is its natural-k-order tr_frag.
 template <int RB>
 __device__ __forceinline__ bf16x8_t wg_frag(const unsigned char* img, int krow0, int col0, int lane) {
-  // 16-lane group g reads rows krow0 + 8*(g>>1) + {0..3} (then +4) and columns col0 + 16*(g&1) + 0..15
-  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  const int colb = col0 + 16 * (g & 1) + 4 * pp;  // this lane's 4 columns
-  const int ch = colb >> 3, sub = (colb & 7) * 2;
-  const int r1 = krow0 + 8 * (g >> 1) + q, r2 = r1 + 4;
-  typedef __attribute__((address_space(3))) i16x4_t lds_v4;
-  const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_v4*)(img + r1 * RB + wg_slot<RB>(r1, ch) * 16 + sub));
-  const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_v4*)(img + r2 * RB + wg_slot<RB>(r2, ch) * 16 + sub));
-  typedef short i16x8_t __attribute__((ext_vector_type(8)));
-  i16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8_t, v);
+  return tr_frag<RB, false>(img, krow0, col0, lane);
 }
 
 // 16 zero bytes: the global source of glds lanes whose A row falls in the zero padding.

@@ -137,4 +137,13 @@ void launch_im2col(const void* x, bool x_bf16, uint16_t* a, int N, int H, int W,
 // wt[ci, r, s, co] = w[co, R-1-r, S-1-s, ci]
 void launch_conv_wt_flip(const uint16_t* w, uint16_t* wt, int Cout, int R, int S, int C, hipStream_t s);
 
+// attn_kernels.hip: fused self-attention for short sequences (S <= 256, head dim 64).
+// qkv [B, S, 3, H, 64] bf16 (the QKV projection output), ctx/out/dout [B, S, H*64] bf16,
+// lse2 [B*H][attn_lse_stride(S)] fp32 (log2-sum-exp of the scaled scores), dqkv like qkv.
+bool attn_supported(int S, int Dh);
+int attn_lse_stride(int S);
+void launch_attn_fwd(const uint16_t* qkv, uint16_t* ctx, float* lse2, int B, int S, int H, float scale,
+                     hipStream_t s);
+void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse2,
+                     uint16_t* dqkv, int B, int S, int H, float scale, hipStream_t s);
 }  // namespace dpt

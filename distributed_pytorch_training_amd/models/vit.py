@@ -6,9 +6,10 @@ BASELINE.json config 5 trains ViT-B/16 under DDP to stress large-parameter bucke
 
 MI355X notes
 ------------
-* Self-attention uses ``F.scaled_dot_product_attention`` (PyTorch-ROCm dispatches it to its
-  fused CK/aotriton flash kernels on gfx950) instead of ``nn.MultiheadAttention``'s unfused
-  training path.  The parameters keep ``nn.MultiheadAttention``'s names (``in_proj_weight``,
+* Self-attention runs the fused MFMA kernels of ops/attention.py (csrc/kernels/attn_kernels.hip:
+  one workgroup per (image, head), Q/K/V read straight from the QKV projection output, context
+  written straight into the out-projection input) for bf16 GPU runs; elsewhere it uses
+  ``F.scaled_dot_product_attention`` instead of ``nn.MultiheadAttention``'s unfused path.  The parameters keep ``nn.MultiheadAttention``'s names (``in_proj_weight``,
   ``in_proj_bias``, ``out_proj.*``) so state dicts load into torchvision unchanged.
 * 197 tokens (14x14 patches + CLS): no sequence sharding is needed.
 * Under bf16/fp16 autocast on the GPU the encoder runs a fused path (ops/vit.py,
@@ -28,6 +29,7 @@ import torch.nn.functional as F
 
 from ..ops.vit import (add_bias_layer_norm16, bias_gelu16, layer_norm16, linear16, ln_fusable, merge_heads,
                        split_heads)
+from ..ops import attention as fused_attn
 from ..parallel.shadow import shadow_param
 
 
@@ -47,6 +49,8 @@ class SelfAttention(nn.Module):
     def _context(self, x: torch.Tensor) -> torch.Tensor:
         b, s, d = x.shape
         qkv = linear16(x, shadow_param(self, "in_proj_weight", x), shadow_param(self, "in_proj_bias", x))
+        if (not self.training or self.dropout == 0.0) and fused_attn.supported(qkv, self.heads):
+            return fused_attn.attention(qkv, self.heads)  # heads split/merged inside the kernels
         q, k, v = split_heads(qkv, self.heads)
         y = F.scaled_dot_product_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0)
         return merge_heads(y)
