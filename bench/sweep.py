@@ -31,9 +31,12 @@ TABLES = {
 }
 
 
-def run_point(extra, steps, warmup, out, timeout, launcher=None):
+def run_point(extra, steps, warmup, out, timeout, launcher=None, find=True):
+    # --find: MIOpen find mode (cudnn.benchmark).  Off = immediate mode over the shipped find-db
+    # (bf16 shapes); fp32 shapes then use MIOpen's heuristics instead of minutes of searching.
     cmd = (launcher or [sys.executable]) + [os.path.join(ROOT, "bench.py"), "--steps", str(steps),
-                                            "--warmup", str(warmup), "--json-out", out, "--find"] + extra
+                                            "--warmup", str(warmup), "--json-out", out] + \
+        (["--find"] if find else []) + extra
     print("+", " ".join(cmd), flush=True)
     r = subprocess.run(cmd, cwd=ROOT, timeout=timeout)
     return r.returncode
@@ -58,6 +61,7 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--timeout", type=int, default=600)
+    ap.add_argument("--no-find", action="store_true", help="MIOpen immediate mode (no find-mode search)")
     ap.add_argument("--extra", default="", help="extra bench.py args for every point")
     ap.add_argument("--nproc", type=int, default=1, help=">1: launch each point with torch.distributed.run")
     ap.add_argument("--markdown", default=None)
@@ -71,7 +75,7 @@ def main(argv=None):
                     "--master-addr", "127.0.0.1", "--master-port", "29561"]
     rc = 0
     for extra in TABLES[a.table]:
-        rc |= run_point(extra + a.extra.split(), a.steps, a.warmup, a.out, a.timeout, launcher)
+        rc |= run_point(extra + a.extra.split(), a.steps, a.warmup, a.out, a.timeout, launcher, not a.no_find)
         if rc:
             break
     return rc
