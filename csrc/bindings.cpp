@@ -222,16 +222,21 @@ void check_cl_bf16(const Tensor& t, const char* name) {
 }
 
 // Returns {y, psum, psq} (psum/psq empty unless want_stats): y = conv2d(x, w, stride, pad).
-std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bool want_stats) {
+// out_h/out_w > 0: explicit output size, no larger than the symmetric-padding one (the extra
+// padding rows/columns at the bottom/right are dropped: asymmetric padding).
+std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bool want_stats, int64_t out_h,
+                             int64_t out_w) {
   check_cl_bf16(x, "x");
   check_cl_bf16(w, "w");
   const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int Cout = w.size(0), R = w.size(2), S = w.size(3);
   TORCH_CHECK(w.size(1) == C, "conv_fwd: channel mismatch");
-  TORCH_CHECK(dpt::conv_supported(C, Cout), "conv_fwd: needs C % 64 == 0 and Cout % 64 == 0");
+  TORCH_CHECK(dpt::conv_supported(C, Cout) || dpt::conv_supported_narrow(C, Cout, S),
+              "conv_fwd: needs C % 64 == 0 (or C in {16, 32} with S % (64/C) == 0) and Cout % 64 == 0");
   TORCH_CHECK(stride >= 1 && pad >= 0, "conv_fwd: bad stride/pad");
-  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
-  TORCH_CHECK(Ho > 0 && Wo > 0, "conv_fwd: empty output");
+  const int Hs = (H + 2 * pad - R) / stride + 1, Ws = (W + 2 * pad - S) / stride + 1;
+  const int Ho = out_h > 0 ? out_h : Hs, Wo = out_w > 0 ? out_w : Ws;
+  TORCH_CHECK(Ho > 0 && Wo > 0 && Ho <= Hs && Wo <= Ws, "conv_fwd: bad output size");
   auto y = at::empty({N, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor ps, pq;
   if (want_stats) {
@@ -243,7 +248,7 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bo
   dpt::launch_conv_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()), N, H, W, C, Cout, R, S, (int)stride, (int)pad,
                        want_stats ? ps.data_ptr<float>() : nullptr, want_stats ? pq.data_ptr<float>() : nullptr,
-                       cur_stream(x));
+                       cur_stream(x), Ho, Wo);
   return {y, ps, pq};
 }
 
@@ -296,9 +301,13 @@ Tensor conv_wgrad(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stri
   const int Cout = wshape[0], C = wshape[1], R = wshape[2], S = wshape[3];
   const int N = x.size(0), H = x.size(2), W = x.size(3);
   TORCH_CHECK(x.size(1) == C && dy.size(1) == Cout && dy.size(0) == N, "conv_wgrad: shape mismatch");
-  TORCH_CHECK(dpt::conv_supported(C, Cout), "conv_wgrad: needs C % 64 == 0 and Cout % 64 == 0");
-  auto pl = dpt::conv_wgrad_plan(N, H, W, C, Cout, R, S, (int)stride, (int)pad);
-  TORCH_CHECK(dy.size(2) == pl.Ho && dy.size(3) == pl.Wo, "conv_wgrad: grad_output spatial mismatch");
+  TORCH_CHECK(dpt::conv_supported(C, Cout) || dpt::conv_supported_narrow(C, Cout, S),
+              "conv_wgrad: needs C % 64 == 0 (or C in {16, 32} with S % (64/C) == 0) and Cout % 64 == 0");
+  const int Hs = (H + 2 * pad - R) / stride + 1, Ws = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(dy.size(2) >= 1 && dy.size(2) <= Hs && dy.size(3) >= 1 && dy.size(3) <= Ws,
+              "conv_wgrad: grad_output spatial mismatch");
+  // the output size comes from dy (covers asymmetric padding)
+  auto pl = dpt::conv_wgrad_plan(N, H, W, C, Cout, R, S, (int)stride, (int)pad, (int)dy.size(2), (int)dy.size(3));
   TORCH_CHECK((int64_t)N * pl.Ho * pl.Wo < (1ll << 31), "conv_wgrad: too many pixels");
   auto dw = at::empty({Cout, C, R, S}, x.options().dtype(fp32_out ? at::kFloat : at::kBFloat16)
                                           .memory_format(at::MemoryFormat::ChannelsLast));
@@ -362,6 +371,21 @@ Tensor attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, int64_t heads, 
                        reinterpret_cast<const uint16_t*>(dout.data_ptr()), lse.data_ptr<float>(),
                        reinterpret_cast<uint16_t*>(dqkv.data_ptr()), B, S, H, (float)scale, cur_stream(qkv));
   return dqkv;
+}
+
+// 2x2 space-to-depth of a channels_last [N, C<=4, H, W] fp32/bf16 image -> channels_last bf16
+// [N, 16, H/2, W/2] (channel (a*2 + b)*4 + c)
+Tensor space_to_depth2(Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
+              "space_to_depth2: x must be a 4-d fp32/bf16 GPU tensor");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "space_to_depth2: x must be channels_last");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C <= 4 && H % 2 == 0 && W % 2 == 0, "space_to_depth2: needs C <= 4 and even H, W");
+  auto a = at::empty({N, 16, H / 2, W / 2}, x.options().dtype(at::kBFloat16).memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(x.device().index());
+  dpt::launch_space_to_depth2(x.data_ptr(), x.scalar_type() == at::kBFloat16, reinterpret_cast<uint16_t*>(a.data_ptr()),
+                              N, H, W, C, cur_stream(x));
+  return a;
 }
 
 std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::optional<Tensor> weight,
@@ -720,7 +744,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("stride"), py::arg("pad"));
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("grad_output"), py::arg("idx"), py::arg("H"), py::arg("W"),
         py::arg("k"), py::arg("stride"), py::arg("pad"));
-  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"));
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"),
+        py::arg("out_h") = 0, py::arg("out_w") = 0);
+  m.def("space_to_depth2", &space_to_depth2, py::arg("x"));
   m.def("conv_wgrad", &conv_wgrad, py::arg("grad_output"), py::arg("x"), py::arg("weight_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("fp32_out"));
   m.def("im2col", &im2col, py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("Kp"));

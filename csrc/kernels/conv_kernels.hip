@@ -115,6 +115,9 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
   // One glds wave instruction fills 8 whole LDS rows lane-linearly: lane L of wave w owns
   // LDS slot L&7 of row (A_PER_T*w + i)*8 + L/8 and loads the chunk the swizzle puts there
   // (slot ^ ((row>>1)&7): the XOR is its own inverse).
+  // Narrow inputs (C = 16/32): one 64-wide K-step spans 64/C consecutive taps along s, i.e.
+  // consecutive input pixels, so a lane's 16-byte chunk sits at sub-tap (chunk*8)/C and the
+  // address is unchanged (pixel stride = C elements); only its bounds check moves.
   int hi0[A_PER_T], wi0[A_PER_T];
   int64_t abase[A_PER_T];
   const int64_t HoWo = (int64_t)p.Ho * p.Wo;
@@ -128,8 +131,8 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
       const int rem = (int)(m - n * HoWo);
       const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
       hi0[i] = ho * p.stride - p.pad;
-      wi0[i] = wo * p.stride - p.pad;
-      abase[i] = ((n * p.H + hi0[i]) * (int64_t)p.W + wi0[i]) * p.C + achunk * 8;
+      wi0[i] = wo * p.stride - p.pad + (p.C < BK ? achunk * 8 / p.C : 0);
+      abase[i] = ((n * p.H + hi0[i]) * (int64_t)p.W + wo * p.stride - p.pad) * p.C + achunk * 8;
     } else {
       hi0[i] = -(1 << 28);  // never in bounds
       wi0[i] = 0;
@@ -155,12 +158,13 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
     }
   }
 
-  const int cblocks = p.C / BK;
-  const int nk = p.R * p.S * cblocks;
+  const int cblocks = p.C >= BK ? p.C / BK : 1;
+  const int tps = p.C >= BK ? 1 : BK / p.C;  // taps per K-step (narrow inputs)
+  const int nk = (int)(Kg / BK);
 
   // global -> LDS directly (no staging registers); wave-uniform LDS base per 1 KiB.
   auto stage = [&](int ks, int buf) {
-    const int rs = ks / cblocks, cb = ks - rs * cblocks;
+    const int rs = (ks / cblocks) * tps, cb = ks - (ks / cblocks) * cblocks;
     const int r = rs / p.S, s = rs - r * p.S;
     const int64_t koff = ((int64_t)r * p.W + s) * p.C + cb * BK;
     unsigned char* a = lds + buf * STAGE;
@@ -175,7 +179,7 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
     }
     // BKN: rows co = cb*BK + krow, flipped tap (R-1-r, S-1-s)
     const int64_t wk = BKN ? ((int64_t)cb * BK * p.R * p.S + (p.R - 1 - r) * p.S + (p.S - 1 - s)) * p.Cout
-                           : (int64_t)rs * p.C + cb * BK;
+                           : (int64_t)ks * BK;  // k = (r*S + s)*C + c: K-step ks is [64ks, 64ks+64)
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(wrow[i] + wk),
@@ -579,8 +583,11 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_wgrad_kernel(ConvWgrad
   const int sp = bid / tiles, tile = bid - sp * tiles;
   const int ct = tile / p.n_tiles, nt = tile - ct * p.n_tiles;
   const int co0 = ct * BMW;
-  const int cblocks = p.C / BNW;
-  const int rs = nt / cblocks, cb = nt - rs * cblocks;
+  // n-tile = K range [nt*BNW, nt*BNW + BNW) of k = (r*S + s)*C + c; narrow inputs (C < BNW)
+  // cover BNW/C consecutive taps along s per tile (consecutive input pixels)
+  const int cblocks = p.C >= BNW ? p.C / BNW : 1;
+  const int tps = p.C >= BNW ? 1 : BNW / p.C;
+  const int rs = (nt / cblocks) * tps, cb = nt - (nt / cblocks) * cblocks;
   const int r = rs / p.S, s = rs - r * p.S;
   const int ci0 = cb * BNW;
   const int k0 = sp * p.steps_per_split;
@@ -623,7 +630,8 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_wgrad_kernel(ConvWgrad
           const uint32_t rem = (uint32_t)m - n * (uint32_t)(p.Ho * p.Wo);
           const uint32_t ho = fdiv(rem, p.div_wo), wo = rem - ho * (uint32_t)p.Wo;
           const int hi = (int)ho * p.stride - p.pad + r, wi = (int)wo * p.stride - p.pad + s;
-          if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+          const int sub = tps > 1 ? bchk[i] * 8 / p.C : 0;  // narrow inputs: this chunk's tap
+          if ((unsigned)hi < (unsigned)p.H && (unsigned)(wi + sub) < (unsigned)p.W)
             src = p.x + (((int64_t)n * p.H + hi) * p.W + wi) * p.C + ci0 + bchk[i] * 8;
         }
       }
@@ -681,7 +689,7 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_wgrad_kernel(ConvWgrad
   }
   // fp32 partial tile: rows = output channels, columns = (r, s, ci) of this tap
   const int64_t Kg = (int64_t)p.R * p.S * p.C;
-  float* out = p.part + (int64_t)sp * p.Cout * Kg + (int64_t)rs * p.C + ci0;
+  float* out = p.part + (int64_t)sp * p.Cout * Kg + (int64_t)nt * BNW;
   const int lr = lane & 31, lh = lane >> 5;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -781,6 +789,53 @@ __global__ __launch_bounds__(kBlock) void im2col_kernel(const T* __restrict__ x,
   }
 }
 
+// ---- space-to-depth (2x2) stem input ---------------------------------------------------------
+// A 7x7/2 conv on [H, W, 3] is a 4x4/1 conv on the 2x2 space-to-depth image [H/2, W/2, 12]
+// (channels padded to 16, weight taps re-indexed as r = 2r' + a - 1, s = 2s' + b - 1): K = 256,
+// every 64-wide K-step four consecutive pixels of one row - the narrow-input path of the
+// implicit-GEMM kernels.  One thread per output pixel: 4 input pixels in, 32 bytes out.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void space_to_depth2_kernel(const T* __restrict__ x, uint16_t* __restrict__ a,
+                                                                 int64_t npix, int H, int W, int C) {
+  const int H2 = H / 2, W2 = W / 2;
+  for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < npix; t += (int64_t)gridDim.x * kBlock) {
+    const int64_t n = t / ((int64_t)H2 * W2);
+    const int rem = (int)(t - n * H2 * W2);
+    const int i = rem / W2, j = rem - i * W2;
+    uint32_t pk[8];
+#pragma unroll
+    for (int ab = 0; ab < 4; ++ab) {
+      const T* src = x + ((n * H + 2 * i + (ab >> 1)) * (int64_t)W + 2 * j + (ab & 1)) * C;
+      float f[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        f[c] = 0.f;
+        if (c < C) {
+          if constexpr (sizeof(T) == 4) f[c] = (float)src[c];
+          else f[c] = bf16_to_f32((uint16_t)src[c]);
+        }
+      }
+      const f32x2_t v0 = {f[0], f[1]}, v1 = {f[2], f[3]};
+      pk[2 * ab] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v0, bf16x2_t));
+      pk[2 * ab + 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v1, bf16x2_t));
+    }
+    uint4* dst = reinterpret_cast<uint4*>(a + t * 16);
+    dst[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    dst[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+  }
+}
+
+void launch_space_to_depth2(const void* x, bool x_bf16, uint16_t* a, int N, int H, int W, int C, hipStream_t st) {
+  const int64_t npix = (int64_t)N * (H / 2) * (W / 2);
+  const dim3 grid((unsigned)grid_for(npix, 2));
+  if (x_bf16)
+    hipLaunchKernelGGL(space_to_depth2_kernel<uint16_t>, grid, dim3(kBlock), 0, st, static_cast<const uint16_t*>(x), a,
+                       npix, H, W, C);
+  else
+    hipLaunchKernelGGL(space_to_depth2_kernel<float>, grid, dim3(kBlock), 0, st, static_cast<const float*>(x), a, npix,
+                       H, W, C);
+}
+
 void launch_im2col(const void* x, bool x_bf16, uint16_t* a, int N, int H, int W, int C, int R, int S, int stride,
                    int pad, int Kp, hipStream_t st) {
   const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
@@ -813,6 +868,11 @@ __global__ __launch_bounds__(kBlock) void conv_wt_flip_kernel(const uint16_t* __
 }
 
 bool conv_supported(int C, int Cout) { return C % 64 == 0 && Cout % 64 == 0; }
+
+// Narrow inputs (C = 16 or 32) need the taps of one K-step to be consecutive along s.
+bool conv_supported_narrow(int C, int Cout, int S) {
+  return (C == 16 || C == 32) && Cout % 64 == 0 && S % (64 / C) == 0;
+}
 
 int conv_m_tiles(int64_t M) { return (int)((M + conv::BM - 1) / conv::BM); }
 
@@ -874,12 +934,14 @@ static void conv_fwd_dispatch(int variant, bool bkn, ConvFwdArgs a, hipStream_t 
 }
 
 static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
-                          int R, int S, int stride, int pad, float* psum, float* psq, bool bkn, hipStream_t s) {
+                          int R, int S, int stride, int pad, float* psum, float* psq, bool bkn, hipStream_t s,
+                          int Ho = 0, int Wo = 0) {
   ConvFwdArgs a;
   a.x = x; a.w = w; a.y = y; a.psum = psum; a.psq = psq;
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S; a.stride = stride; a.pad = pad;
-  a.Ho = (H + 2 * pad - R) / stride + 1;
-  a.Wo = (W + 2 * pad - S) / stride + 1;
+  // explicit output size: asymmetric padding (pad on top/left only, e.g. the space-to-depth stem)
+  a.Ho = Ho > 0 ? Ho : (H + 2 * pad - R) / stride + 1;
+  a.Wo = Wo > 0 ? Wo : (W + 2 * pad - S) / stride + 1;
   a.M = (int64_t)N * a.Ho * a.Wo;
   a.m_tiles = conv_m_tiles(a.M);
   const bool wide = Cout % 128 == 0;
@@ -890,8 +952,8 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
 }
 
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
-                     int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s) {
-  conv_fwd_impl(x, w, y, N, H, W, C, Cout, R, S, stride, pad, psum, psq, false, s);
+                     int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s, int Ho, int Wo) {
+  conv_fwd_impl(x, w, y, N, H, W, C, Cout, R, S, stride, pad, psum, psq, false, s, Ho, Wo);
 }
 
 // Stride-1 backward-data: dx[N,H,W,C] = conv(dy, flip(w)^T, pad' = R-1-pad) with the flip and
@@ -914,14 +976,15 @@ static FastDiv make_fastdiv(uint32_t d) {
   return f;
 }
 
-ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad) {
+ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad, int Ho,
+                              int Wo) {
   ConvWgradPlan pl;
-  pl.Ho = (H + 2 * pad - R) / stride + 1;
-  pl.Wo = (W + 2 * pad - S) / stride + 1;
+  pl.Ho = Ho > 0 ? Ho : (H + 2 * pad - R) / stride + 1;
+  pl.Wo = Wo > 0 ? Wo : (W + 2 * pad - S) / stride + 1;
   const int64_t M = (int64_t)N * pl.Ho * pl.Wo;
   pl.bmw = Cout % 128 == 0 ? 128 : 64;
   pl.bnw = C % 128 == 0 ? 128 : 64;
-  const int tiles = (Cout / pl.bmw) * (R * S * (C / pl.bnw));
+  const int tiles = (Cout / pl.bmw) * (R * S * C / pl.bnw);
   const int steps = (int)((M + 63) / 64);
   // ~768 blocks (3 per CU) and at least 32 K-steps per split: a split's fp32 partial tile
   // (BMW x BNW x 4 B, written once and read once by the reduce) then costs < 1/8 of the
@@ -944,7 +1007,7 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
   a.Ho = pl.Ho; a.Wo = pl.Wo;
   a.M = N * pl.Ho * pl.Wo;
   a.co_tiles = Cout / pl.bmw;
-  a.n_tiles = R * S * (C / pl.bnw);
+  a.n_tiles = R * S * C / pl.bnw;
   a.splits = pl.splits;
   a.steps_per_split = pl.steps_per_split;
   a.div_wo = make_fastdiv((uint32_t)pl.Wo);

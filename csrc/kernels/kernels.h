@@ -114,23 +114,30 @@ void launch_rows_copy16(const uint16_t* src, uint16_t* dst, const int n[4], cons
 // w [Cout,R,S,C], y [N,Ho,Wo,Cout]; C % 64 == 0, Cout % 64 == 0.  psum/psq (optional): BN
 // partial sums of y per (channel, M-tile), layout [Cout][conv_m_tiles(M)].
 bool conv_supported(int C, int Cout);
+bool conv_supported_narrow(int C, int Cout, int S);  // C = 16/32 with S % (64/C) == 0 (fwd, wgrad)
 int conv_m_tiles(int64_t M);
 void conv_set_variant(int v);
+// Ho/Wo > 0: explicit output size (padding applied on top/left only beyond what it needs)
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
-                     int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s);
+                     int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s, int Ho = 0,
+                     int Wo = 0);
 // backward-weight: dw [Cout,R,S,C] (kind 0 f32 / 1 bf16) = sum over pixels of dy x x-shifted;
 // part: plan.part_floats floats of split-K scratch.  C % 64 == 0, Cout % 64 == 0.
 struct ConvWgradPlan {
   int Ho, Wo, bmw, bnw, splits, steps_per_split;
   int64_t part_floats;
 };
-ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad);
+ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad, int Ho = 0,
+                              int Wo = 0);
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void* dw, int dw_kind, int N, int H,
                        int W, int C, int Cout, int R, int S, int stride, int pad, const ConvWgradPlan& plan,
                        hipStream_t s);
 // stride-1 backward-data straight from the KRSC weight w [Cout,R,S,C]: dy [N,Ho,Wo,Cout] -> dx [N,Ho,Wo,C]
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout, int C,
                        int R, int S, int pad, hipStream_t s);
+// space-to-depth stem input: x [N,H,W,C] fp32/bf16 (channels_last, H, W even, C <= 4) ->
+// a [N, H/2, W/2, 16] bf16 with channel (a*2 + b)*4 + c = x[2i + a][2j + b][c] (zero for c >= C)
+void launch_space_to_depth2(const void* x, bool x_bf16, uint16_t* a, int N, int H, int W, int C, hipStream_t s);
 // im2col for narrow-input convs: a [N*Ho*Wo, Kp] bf16 (k = (r*S+s)*C + c, zero past R*S*C)
 void launch_im2col(const void* x, bool x_bf16, uint16_t* a, int N, int H, int W, int C, int R, int S, int stride,
                    int pad, int Kp, hipStream_t s);

@@ -61,21 +61,21 @@ def _backward(ctx, dy):
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride: int, pad: int):
-        y = native().conv_fwd(x, w, stride, pad, False)[0]
+    def forward(ctx, x, w, stride: int, pad: int, out_hw):
+        y = native().conv_fwd(x, w, stride, pad, False, *out_hw)[0]
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad = stride, pad
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        return _backward(ctx, dy) + (None, None)
+        return _backward(ctx, dy) + (None, None, None)
 
 
 class _ConvStats(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride: int, pad: int):
-        y, ps, pq = native().conv_fwd(x, w, stride, pad, True)
+    def forward(ctx, x, w, stride: int, pad: int, out_hw):
+        y, ps, pq = native().conv_fwd(x, w, stride, pad, True, *out_hw)
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad = stride, pad
         ctx.mark_non_differentiable(ps, pq)
@@ -84,16 +84,18 @@ class _ConvStats(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dps, _dpq):
-        return _backward(ctx, dy) + (None, None)
+        return _backward(ctx, dy) + (None, None, None)
 
 
-def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bool = False) -> torch.Tensor:
+def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bool = False,
+           out_hw=(0, 0)) -> torch.Tensor:
     """y = conv2d(x, w, stride, pad) on the MFMA kernels; ``bn_stats`` attaches the output's
-    BatchNorm partial sums as ``y._dpt_bn_partials`` (consumed by ops/bn.py)."""
+    BatchNorm partial sums as ``y._dpt_bn_partials`` (consumed by ops/bn.py).  ``out_hw``:
+    explicit output size (asymmetric padding: top/left ``pad``, bottom/right what fits)."""
     w = _cl(w)
     if not bn_stats:
-        return _Conv.apply(x, w, int(stride), int(pad))
-    y, ps, pq = _ConvStats.apply(x, w, int(stride), int(pad))
+        return _Conv.apply(x, w, int(stride), int(pad), tuple(out_hw))
+    y, ps, pq = _ConvStats.apply(x, w, int(stride), int(pad), tuple(out_hw))
     y._dpt_bn_partials = (ps, pq)
     return y
 
@@ -104,8 +106,38 @@ def take_bn_partials(x: torch.Tensor):
     return part
 
 
+def s2d_stem_supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups) -> bool:
+    """ResNet's 7x7/2 pad-3 stem on <= 4 input channels: space-to-depth + 4x4 MFMA conv."""
+    if not (ENABLED and x.is_cuda and native_available() and x.dim() == 4 and groups == 1
+            and x.dtype in (torch.float32, torch.bfloat16) and w.dtype == torch.bfloat16):
+        return False
+    cout, cin, r, s = w.shape
+    return (cin <= 4 and cout % 64 == 0 and (r, s) == (7, 7) and tuple(stride) == (2, 2)
+            and tuple(padding) == (3, 3) and tuple(dilation) == (1, 1) and not x.requires_grad
+            and x.shape[1] == cin and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0
+            and x.is_contiguous(memory_format=_CL))
+
+
+def s2d_stem_conv2d(x: torch.Tensor, w: torch.Tensor, bn_stats: bool = False) -> torch.Tensor:
+    """7x7 / stride 2 / pad 3 conv as a 4x4 / stride 1 conv on the 2x2 space-to-depth image.
+
+    With r = 2r' + a - 1 and s = 2s' + b - 1 (r', s' in 0..3, a, b in {0, 1}; tap -1 has zero
+    weight) the input row 2*ho - 3 + r is 2*(ho - 2 + r') + a, so
+    y[ho, wo] = sum_{r', s'} X2[ho - 2 + r', wo - 2 + s'] . W2[r', s']  with
+    X2[i, j, (a*2 + b)*4 + c] = x[2i + a, 2j + b, c] and W2[r', s', (a*2+b)*4 + c] = w[2r'+a-1, 2s'+b-1, c]:
+    K = 4*4*16 = 256, each 64-wide K-step four consecutive pixels of one row (the kernels' narrow-
+    input path), top/left padding 2, output H/2 x W/2.  The weight re-indexing is plain torch ops,
+    so autograd maps the 4x4 weight gradient back onto the 7x7 one."""
+    cout, cin = w.shape[0], w.shape[1]
+    x2 = native().space_to_depth2(x)
+    wk = torch.nn.functional.pad(w.permute(0, 2, 3, 1), (0, 4 - cin, 1, 0, 1, 0))       # [Co, 8, 8, 4]
+    w2 = wk.reshape(cout, 4, 2, 4, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(cout, 4, 4, 16)
+    w2 = w2.permute(0, 3, 1, 2)                                                         # [Co, 16, 4, 4] cl
+    return conv2d(x2, w2, 1, 2, bn_stats, out_hw=(x.shape[2] // 2, x.shape[3] // 2))
+
+
 def stem_supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups) -> bool:
-    """Narrow-input conv (ResNet's 3-channel 7x7 stem) on the im2col + MFMA GEMM path."""
+    """Narrow-input conv (any kernel/stride) on the im2col + MFMA GEMM path."""
     if not (ENABLED and x.is_cuda and native_available() and x.dim() == 4 and groups == 1
             and x.dtype in (torch.float32, torch.bfloat16) and w.dtype == torch.bfloat16):
         return False

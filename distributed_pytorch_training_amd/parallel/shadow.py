@@ -48,6 +48,8 @@ class ShadowConv2d(nn.Conv2d):
         w, b = sh["weight"], sh.get("bias", self.bias)
         if b is None and native_conv.supported(x, w, self.stride, self.padding, self.dilation, self.groups):
             return native_conv.conv2d(x, w, self.stride[0], self.padding[0], self.dpt_bn_stats)
+        if b is None and native_conv.s2d_stem_supported(x, w, self.stride, self.padding, self.dilation, self.groups):
+            return native_conv.s2d_stem_conv2d(x, w, self.dpt_bn_stats)
         if (b is None and native_conv.STEM_ENABLED
                 and native_conv.stem_supported(x, w, self.stride, self.padding, self.dilation, self.groups)):
             return native_conv.stem_conv2d(x, w, self.stride[0], self.padding[0], self.dpt_bn_stats)

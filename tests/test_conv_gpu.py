@@ -182,3 +182,29 @@ def test_stem_im2col_conv_matches_fp32(cuda, xdtype):
     y.backward(gy)
     wref = torch.nn.grad.conv2d_weight(x.float().to(torch.bfloat16).float(), w.shape, gy.float(), stride=2, padding=3)
     torch.testing.assert_close(w.grad.float(), wref, rtol=2e-2, atol=2e-2 * wref.abs().max().item())
+
+
+@pytest.mark.parametrize("xdtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("hw", [(224, 224), (34, 30)])
+def test_s2d_stem_matches_fp32(cuda, xdtype, hw):
+    """7x7/2 stem as space-to-depth + 4x4 MFMA conv (narrow-input path): forward, BN partials,
+    and the 7x7 weight gradient through the re-indexing."""
+    from distributed_pytorch_training_amd.ops import conv as native_conv
+
+    g = torch.Generator(device=cuda).manual_seed(11)
+    n = 2 if hw[0] == 224 else 3
+    x = torch.randn(n, 3, *hw, device=cuda, generator=g).to(xdtype).contiguous(memory_format=CL)
+    w = (torch.randn(64, 3, 7, 7, device=cuda, generator=g) * 0.05).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL).requires_grad_(True)
+    assert native_conv.s2d_stem_supported(x, w, (2, 2), (3, 3), (1, 1), 1)
+    y = native_conv.s2d_stem_conv2d(x, w, bn_stats=True)
+    xr = x.float().to(torch.bfloat16).float()
+    ref = F.conv2d(xr, w.detach().float(), stride=2, padding=3)
+    assert y.shape == ref.shape
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+    ps, pq = y._dpt_bn_partials
+    torch.testing.assert_close(ps.sum(1), y.float().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    wref = torch.nn.grad.conv2d_weight(xr, w.shape, gy.float(), stride=2, padding=3)
+    torch.testing.assert_close(w.grad.float(), wref, rtol=2e-2, atol=2e-2 * wref.abs().max().item())
