@@ -113,7 +113,9 @@ def test_bn_from_conv_partials_matches_stats_pass(cuda, n, hw):
     torch.testing.assert_close(i1, i2, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(rv1, rv2, rtol=1e-5, atol=1e-6)
     assert nb1.item() == nb2.item() == 1
-    assert (o1.float() - o2.float()).abs().max().item() <= 2 ** -6
+    # the two statistics differ only in summation order: outputs agree to one bf16 ulp
+    d = (o1.float() - o2.float()).abs()
+    assert (d <= 2 ** -7 * o2.float().abs().clamp_min(1.0)).all()
 
 
 def test_resnet50_native_conv_matches_miopen(cuda):
