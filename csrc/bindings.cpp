@@ -271,6 +271,37 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t pad) {
   return dx;
 }
 
+// Stride-1 backward-data whose epilogue also sums the backward statistics of the BatchNorm+ReLU
+// that produced the conv's input (bn_x: that BN's input, same shape as dx; coef = [a | b]).
+// Returns {dx, p1, p2} with p1/p2 [C, m_tiles] for bn_bwd_partials.
+std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor bn_x, Tensor bn_mean, Tensor bn_coef) {
+  check_cl_bf16(dy, "grad_output");
+  check_cl_bf16(w, "w");
+  check_cl_bf16(bn_x, "bn_x");
+  const int Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(dy.size(1) == Cout && dpt::conv_supported(Cout, C), "conv_dgrad_bnstats: bad shapes");
+  TORCH_CHECK(R - 1 - pad >= 0 && S == R, "conv_dgrad_bnstats: needs square kernel and pad <= R-1");
+  const int N = dy.size(0), Ho = dy.size(2), Wo = dy.size(3);
+  const int H = Ho + R - 1 - 2 * (int)pad, W = Wo + S - 1 - 2 * (int)pad;
+  TORCH_CHECK(bn_x.size(0) == N && bn_x.size(1) == C && bn_x.size(2) == H && bn_x.size(3) == W,
+              "conv_dgrad_bnstats: bn_x must match the conv input");
+  auto wt = at::empty({C, Cout, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int mt = dpt::conv_m_tiles((int64_t)N * H * W);
+  auto p1 = at::empty({C, mt}, dy.options().dtype(at::kFloat));
+  auto p2 = at::empty({C, mt}, dy.options().dtype(at::kFloat));
+  c10::hip::HIPGuard guard(dy.device().index());
+  auto st = cur_stream(dy);
+  dpt::launch_conv_wt_flip(reinterpret_cast<const uint16_t*>(w.data_ptr()), reinterpret_cast<uint16_t*>(wt.data_ptr()),
+                           Cout, R, S, C, st);
+  dpt::launch_conv_dgrad_bnstats(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                 reinterpret_cast<const uint16_t*>(wt.data_ptr()), reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                                 N, Ho, Wo, Cout, C, R, S, (int)pad, reinterpret_cast<const uint16_t*>(bn_x.data_ptr()),
+                                 f32_param(bn_mean, C, "bn_mean"), f32_param(bn_coef, 2 * C, "bn_coef"),
+                                 p1.data_ptr<float>(), p2.data_ptr<float>(), st);
+  return {dx, p1, p2};
+}
+
 // Same through an explicitly flipped/transposed weight copy (returned too): the reference
 // path the tests compare the folded addressing against.
 std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad) {
@@ -488,6 +519,31 @@ std::vector<Tensor> bn_bwd(Tensor dy, c10::optional<Tensor> dy2, c10::optional<T
                      want_dparams ? dg.data_ptr<float>() : nullptr, want_dparams ? db.data_ptr<float>() : nullptr,
                      dx.data_ptr(), make_dz ? dz.data_ptr() : nullptr, ws.data_ptr<float>(), relu, cur_stream(x));
   return {dx, dg, db, dz};
+}
+
+// BN+ReLU backward from statistics partials summed by the consuming conv's dgrad epilogue:
+// {dx, dgamma, dbeta}; the ReLU mask is recomputed from x and coef.
+std::vector<Tensor> bn_bwd_partials(Tensor dy, Tensor x, c10::optional<Tensor> weight, Tensor mean, Tensor invstd,
+                                    Tensor coef, Tensor p1, Tensor p2, bool want_dparams) {
+  auto [M, C] = bn_rows(x, "x");
+  auto [Md, Cd] = bn_rows(dy, "grad_output");
+  TORCH_CHECK(M == Md && C == Cd && dy.scalar_type() == x.scalar_type(), "grad_output mismatch");
+  TORCH_CHECK(p1.is_cuda() && p1.scalar_type() == at::kFloat && p1.dim() == 2 && p1.size(0) == C &&
+                  p1.is_contiguous() && p2.sizes() == p1.sizes() && p2.is_contiguous(),
+              "bn_bwd_partials: partials must be contiguous fp32 [C, chunks]");
+  auto fopt = x.options().dtype(at::kFloat);
+  auto dx = at::empty_like(x);
+  Tensor dg = want_dparams ? at::empty({C}, fopt) : Tensor();
+  Tensor db = want_dparams ? at::empty({C}, fopt) : Tensor();
+  auto kbuf = at::empty({3 * C}, fopt);
+  c10::hip::HIPGuard guard(x.device().index());
+  dpt::launch_bn_bwd_from_partials(bn_dtype(x), dy.data_ptr(), x.data_ptr(), M, C, f32_param(weight, C, "weight"),
+                                   f32_param(mean, C, "mean"), f32_param(invstd, C, "invstd"),
+                                   f32_param(coef, 2 * C, "coef"), p1.data_ptr<float>(), p2.data_ptr<float>(),
+                                   (int)p1.size(1), want_dparams ? dg.data_ptr<float>() : nullptr,
+                                   want_dparams ? db.data_ptr<float>() : nullptr, dx.data_ptr(), kbuf.data_ptr<float>(),
+                                   cur_stream(x));
+  return {dx, dg, db};
 }
 
 std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t stride, int64_t pad) {
@@ -755,6 +811,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("heads"), py::arg("scale"));
   m.def("conv_set_variant", &dpt::conv_set_variant, py::arg("variant"));
   m.def("conv_dgrad", &conv_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
+  m.def("conv_dgrad_bnstats", &conv_dgrad_bnstats, py::arg("grad_output"), py::arg("w"), py::arg("pad"),
+        py::arg("bn_x"), py::arg("bn_mean"), py::arg("bn_coef"));
+  m.def("bn_bwd_partials", &bn_bwd_partials, py::arg("grad_output"), py::arg("x"), py::arg("weight"), py::arg("mean"),
+        py::arg("invstd"), py::arg("coef"), py::arg("p1"), py::arg("p2"), py::arg("want_dparams"));
   m.def("conv_dgrad_flip", &conv_dgrad_flip, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
 

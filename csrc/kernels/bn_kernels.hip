@@ -648,6 +648,72 @@ void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, co
   }
 }
 
+// Backward finalize over MANY [C][chunks] partials (the dgrad epilogue of the consuming conv
+// writes one per 128 rows): one 256-thread block per channel, fp64 block reduce.
+__global__ __launch_bounds__(kBlock) void bn_bwd_finalize_wide_kernel(
+    const float* __restrict__ p1, const float* __restrict__ p2, int chunks, int C, int64_t M,
+    const float* __restrict__ gamma, const float* __restrict__ invstd, float* dgamma, float* dbeta,
+    float* k1, float* k2, float* k3) {
+  __shared__ double red[2][kBlock / 64];
+  const int c = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* q1 = p1 + (int64_t)c * chunks;
+  const float* q2 = p2 + (int64_t)c * chunks;
+  double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+  int k = threadIdx.x;
+  for (; k + kBlock < chunks; k += 2 * kBlock) {
+    const float x0 = q1[k], x1 = q1[k + kBlock], y0 = q2[k], y1 = q2[k + kBlock];
+    a0 += (double)x0; a1 += (double)x1; b0 += (double)y0; b1 += (double)y1;
+  }
+  if (k < chunks) { a0 += (double)q1[k]; b0 += (double)q2[k]; }
+  double s1 = a0 + a1, s2 = b0 + b1;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off, 64);
+    s2 += __shfl_xor(s2, off, 64);
+  }
+  if (lane == 0) { red[0][wave] = s1; red[1][wave] = s2; }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  s1 = 0.0;
+  s2 = 0.0;
+#pragma unroll
+  for (int w = 0; w < kBlock / 64; ++w) { s1 += red[0][w]; s2 += red[1][w]; }
+  const double is = (double)invstd[c];
+  const double g = gamma ? (double)gamma[c] : 1.0;
+  if (dgamma) dgamma[c] = (float)(s2 * is);
+  if (dbeta) dbeta[c] = (float)s1;
+  const double a = g * is;
+  k1[c] = (float)a;
+  k2[c] = (float)(-a * is * is * s2 / (double)M);
+  k3[c] = (float)(-a * s1 / (double)M);
+}
+
+// BN+ReLU backward whose statistics (s1 = sum dz, s2 = sum dz*(x - mean), dz = dy * relu mask)
+// were summed by the dgrad epilogue of the conv that consumed this BN's output: [C][chunks]
+// partials -> finalize -> apply (mask recomputed from x and the forward coefficients).
+void launch_bn_bwd_from_partials(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* gamma,
+                                 const float* mean, const float* invstd, const float* coef, const float* p1,
+                                 const float* p2, int chunks, float* dgamma, float* dbeta, void* dx, float* kbuf,
+                                 hipStream_t s) {
+  BnGeometry g = bn_geometry(M, C);
+  float* k1 = kbuf;
+  float* k2 = k1 + C;
+  float* k3 = k2 + C;
+  dim3 bl(kBlock);
+  if (chunks > 256)
+    hipLaunchKernelGGL(bn_bwd_finalize_wide_kernel, dim3((unsigned)C), bl, 0, s, p1, p2, chunks, (int)C, M, gamma,
+                       invstd, dgamma, dbeta, k1, k2, k3);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p2, chunks, (int)C, M,
+                       gamma, invstd, dgamma, dbeta, k1, k2, k3);
+  dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
+  switch (dtype) {
+    case 0: hipLaunchKernelGGL((bn_bwd_apply_kernel<F32, true, false, true>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
+    case 1: hipLaunchKernelGGL((bn_bwd_apply_kernel<BF16, true, false, true>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
+    default: hipLaunchKernelGGL((bn_bwd_apply_kernel<F16, true, false, true>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
+  }
+}
+
 int64_t bn_workspace_floats(int64_t M, int64_t C) {
   BnGeometry g = bn_geometry(M, C);
   return 2 * (int64_t)C * g.chunks + 3 * C;

@@ -63,6 +63,12 @@ struct ConvFwdArgs {
   int64_t M;
   int m_tiles, n_tiles;  // m_tiles: 128-row tiles (the BN-partials layout)
   int mt256;             // 256-row tiles when BM = 256
+  // BNB epilogue: the BatchNorm whose ReLU output was this conv's input
+  const uint16_t* bnx;   // BN input x [M, Cout] (same layout as y)
+  const float* bn_mean;  // [Cout]
+  const float* bn_coef;  // [2*Cout] = [a | b]
+  float* bp1;            // partials [Cout][m_tiles]
+  float* bp2;
 };
 
 // K-major operands (rows of the LDS image = k) use the transposing reads and the swizzle of
@@ -84,7 +90,11 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 // as K-major rows and taken with transposing LDS reads.
 // BMT: block rows (128, or 256 = 4 MFMA row tiles per wave for more reuse per LDS byte).
 // STATS: emit the BN partial sums (compiled out otherwise).
-template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true>
+// BNB (backward-data of a conv whose input is relu(bn(x)), LDS epilogue only): while storing
+// the input gradient dz, also sum that BatchNorm's backward statistics s1 = sum dz*mask,
+// s2 = sum dz*mask*(x - mean) with mask = fma(x, a, b) > 0 recomputed from the BN input x and
+// the forward coefficients - the BN backward then skips its statistics pass (ops/conv.py).
+template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false>
 __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
   constexpr int BM = BMT;
@@ -315,6 +325,18 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
     constexpr int CPR = BN / 8;          // 16-byte chunks per output row
     constexpr int RPP = kThreads / CPR;  // rows per pass
     const int oc = tid % CPR, orow = tid / CPR;
+    float ba[8], bb[8], bm[8], s1[8], s2[8];
+    if (BNB) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = n0 + oc * 8 + k;
+        ba[k] = p.bn_coef[c];
+        bb[k] = p.bn_coef[p.Cout + c];
+        bm[k] = p.bn_mean[c];
+        s1[k] = 0.f;
+        s2[k] = 0.f;
+      }
+    }
 #pragma unroll
     for (int r0 = 0; r0 < BM; r0 += RPP) {
       const int row = r0 + orow;
@@ -322,6 +344,48 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
       if (m < p.M) {
         const uint4 v = *reinterpret_cast<const uint4*>(lds + row * C_STRIDE + oc * 16);
         *reinterpret_cast<uint4*>(p.y + m * p.Cout + n0 + oc * 8) = v;
+        if (BNB) {
+          const uint4 xv = *reinterpret_cast<const uint4*>(p.bnx + m * p.Cout + n0 + oc * 8);
+          const uint32_t gu[4] = {v.x, v.y, v.z, v.w}, xu[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t gw = gu[k >> 1], xw = xu[k >> 1];
+            const float g = __uint_as_float((k & 1) ? (gw & 0xffff0000u) : (gw << 16));
+            const float x = __uint_as_float((k & 1) ? (xw & 0xffff0000u) : (xw << 16));
+            const float dz = __builtin_fmaf(x, ba[k], bb[k]) > 0.0f ? g : 0.0f;
+            s1[k] += dz;
+            s2[k] = __builtin_fmaf(dz, x - bm[k], s2[k]);
+          }
+        }
+      }
+    }
+    if (BNB) {
+      // threads sharing a channel group: orow = tid / CPR -> lanes l, l+CPR, ... of a wave, then
+      // the 4 waves through LDS (the epilogue image is no longer read: reuse its space)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+#pragma unroll
+        for (int off = CPR; off < 64; off <<= 1) {
+          s1[k] += __shfl_xor(s1[k], off, 64);
+          s2[k] += __shfl_xor(s2[k], off, 64);
+        }
+      }
+      __syncthreads();
+      float* bred = reinterpret_cast<float*>(lds);  // [4 waves][2][BN]
+      if (lane < CPR) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          bred[(wid * 2) * BN + oc * 8 + k] = s1[k];
+          bred[(wid * 2 + 1) * BN + oc * 8 + k] = s2[k];
+        }
+      }
+      __syncthreads();
+      if (tid < BN) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) { a += bred[(w * 2) * BN + tid]; b += bred[(w * 2 + 1) * BN + tid]; }
+        p.bp1[(int64_t)(n0 + tid) * p.m_tiles + mt] = a;
+        p.bp2[(int64_t)(n0 + tid) * p.m_tiles + mt] = b;
       }
     }
   }
@@ -949,6 +1013,33 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
   a.mt256 = 0;
   if (wide) conv_fwd_dispatch<128>(conv_variant(), bkn, a, s);
   else conv_fwd_dispatch<64>(conv_variant(), bkn, a, s);
+}
+
+// Stride-1 backward-data through a flipped/transposed weight wt [C][R][S][Cout] (the forward
+// kernel on dy), whose epilogue also sums the backward statistics of the BatchNorm+ReLU that
+// produced the conv's input (BNB epilogue).  bnx/dx: [N, Ho, Wo, C].
+void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int Ho, int Wo, int Cout,
+                               int C, int R, int S, int pad, const uint16_t* bnx, const float* bn_mean,
+                               const float* bn_coef, float* bp1, float* bp2, hipStream_t s) {
+  ConvFwdArgs a;
+  a.x = dy; a.w = wt; a.y = dx; a.psum = nullptr; a.psq = nullptr;
+  a.N = N; a.H = Ho; a.W = Wo; a.C = Cout; a.Cout = C; a.R = R; a.S = S; a.stride = 1; a.pad = R - 1 - pad;
+  a.Ho = Ho + 2 * a.pad - R + 1;
+  a.Wo = Wo + 2 * a.pad - S + 1;
+  a.M = (int64_t)N * a.Ho * a.Wo;
+  a.m_tiles = conv_m_tiles(a.M);
+  a.mt256 = 0;
+  a.bnx = bnx; a.bn_mean = bn_mean; a.bn_coef = bn_coef; a.bp1 = bp1; a.bp2 = bp2;
+  const dim3 block(conv::kThreads);
+  if (C % 128 == 0) {
+    a.n_tiles = C / 128;
+    hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, false, false, true>), dim3((unsigned)(a.m_tiles * a.n_tiles)),
+                       block, 0, s, a);
+  } else {
+    a.n_tiles = C / 64;
+    hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, true, false, false, true>), dim3((unsigned)(a.m_tiles * a.n_tiles)),
+                       block, 0, s, a);
+  }
 }
 
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,

@@ -61,6 +61,10 @@ void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void
                                  const float* beta, float eps, float momentum, float* run_mean, float* run_var,
                                  int64_t* num_batches, float* save_mean, float* save_invstd, float* save_coef,
                                  bool relu, hipStream_t s);
+void launch_bn_bwd_from_partials(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* gamma,
+                                 const float* mean, const float* invstd, const float* coef, const float* p1,
+                                 const float* p2, int chunks, float* dgamma, float* dbeta, void* dx, float* kbuf,
+                                 hipStream_t s);
 void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                      const float* coef_a, const float* coef_b, bool relu, hipStream_t s);
 void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, const void* x, int64_t M,
@@ -132,6 +136,11 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void* dw, int dw_kind, int N, int H,
                        int W, int C, int Cout, int R, int S, int stride, int pad, const ConvWgradPlan& plan,
                        hipStream_t s);
+// stride-1 backward-data (flipped weight wt [C,R,S,Cout]) + the backward statistics of the
+// BatchNorm+ReLU (input bnx, mean, coef [a|b]) that produced the conv's input: bp1/bp2 [C][m_tiles]
+void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int Ho, int Wo, int Cout,
+                               int C, int R, int S, int pad, const uint16_t* bnx, const float* bn_mean,
+                               const float* bn_coef, float* bp1, float* bp2, hipStream_t s);
 // stride-1 backward-data straight from the KRSC weight w [Cout,R,S,C]: dy [N,Ho,Wo,Cout] -> dx [N,Ho,Wo,C]
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout, int C,
                        int R, int S, int pad, hipStream_t s);

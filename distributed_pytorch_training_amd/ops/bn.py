@@ -20,6 +20,7 @@ from typing import Optional
 import torch
 
 from . import native, native_available
+from .conv import take_bnb_partials
 
 
 def _cl(t: torch.Tensor) -> torch.Tensor:
@@ -71,6 +72,9 @@ def _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches,
     mask_from_x = ctx.relu and not ctx.has_res and not pair   # pair outputs always write dz
     ctx.save_for_backward(x, y if (relu and not mask_from_x) else None, weight, mean, invstd,
                           coef if mask_from_x else None)
+    if mask_from_x:
+        # a native conv consuming y sums this BN's backward statistics in its dgrad epilogue
+        y._dpt_bn_src = (x, mean, coef)
     return y
 
 
@@ -82,6 +86,12 @@ def _bwd(ctx, dy, dy2):
         return (None, None, None, None)
     want_params = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
     want_dz = ctx.has_res and ctx.needs_input_grad[1]
+    if coef is not None and dy2 is None:
+        part = take_bnb_partials(dy)
+        if part is not None:  # statistics already summed by the consuming conv's dgrad epilogue
+            dx, dg, db = native().bn_bwd_partials(dy, x, weight, mean, invstd, coef, part[0], part[1],
+                                                  bool(want_params))
+            return (dx, None, dg if want_params else None, db if want_params else None)
     dx, dg, db, dz = native().bn_bwd(_cl(dy), None if dy2 is None else _cl(dy2), y, x, weight, mean, invstd,
                                      ctx.relu, bool(want_dz), bool(want_params), coef)
     return (dx, dz if want_dz else None, dg if want_params else None, db if want_params else None)

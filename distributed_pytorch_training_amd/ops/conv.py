@@ -23,6 +23,12 @@ from . import native, native_available
 
 _CL = torch.channels_last
 ENABLED = os.environ.get("DPT_NATIVE_CONV", "1") != "0"
+# Backward-data of a conv fed by a fused BN+ReLU also sums that BN's backward statistics in its
+# epilogue (the BN backward then skips its statistics pass).
+BN_BWD_FUSE = os.environ.get("DPT_BN_BWD_FUSE", "1") != "0"
+# dx.data_ptr() -> (p1, p2, shape): handed from a conv's backward to the BN backward that
+# receives dx as its output gradient (ops/bn.py), consumed once
+_BNB_PARTIALS = {}
 # The im2col stem path is correct but measured slower than MIOpen on ResNet-50's 7x7/2 stem at
 # batch 256 (the [3.2M x 192] bf16 patch matrix is 1.2 GB written and read twice): opt-in only.
 STEM_ENABLED = os.environ.get("DPT_NATIVE_STEM", "0") == "1"
@@ -49,7 +55,11 @@ def _backward(ctx, dy):
     s, p = ctx.stride, ctx.pad
     dx = dw = None
     if ctx.needs_input_grad[0]:
-        if s == 1:
+        if s == 1 and ctx.bn_src is not None and BN_BWD_FUSE:
+            bn_x, bn_mean, bn_coef = ctx.bn_src
+            dx, p1, p2 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, bn_coef)
+            _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape))
+        elif s == 1:
             dx = native().conv_dgrad_flip(dy, w, p)[0]
         else:
             dx = torch.ops.aten.convolution_backward(dy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
@@ -61,30 +71,30 @@ def _backward(ctx, dy):
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride: int, pad: int, out_hw):
+    def forward(ctx, x, w, stride: int, pad: int, out_hw, bn_src):
         y = native().conv_fwd(x, w, stride, pad, False, *out_hw)[0]
         ctx.save_for_backward(x, w)
-        ctx.stride, ctx.pad = stride, pad
+        ctx.stride, ctx.pad, ctx.bn_src = stride, pad, bn_src
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        return _backward(ctx, dy) + (None, None, None)
+        return _backward(ctx, dy) + (None, None, None, None)
 
 
 class _ConvStats(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride: int, pad: int, out_hw):
+    def forward(ctx, x, w, stride: int, pad: int, out_hw, bn_src):
         y, ps, pq = native().conv_fwd(x, w, stride, pad, True, *out_hw)
         ctx.save_for_backward(x, w)
-        ctx.stride, ctx.pad = stride, pad
+        ctx.stride, ctx.pad, ctx.bn_src = stride, pad, bn_src
         ctx.mark_non_differentiable(ps, pq)
         ctx.set_materialize_grads(False)  # no zero-filled gradients for the statistics outputs
         return y, ps, pq
 
     @staticmethod
     def backward(ctx, dy, _dps, _dpq):
-        return _backward(ctx, dy) + (None, None, None)
+        return _backward(ctx, dy) + (None, None, None, None)
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bool = False,
@@ -93,11 +103,23 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bo
     BatchNorm partial sums as ``y._dpt_bn_partials`` (consumed by ops/bn.py).  ``out_hw``:
     explicit output size (asymmetric padding: top/left ``pad``, bottom/right what fits)."""
     w = _cl(w)
+    # (BN input, mean, coef) of the fused BN+ReLU that produced x, if any (ops/bn.py)
+    bn_src = x.__dict__.get("_dpt_bn_src")
     if not bn_stats:
-        return _Conv.apply(x, w, int(stride), int(pad), tuple(out_hw))
-    y, ps, pq = _ConvStats.apply(x, w, int(stride), int(pad), tuple(out_hw))
+        return _Conv.apply(x, w, int(stride), int(pad), tuple(out_hw), bn_src)
+    y, ps, pq = _ConvStats.apply(x, w, int(stride), int(pad), tuple(out_hw), bn_src)
     y._dpt_bn_partials = (ps, pq)
     return y
+
+
+def take_bnb_partials(dy: torch.Tensor):
+    """(p1, p2) the backward of the conv that consumed a BN output summed for ``dy``, once."""
+    if not _BNB_PARTIALS:
+        return None
+    ent = _BNB_PARTIALS.pop(dy.data_ptr(), None)
+    if ent is None or ent[2] != tuple(dy.shape):
+        return None
+    return ent[0], ent[1]
 
 
 def take_bn_partials(x: torch.Tensor):

@@ -210,3 +210,36 @@ def test_s2d_stem_matches_fp32(cuda, xdtype, hw):
     y.backward(gy)
     wref = torch.nn.grad.conv2d_weight(xr, w.shape, gy.float(), stride=2, padding=3)
     torch.testing.assert_close(w.grad.float(), wref, rtol=2e-2, atol=2e-2 * wref.abs().max().item())
+
+
+@pytest.mark.parametrize("k2", [1, 3])
+def test_bn_backward_stats_from_dgrad_epilogue(cuda, k2):
+    """conv -> fused BN+ReLU -> conv: the second conv's backward-data epilogue sums the BN's
+    backward statistics; gradients must equal the unfused path's (same math, other order)."""
+    from distributed_pytorch_training_amd.ops import bn as fbn
+    from distributed_pytorch_training_amd.ops import conv as nc
+
+    g = torch.Generator(device=cuda).manual_seed(21)
+    x = torch.randn(4, 64, 14, 14, device=cuda, generator=g).to(torch.bfloat16).contiguous(memory_format=CL)
+    w1 = (torch.randn(128, 64, 1, 1, device=cuda, generator=g) * 0.1).to(torch.bfloat16).contiguous(memory_format=CL)
+    w2 = (torch.randn(128, 128, k2, k2, device=cuda, generator=g) * 0.05).to(torch.bfloat16)
+    w2 = w2.contiguous(memory_format=CL)
+    gamma = torch.rand(128, device=cuda, generator=g) + 0.5
+    beta = torch.randn(128, device=cuda, generator=g) * 0.1
+    gy = torch.randn(4, 128, 14, 14, device=cuda, generator=g).to(torch.bfloat16).contiguous(memory_format=CL)
+    grads = []
+    for fuse in (True, False):
+        nc.BN_BWD_FUSE = fuse
+        ps = [t.detach().clone().requires_grad_(True) for t in (w1, w2, gamma, beta)]
+        xi = x.detach().clone().requires_grad_(True)
+        rm, rv = torch.zeros(128, device=cuda), torch.ones(128, device=cuda)
+        nb = torch.zeros((), dtype=torch.long, device=cuda)
+        h = nc.conv2d(xi, ps[0], 1, 0, bn_stats=True)
+        z = fbn.bn_act_train(h, None, ps[2], ps[3], rm, rv, nb, 0.1, 1e-5, True)
+        y = nc.conv2d(z, ps[1], 1, k2 // 2)
+        y.backward(gy)
+        grads.append([xi.grad.float()] + [p.grad.float() for p in ps])
+    nc.BN_BWD_FUSE = True
+    assert not nc._BNB_PARTIALS  # every handed-over partial was consumed
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item() + 1e-6)
