@@ -274,7 +274,11 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t pad) {
 // Stride-1 backward-data whose epilogue also sums the backward statistics of the BatchNorm+ReLU
 // that produced the conv's input (bn_x: that BN's input, same shape as dx; coef = [a | b]).
 // Returns {dx, p1, p2} with p1/p2 [C, m_tiles] for bn_bwd_partials.
-std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor bn_x, Tensor bn_mean, Tensor bn_coef) {
+// With bn_y / bn_res (block-tail BN+add+ReLU whose output also fed the identity path): dx is
+// the tail's whole masked gradient (dx + bn_res) * (bn_y > 0) and p1/p2 are summed from it.
+std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor bn_x, Tensor bn_mean,
+                                       c10::optional<Tensor> bn_coef,
+                                       c10::optional<Tensor> bn_y, c10::optional<Tensor> bn_res) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
   check_cl_bf16(bn_x, "bn_x");
@@ -285,6 +289,15 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
   const int H = Ho + R - 1 - 2 * (int)pad, W = Wo + S - 1 - 2 * (int)pad;
   TORCH_CHECK(bn_x.size(0) == N && bn_x.size(1) == C && bn_x.size(2) == H && bn_x.size(3) == W,
               "conv_dgrad_bnstats: bn_x must match the conv input");
+  const bool res = bn_y.has_value() && bn_y->defined();
+  TORCH_CHECK(res == (bn_res.has_value() && bn_res->defined()), "conv_dgrad_bnstats: bn_y and bn_res go together");
+  TORCH_CHECK(res || (bn_coef.has_value() && bn_coef->defined()), "conv_dgrad_bnstats: bn_coef needed without bn_y");
+  if (res) {
+    check_cl_bf16(*bn_y, "bn_y");
+    check_cl_bf16(*bn_res, "bn_res");
+    TORCH_CHECK(bn_y->sizes() == bn_x.sizes() && bn_res->sizes() == bn_x.sizes(),
+                "conv_dgrad_bnstats: bn_y / bn_res must match bn_x");
+  }
   auto wt = at::empty({C, Cout, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int mt = dpt::conv_m_tiles((int64_t)N * H * W);
@@ -298,7 +311,9 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
                                  reinterpret_cast<const uint16_t*>(wt.data_ptr()), reinterpret_cast<uint16_t*>(dx.data_ptr()),
                                  N, Ho, Wo, Cout, C, R, S, (int)pad, reinterpret_cast<const uint16_t*>(bn_x.data_ptr()),
                                  f32_param(bn_mean, C, "bn_mean"), f32_param(bn_coef, 2 * C, "bn_coef"),
-                                 p1.data_ptr<float>(), p2.data_ptr<float>(), st);
+                                 p1.data_ptr<float>(), p2.data_ptr<float>(), st,
+                                 res ? reinterpret_cast<const uint16_t*>(bn_y->data_ptr()) : nullptr,
+                                 res ? reinterpret_cast<const uint16_t*>(bn_res->data_ptr()) : nullptr);
   return {dx, p1, p2};
 }
 
@@ -524,13 +539,14 @@ std::vector<Tensor> bn_bwd(Tensor dy, c10::optional<Tensor> dy2, c10::optional<T
 // BN+ReLU backward from statistics partials summed by the consuming conv's dgrad epilogue:
 // {dx, dgamma, dbeta}; the ReLU mask is recomputed from x and coef.
 std::vector<Tensor> bn_bwd_partials(Tensor dy, Tensor x, c10::optional<Tensor> weight, Tensor mean, Tensor invstd,
-                                    Tensor coef, Tensor p1, Tensor p2, bool want_dparams) {
+                                    c10::optional<Tensor> coef, Tensor p1, Tensor p2, bool want_dparams, bool from_dz) {
   auto [M, C] = bn_rows(x, "x");
   auto [Md, Cd] = bn_rows(dy, "grad_output");
   TORCH_CHECK(M == Md && C == Cd && dy.scalar_type() == x.scalar_type(), "grad_output mismatch");
   TORCH_CHECK(p1.is_cuda() && p1.scalar_type() == at::kFloat && p1.dim() == 2 && p1.size(0) == C &&
                   p1.is_contiguous() && p2.sizes() == p1.sizes() && p2.is_contiguous(),
               "bn_bwd_partials: partials must be contiguous fp32 [C, chunks]");
+  TORCH_CHECK(from_dz || (coef.has_value() && coef->defined()), "bn_bwd_partials: coef needed unless from_dz");
   auto fopt = x.options().dtype(at::kFloat);
   auto dx = at::empty_like(x);
   Tensor dg = want_dparams ? at::empty({C}, fopt) : Tensor();
@@ -542,7 +558,7 @@ std::vector<Tensor> bn_bwd_partials(Tensor dy, Tensor x, c10::optional<Tensor> w
                                    f32_param(coef, 2 * C, "coef"), p1.data_ptr<float>(), p2.data_ptr<float>(),
                                    (int)p1.size(1), want_dparams ? dg.data_ptr<float>() : nullptr,
                                    want_dparams ? db.data_ptr<float>() : nullptr, dx.data_ptr(), kbuf.data_ptr<float>(),
-                                   cur_stream(x));
+                                   cur_stream(x), from_dz);
   return {dx, dg, db};
 }
 
@@ -812,9 +828,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_set_variant", &dpt::conv_set_variant, py::arg("variant"));
   m.def("conv_dgrad", &conv_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("conv_dgrad_bnstats", &conv_dgrad_bnstats, py::arg("grad_output"), py::arg("w"), py::arg("pad"),
-        py::arg("bn_x"), py::arg("bn_mean"), py::arg("bn_coef"));
+        py::arg("bn_x"), py::arg("bn_mean"), py::arg("bn_coef"), py::arg("bn_y") = py::none(),
+        py::arg("bn_res") = py::none());
   m.def("bn_bwd_partials", &bn_bwd_partials, py::arg("grad_output"), py::arg("x"), py::arg("weight"), py::arg("mean"),
-        py::arg("invstd"), py::arg("coef"), py::arg("p1"), py::arg("p2"), py::arg("want_dparams"));
+        py::arg("invstd"), py::arg("coef"), py::arg("p1"), py::arg("p2"), py::arg("want_dparams"),
+        py::arg("from_dz") = false);
   m.def("conv_dgrad_flip", &conv_dgrad_flip, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
 

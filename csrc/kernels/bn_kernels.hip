@@ -694,7 +694,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_wide_kernel(
 void launch_bn_bwd_from_partials(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* gamma,
                                  const float* mean, const float* invstd, const float* coef, const float* p1,
                                  const float* p2, int chunks, float* dgamma, float* dbeta, void* dx, float* kbuf,
-                                 hipStream_t s) {
+                                 hipStream_t s, bool from_dz) {
   BnGeometry g = bn_geometry(M, C);
   float* k1 = kbuf;
   float* k2 = k1 + C;
@@ -707,6 +707,14 @@ void launch_bn_bwd_from_partials(int dtype, const void* dy, const void* x, int64
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p2, chunks, (int)C, M,
                        gamma, invstd, dgamma, dbeta, k1, k2, k3);
   dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
+  if (from_dz) {  // dy is already the masked gradient dz (block-tail BN, ops/conv.py BNR)
+    switch (dtype) {
+      case 0: hipLaunchKernelGGL((bn_bwd_apply_kernel<F32, false, true, false>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
+      case 1: hipLaunchKernelGGL((bn_bwd_apply_kernel<BF16, false, true, false>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
+      default: hipLaunchKernelGGL((bn_bwd_apply_kernel<F16, false, true, false>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
+    }
+    return;
+  }
   switch (dtype) {
     case 0: hipLaunchKernelGGL((bn_bwd_apply_kernel<F32, true, false, true>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
     case 1: hipLaunchKernelGGL((bn_bwd_apply_kernel<BF16, true, false, true>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;

@@ -69,6 +69,10 @@ struct ConvFwdArgs {
   const float* bn_coef;  // [2*Cout] = [a | b]
   float* bp1;            // partials [Cout][m_tiles]
   float* bp2;
+  // BNR epilogue: that BatchNorm was a block tail relu(bn(x) + res) whose output also fed the
+  // next block's identity path
+  const uint16_t* bny;    // its output y (ReLU mask)
+  const uint16_t* bnres;  // the identity-path gradient (added before the mask)
 };
 
 // K-major operands (rows of the LDS image = k) use the transposing reads and the swizzle of
@@ -94,7 +98,13 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 // the input gradient dz, also sum that BatchNorm's backward statistics s1 = sum dz*mask,
 // s2 = sum dz*mask*(x - mean) with mask = fma(x, a, b) > 0 recomputed from the BN input x and
 // the forward coefficients - the BN backward then skips its statistics pass (ops/conv.py).
-template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false>
+// BNR (with BNB): the BatchNorm was a residual-block tail y = relu(bn(x) + res) whose output
+// fed this conv AND the next block's identity path: the stored gradient is the block tail's
+// whole masked gradient dz = (g + g_identity) * (y > 0) - the tail's residual-path gradient
+// and the input of its backward apply - and s1/s2 are summed from it.  Replaces the
+// tail's backward-statistics pass (4 reads + 1 write of a 4C-channel tensor) by 3 reads here.
+template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
+          bool BNR = false>
 __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
   constexpr int BM = BMT;
@@ -324,38 +334,79 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
   if (LDSEPI) {
     constexpr int CPR = BN / 8;          // 16-byte chunks per output row
     constexpr int RPP = kThreads / CPR;  // rows per pass
+    constexpr int NPASS = BM / RPP;
+    // global operands of the BN epilogues are loaded a group of passes at a time, before any
+    // store of the group (the output may alias nothing, but the compiler cannot know that)
+    constexpr int GRP = NPASS < 4 ? NPASS : 4;
     const int oc = tid % CPR, orow = tid / CPR;
     float ba[8], bb[8], bm[8], s1[8], s2[8];
     if (BNB) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int c = n0 + oc * 8 + k;
-        ba[k] = p.bn_coef[c];
-        bb[k] = p.bn_coef[p.Cout + c];
+        ba[k] = BNR ? 0.f : p.bn_coef[c];
+        bb[k] = BNR ? 0.f : p.bn_coef[p.Cout + c];
         bm[k] = p.bn_mean[c];
         s1[k] = 0.f;
         s2[k] = 0.f;
       }
     }
 #pragma unroll
-    for (int r0 = 0; r0 < BM; r0 += RPP) {
-      const int row = r0 + orow;
-      const int64_t m = m0 + row;
-      if (m < p.M) {
-        const uint4 v = *reinterpret_cast<const uint4*>(lds + row * C_STRIDE + oc * 16);
-        *reinterpret_cast<uint4*>(p.y + m * p.Cout + n0 + oc * 8) = v;
-        if (BNB) {
-          const uint4 xv = *reinterpret_cast<const uint4*>(p.bnx + m * p.Cout + n0 + oc * 8);
-          const uint32_t gu[4] = {v.x, v.y, v.z, v.w}, xu[4] = {xv.x, xv.y, xv.z, xv.w};
+    for (int g0 = 0; g0 < NPASS; g0 += GRP) {
+      uint4 xv[GRP], yv[GRP], rv[GRP];
+      if (BNB) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const uint32_t gw = gu[k >> 1], xw = xu[k >> 1];
-            const float g = __uint_as_float((k & 1) ? (gw & 0xffff0000u) : (gw << 16));
-            const float x = __uint_as_float((k & 1) ? (xw & 0xffff0000u) : (xw << 16));
-            const float dz = __builtin_fmaf(x, ba[k], bb[k]) > 0.0f ? g : 0.0f;
-            s1[k] += dz;
-            s2[k] = __builtin_fmaf(dz, x - bm[k], s2[k]);
+        for (int q = 0; q < GRP; ++q) {
+          const int64_t m = m0 + (g0 + q) * RPP + orow;
+          const int64_t off = (m < p.M ? m : 0) * p.Cout + n0 + oc * 8;
+          xv[q] = *reinterpret_cast<const uint4*>(p.bnx + off);
+          if (BNR) {
+            yv[q] = *reinterpret_cast<const uint4*>(p.bny + off);
+            rv[q] = *reinterpret_cast<const uint4*>(p.bnres + off);
           }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < GRP; ++q) {
+        const int row = (g0 + q) * RPP + orow;
+        const int64_t m = m0 + row;
+        if (m < p.M) {
+          uint4 v = *reinterpret_cast<const uint4*>(lds + row * C_STRIDE + oc * 16);
+          if (BNB) {
+            const uint32_t gu[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t xu[4] = {xv[q].x, xv[q].y, xv[q].z, xv[q].w};
+            const uint32_t yu[4] = {yv[q].x, yv[q].y, yv[q].z, yv[q].w};
+            const uint32_t ru[4] = {rv[q].x, rv[q].y, rv[q].z, rv[q].w};
+            uint32_t du[4];
+#pragma unroll
+            for (int k2 = 0; k2 < 4; ++k2) {
+              float dzp[2];
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const int k = 2 * k2 + h;
+                const uint32_t sh = h ? 0u : 16u;
+                const float g = __uint_as_float((gu[k2] << sh) & 0xffff0000u);
+                const float x = __uint_as_float((xu[k2] << sh) & 0xffff0000u);
+                float dz;
+                if (BNR) {
+                  const float yy = __uint_as_float((yu[k2] << sh) & 0xffff0000u);
+                  const float rr = __uint_as_float((ru[k2] << sh) & 0xffff0000u);
+                  dz = yy > 0.0f ? g + rr : 0.0f;
+                } else {
+                  dz = __builtin_fmaf(x, ba[k], bb[k]) > 0.0f ? g : 0.0f;
+                }
+                dzp[h] = dz;
+                s1[k] += dz;
+                s2[k] = __builtin_fmaf(dz, x - bm[k], s2[k]);
+              }
+              if (BNR) {
+                const f32x2_t d2 = {dzp[0], dzp[1]};
+                du[k2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(d2, bf16x2_t));
+              }
+            }
+            if (BNR) v = make_uint4(du[0], du[1], du[2], du[3]);
+          }
+          *reinterpret_cast<uint4*>(p.y + m * p.Cout + n0 + oc * 8) = v;
         }
       }
     }
@@ -1020,7 +1071,8 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
 // produced the conv's input (BNB epilogue).  bnx/dx: [N, Ho, Wo, C].
 void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int Ho, int Wo, int Cout,
                                int C, int R, int S, int pad, const uint16_t* bnx, const float* bn_mean,
-                               const float* bn_coef, float* bp1, float* bp2, hipStream_t s) {
+                               const float* bn_coef, float* bp1, float* bp2, hipStream_t s,
+                               const uint16_t* bny, const uint16_t* bnres) {
   ConvFwdArgs a;
   a.x = dy; a.w = wt; a.y = dx; a.psum = nullptr; a.psq = nullptr;
   a.N = N; a.H = Ho; a.W = Wo; a.C = Cout; a.Cout = C; a.R = R; a.S = S; a.stride = 1; a.pad = R - 1 - pad;
@@ -1030,15 +1082,17 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
   a.m_tiles = conv_m_tiles(a.M);
   a.mt256 = 0;
   a.bnx = bnx; a.bn_mean = bn_mean; a.bn_coef = bn_coef; a.bp1 = bp1; a.bp2 = bp2;
+  a.bny = bny; a.bnres = bnres;
+  const bool res = bny != nullptr;
   const dim3 block(conv::kThreads);
+  a.n_tiles = C % 128 == 0 ? C / 128 : C / 64;
+  const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
   if (C % 128 == 0) {
-    a.n_tiles = C / 128;
-    hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, false, false, true>), dim3((unsigned)(a.m_tiles * a.n_tiles)),
-                       block, 0, s, a);
+    if (res) hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, false, false, true, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, false, false, true>), grid, block, 0, s, a);
   } else {
-    a.n_tiles = C / 64;
-    hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, true, false, false, true>), dim3((unsigned)(a.m_tiles * a.n_tiles)),
-                       block, 0, s, a);
+    if (res) hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, true, false, false, true, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, true, false, false, true>), grid, block, 0, s, a);
   }
 }
 

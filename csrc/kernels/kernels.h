@@ -64,7 +64,7 @@ void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void
 void launch_bn_bwd_from_partials(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* gamma,
                                  const float* mean, const float* invstd, const float* coef, const float* p1,
                                  const float* p2, int chunks, float* dgamma, float* dbeta, void* dx, float* kbuf,
-                                 hipStream_t s);
+                                 hipStream_t s, bool from_dz = false);
 void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                      const float* coef_a, const float* coef_b, bool relu, hipStream_t s);
 void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, const void* x, int64_t M,
@@ -140,7 +140,8 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
 // BatchNorm+ReLU (input bnx, mean, coef [a|b]) that produced the conv's input: bp1/bp2 [C][m_tiles]
 void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int Ho, int Wo, int Cout,
                                int C, int R, int S, int pad, const uint16_t* bnx, const float* bn_mean,
-                               const float* bn_coef, float* bp1, float* bp2, hipStream_t s);
+                               const float* bn_coef, float* bp1, float* bp2, hipStream_t s,
+                               const uint16_t* bny = nullptr, const uint16_t* bnres = nullptr);
 // stride-1 backward-data straight from the KRSC weight w [Cout,R,S,C]: dy [N,Ho,Wo,Cout] -> dx [N,Ho,Wo,C]
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout, int C,
                        int R, int S, int pad, hipStream_t s);

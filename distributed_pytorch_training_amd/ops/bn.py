@@ -19,8 +19,13 @@ from typing import Optional
 
 import torch
 
+import os
+
 from . import native, native_available
 from .conv import take_bnb_partials
+
+# Block-tail BN+add+ReLU backward statistics in the consuming conv's dgrad epilogue (see _bwd)
+BNR_FUSE = os.environ.get("DPT_BNR_FUSE", "1") != "0"
 
 
 def _cl(t: torch.Tensor) -> torch.Tensor:
@@ -32,14 +37,14 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
 class _BNActTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
-                partials):
+                partials, links):
         y = _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
-                 partials=partials)
+                 partials=partials, links=links)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        return _bwd(ctx, dy, None) + (None,) * 7
+        return _bwd(ctx, dy, None) + (None,) * 8
 
 
 class _BNActTrainPair(torch.autograd.Function):
@@ -51,19 +56,19 @@ class _BNActTrainPair(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
-                partials):
+                partials, links):
         y = _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
-                 pair=True, partials=partials)
+                 pair=True, partials=partials, links=links)
         ctx.set_materialize_grads(False)  # an unused alias (last block) gives None, not zeros
         return y, y.view_as(y)
 
     @staticmethod
     def backward(ctx, dy, dy2):
-        return _bwd(ctx, dy, dy2) + (None,) * 7
+        return _bwd(ctx, dy, dy2) + (None,) * 8
 
 
 def _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
-         pair=False, partials=None):
+         pair=False, partials=None, links=(None, None)):
     ps, pq = partials if partials is not None else (None, None)
     y, mean, invstd, coef = native().bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
                                                   num_batches, float(momentum), float(eps), bool(relu), ps, pq)
@@ -75,6 +80,12 @@ def _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches,
     if mask_from_x:
         # a native conv consuming y sums this BN's backward statistics in its dgrad epilogue
         y._dpt_bn_src = (x, mean, coef)
+    own_slot, res_slot = links
+    ctx.res_slot = res_slot  # our residual input is the identity alias of an earlier block tail
+    if own_slot is not None:
+        # block tail: the conv consuming y sums the statistics (and folds in the identity-path
+        # gradient the next block's tail leaves in own_slot, see _bwd) in its dgrad epilogue
+        y._dpt_bn_src = (x, mean, own_slot)
     return y
 
 
@@ -92,8 +103,23 @@ def _bwd(ctx, dy, dy2):
             dx, dg, db = native().bn_bwd_partials(dy, x, weight, mean, invstd, coef, part[0], part[1],
                                                   bool(want_params))
             return (dx, None, dg if want_params else None, db if want_params else None)
+    if dy2 is not None and ctx.relu and ctx.has_res:
+        part = take_bnb_partials(dy)
+        if part is not None:
+            # the consuming conv's dgrad epilogue already formed dz = (dy + dy2) * (y > 0) in dy's
+            # storage and summed its statistics (ops/conv.py); dz is also the residual gradient
+            if part[2] != dy2.data_ptr():
+                raise RuntimeError("fused block-tail backward: the identity-path gradient folded into the "
+                                   "conv's dgrad is not the one autograd delivered (alias used twice?)")
+            dx, dg, db = native().bn_bwd_partials(dy, x, weight, mean, invstd, None, part[0], part[1],
+                                                  bool(want_params), True)
+            if ctx.res_slot is not None:
+                ctx.res_slot["dres"] = dy
+            return (dx, dy if want_dz else None, dg if want_params else None, db if want_params else None)
     dx, dg, db, dz = native().bn_bwd(_cl(dy), None if dy2 is None else _cl(dy2), y, x, weight, mean, invstd,
                                      ctx.relu, bool(want_dz), bool(want_params), coef)
+    if want_dz and ctx.res_slot is not None:
+        ctx.res_slot["dres"] = dz  # picked up by the dgrad of the conv that consumed that alias
     return (dx, dz if want_dz else None, dg if want_params else None, db if want_params else None)
 
 
@@ -106,13 +132,23 @@ def bn_act_supported(x: torch.Tensor, num_features: int) -> bool:
 
 def bn_act_train(x: torch.Tensor, residual: Optional[torch.Tensor], weight, bias, running_mean, running_var,
                  num_batches, momentum: float, eps: float, relu: bool, pair: bool = False):
+    res_slot = None
     if residual is not None:
+        if residual.dtype == x.dtype and residual.is_contiguous(memory_format=torch.channels_last):
+            # the identity alias of an earlier fused block tail (see below)
+            res_slot = residual.__dict__.get("_dpt_res_slot")
         residual = _cl(residual.to(x.dtype))
     # statistics already summed by the producing native conv's epilogue (ops/conv.py)
     partials = x.__dict__.pop("_dpt_bn_partials", None)
+    # block tails: own_slot receives the identity-path gradient from the next block's tail
+    # backward (which runs before the backward of the conv consuming our conv-path output)
+    own_slot = {} if (pair and relu and residual is not None and BNR_FUSE and x.dtype == torch.bfloat16) else None
     fn = _BNActTrainPair if pair else _BNActTrain
-    return fn.apply(x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
-                    partials)
+    out = fn.apply(x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
+                   partials, (own_slot, res_slot))
+    if own_slot is not None:
+        out[1]._dpt_res_slot = own_slot
+    return out
 
 
 @torch.no_grad()

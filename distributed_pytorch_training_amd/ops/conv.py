@@ -26,8 +26,8 @@ ENABLED = os.environ.get("DPT_NATIVE_CONV", "1") != "0"
 # Backward-data of a conv fed by a fused BN+ReLU also sums that BN's backward statistics in its
 # epilogue (the BN backward then skips its statistics pass).
 BN_BWD_FUSE = os.environ.get("DPT_BN_BWD_FUSE", "1") != "0"
-# dx.data_ptr() -> (p1, p2, shape): handed from a conv's backward to the BN backward that
-# receives dx as its output gradient (ops/bn.py), consumed once
+# dx.data_ptr() -> (p1, p2, shape, dres_ptr): handed from a conv's backward to the BN backward
+# that receives dx as its output gradient (ops/bn.py), consumed once
 _BNB_PARTIALS = {}
 # The im2col stem path is correct but measured slower than MIOpen on ResNet-50's 7x7/2 stem at
 # batch 256 (the [3.2M x 192] bf16 patch matrix is 1.2 GB written and read twice): opt-in only.
@@ -55,10 +55,19 @@ def _backward(ctx, dy):
     s, p = ctx.stride, ctx.pad
     dx = dw = None
     if ctx.needs_input_grad[0]:
-        if s == 1 and ctx.bn_src is not None and BN_BWD_FUSE:
-            bn_x, bn_mean, bn_coef = ctx.bn_src
+        src = ctx.bn_src if (s == 1 and BN_BWD_FUSE) else None
+        dres = None
+        if src is not None and not isinstance(src[2], dict):  # BN+ReLU: (x, mean, coef)
+            bn_x, bn_mean, bn_coef = src
             dx, p1, p2 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, bn_coef)
-            _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape))
+            _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), None)
+        elif src is not None and _dres_ok(dres := src[2].pop("dres", None), x):  # (x, mean, slot)
+            # block-tail BN+add+ReLU (ops/bn.py pair outputs): the next block's tail already
+            # produced the identity-path gradient dres; dx becomes the tail's masked total
+            # gradient, the conv's input x is the tail's output y (the ReLU mask)
+            bn_x, bn_mean, _ = src
+            dx, p1, p2 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, None, x, dres)
+            _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), dres.data_ptr())
         elif s == 1:
             dx = native().conv_dgrad_flip(dy, w, p)[0]
         else:
@@ -67,6 +76,11 @@ def _backward(ctx, dy):
     if ctx.needs_input_grad[1]:
         dw = native().conv_wgrad(dy, x, list(w.shape), s, p, False)
     return dx, dw
+
+
+def _dres_ok(dres, x) -> bool:
+    return (dres is not None and dres.dtype == torch.bfloat16 and dres.shape == x.shape
+            and dres.is_contiguous(memory_format=_CL))
 
 
 class _Conv(torch.autograd.Function):
@@ -113,13 +127,15 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bo
 
 
 def take_bnb_partials(dy: torch.Tensor):
-    """(p1, p2) the backward of the conv that consumed a BN output summed for ``dy``, once."""
+    """(p1, p2, dres_ptr) the backward of the conv that consumed a BN output summed for ``dy``,
+    once; dres_ptr is None for BN+ReLU, else the data pointer of the identity-path gradient
+    that was folded into ``dy`` (block tails)."""
     if not _BNB_PARTIALS:
         return None
     ent = _BNB_PARTIALS.pop(dy.data_ptr(), None)
     if ent is None or ent[2] != tuple(dy.shape):
         return None
-    return ent[0], ent[1]
+    return ent[0], ent[1], ent[3]
 
 
 def take_bn_partials(x: torch.Tensor):

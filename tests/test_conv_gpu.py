@@ -243,3 +243,55 @@ def test_bn_backward_stats_from_dgrad_epilogue(cuda, k2):
     assert not nc._BNB_PARTIALS  # every handed-over partial was consumed
     for a, b in zip(*grads):
         torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item() + 1e-6)
+
+
+def test_block_tail_backward_folded_into_dgrad_epilogue(cuda, monkeypatch):
+    """Two bottleneck-like blocks joined by a fused tail (BN + identity add + ReLU, pair
+    outputs): the next block's conv1 backward-data epilogue adds the identity-path gradient,
+    applies the tail's ReLU mask and sums the tail's statistics (ops/conv.py BNR).  Gradients
+    must equal the unfused path (the tail's own statistics pass)."""
+    from distributed_pytorch_training_amd.ops import bn as fbn
+    from distributed_pytorch_training_amd.ops import conv as nc
+
+    g = torch.Generator(device=cuda).manual_seed(5)
+    N, C4, C, HW = 4, 256, 64, 14
+
+    def t(*s, scale=1.0):
+        return (torch.randn(*s, device=cuda, generator=g) * scale)
+
+    x0 = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
+    r0 = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
+    wa = t(C4, C4, 1, 1, scale=0.06).to(torch.bfloat16).contiguous(memory_format=CL)
+    w1 = t(C, C4, 1, 1, scale=0.06).to(torch.bfloat16).contiguous(memory_format=CL)
+    w3 = t(C4, C, 1, 1, scale=0.12).to(torch.bfloat16).contiguous(memory_format=CL)
+    bn = [(torch.rand(c, device=cuda, generator=g) + 0.5, t(c, scale=0.1)) for c in (C4, C, C4)]
+    gy = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
+    gy2 = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
+    used = []
+    ok = nc._dres_ok
+    monkeypatch.setattr(nc, "_dres_ok", lambda d, x: used.append(ok(d, x)) or used[-1])
+    grads = []
+    for fuse in (True, False):
+        nc.BN_BWD_FUSE = fuse
+        monkeypatch.setattr(fbn, "BNR_FUSE", fuse)
+        xi, ri = (v.detach().clone().requires_grad_(True) for v in (x0, r0))
+        ps = [v.detach().clone().requires_grad_(True) for v in (wa, w1, w3)]
+        bp = [(a.clone().requires_grad_(True), b.clone().requires_grad_(True)) for a, b in bn]
+
+        def bnt(h, i, res=None, relu=True, pair=False):
+            c = h.shape[1]
+            rm, rv = torch.zeros(c, device=cuda), torch.ones(c, device=cuda)
+            nb = torch.zeros((), dtype=torch.long, device=cuda)
+            return fbn.bn_act_train(h, res, bp[i][0], bp[i][1], rm, rv, nb, 0.1, 1e-5, relu, pair)
+
+        yc, yi = bnt(nc.conv2d(xi, ps[0], 1, 0, bn_stats=True), 0, res=ri, pair=True)
+        u = bnt(nc.conv2d(yc, ps[1], 1, 0, bn_stats=True), 1)
+        oc, oi = bnt(nc.conv2d(u, ps[2], 1, 0, bn_stats=True), 2, res=yi, pair=True)
+        torch.autograd.backward([oc, oi], [gy, gy2])
+        grads.append([xi.grad.float(), ri.grad.float()] + [p.grad.float() for p in ps]
+                     + [v.grad.float() for ab in bp for v in ab])
+    nc.BN_BWD_FUSE = True
+    assert used == [True]  # the fused tail path ran exactly once (first pass only)
+    assert not nc._BNB_PARTIALS
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item() + 1e-6)
