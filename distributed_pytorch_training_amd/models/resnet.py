@@ -52,8 +52,10 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         xc, xi = split_block_input(x)
-        identity = xi if self.downsample is None else self.downsample(xi)
         out = bn_act(self.bn1, self.conv1(xc))
+        # downsample after conv1 (same values): autograd then runs its backward before conv1's,
+        # so conv1's backward-data sees the whole identity-path gradient (ops/bn.py block tails)
+        identity = xi if self.downsample is None else self.downsample(xi)
         return bn_act_block_out(self.bn2, self.conv2(out), identity)
 
 
@@ -77,8 +79,10 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         xc, xi = split_block_input(x)
-        identity = xi if self.downsample is None else self.downsample(xi)
         out = bn_act(self.bn1, self.conv1(xc))
+        # downsample after conv1 (same values): autograd then runs its backward before conv1's,
+        # so conv1's backward-data sees the whole identity-path gradient (ops/bn.py block tails)
+        identity = xi if self.downsample is None else self.downsample(xi)
         out = bn_act(self.bn2, self.conv2(out))
         return bn_act_block_out(self.bn3, self.conv3(out), identity)
 

@@ -75,6 +75,10 @@ def _backward(ctx, dy):
                                                      (True, False, False))[0]
     if ctx.needs_input_grad[1]:
         dw = native().conv_wgrad(dy, x, list(w.shape), s, p, False)
+    if dx is not None and ctx.res_slot is not None:
+        # x is the identity alias of a fused block tail and this conv its downsample: hand the
+        # identity-path gradient to the tail's conv-path consumer (see ops/bn.py)
+        ctx.res_slot["dres"] = dx
     return dx, dw
 
 
@@ -85,30 +89,30 @@ def _dres_ok(dres, x) -> bool:
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride: int, pad: int, out_hw, bn_src):
+    def forward(ctx, x, w, stride: int, pad: int, out_hw, bn_src, res_slot):
         y = native().conv_fwd(x, w, stride, pad, False, *out_hw)[0]
         ctx.save_for_backward(x, w)
-        ctx.stride, ctx.pad, ctx.bn_src = stride, pad, bn_src
+        ctx.stride, ctx.pad, ctx.bn_src, ctx.res_slot = stride, pad, bn_src, res_slot
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        return _backward(ctx, dy) + (None, None, None, None)
+        return _backward(ctx, dy) + (None,) * 5
 
 
 class _ConvStats(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride: int, pad: int, out_hw, bn_src):
+    def forward(ctx, x, w, stride: int, pad: int, out_hw, bn_src, res_slot):
         y, ps, pq = native().conv_fwd(x, w, stride, pad, True, *out_hw)
         ctx.save_for_backward(x, w)
-        ctx.stride, ctx.pad, ctx.bn_src = stride, pad, bn_src
+        ctx.stride, ctx.pad, ctx.bn_src, ctx.res_slot = stride, pad, bn_src, res_slot
         ctx.mark_non_differentiable(ps, pq)
         ctx.set_materialize_grads(False)  # no zero-filled gradients for the statistics outputs
         return y, ps, pq
 
     @staticmethod
     def backward(ctx, dy, _dps, _dpq):
-        return _backward(ctx, dy) + (None, None, None, None)
+        return _backward(ctx, dy) + (None,) * 5
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bool = False,
@@ -119,9 +123,11 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bo
     w = _cl(w)
     # (BN input, mean, coef) of the fused BN+ReLU that produced x, if any (ops/bn.py)
     bn_src = x.__dict__.get("_dpt_bn_src")
+    # x is the identity alias of a fused block tail (this conv is a downsample)
+    res_slot = x.__dict__.get("_dpt_res_slot")
     if not bn_stats:
-        return _Conv.apply(x, w, int(stride), int(pad), tuple(out_hw), bn_src)
-    y, ps, pq = _ConvStats.apply(x, w, int(stride), int(pad), tuple(out_hw), bn_src)
+        return _Conv.apply(x, w, int(stride), int(pad), tuple(out_hw), bn_src, res_slot)
+    y, ps, pq = _ConvStats.apply(x, w, int(stride), int(pad), tuple(out_hw), bn_src, res_slot)
     y._dpt_bn_partials = (ps, pq)
     return y
 

@@ -245,11 +245,14 @@ def test_bn_backward_stats_from_dgrad_epilogue(cuda, k2):
         torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item() + 1e-6)
 
 
-def test_block_tail_backward_folded_into_dgrad_epilogue(cuda, monkeypatch):
+@pytest.mark.parametrize("ds", [False, True], ids=["identity", "downsample"])
+def test_block_tail_backward_folded_into_dgrad_epilogue(cuda, monkeypatch, ds):
     """Two bottleneck-like blocks joined by a fused tail (BN + identity add + ReLU, pair
     outputs): the next block's conv1 backward-data epilogue adds the identity-path gradient,
     applies the tail's ReLU mask and sums the tail's statistics (ops/conv.py BNR).  Gradients
-    must equal the unfused path (the tail's own statistics pass)."""
+    must equal the unfused path (the tail's own statistics pass).  ``ds``: the next block
+    downsamples (1x1/2 conv + BN on the identity path, 3x3/2 conv2), as at ResNet layer
+    boundaries - the identity-path gradient then comes from the downsample conv's backward."""
     from distributed_pytorch_training_amd.ops import bn as fbn
     from distributed_pytorch_training_amd.ops import conv as nc
 
@@ -263,10 +266,13 @@ def test_block_tail_backward_folded_into_dgrad_epilogue(cuda, monkeypatch):
     r0 = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
     wa = t(C4, C4, 1, 1, scale=0.06).to(torch.bfloat16).contiguous(memory_format=CL)
     w1 = t(C, C4, 1, 1, scale=0.06).to(torch.bfloat16).contiguous(memory_format=CL)
+    w2 = t(C, C, 3, 3, scale=0.04).to(torch.bfloat16).contiguous(memory_format=CL)
     w3 = t(C4, C, 1, 1, scale=0.12).to(torch.bfloat16).contiguous(memory_format=CL)
-    bn = [(torch.rand(c, device=cuda, generator=g) + 0.5, t(c, scale=0.1)) for c in (C4, C, C4)]
-    gy = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
-    gy2 = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
+    wd = t(C4, C4, 1, 1, scale=0.06).to(torch.bfloat16).contiguous(memory_format=CL)
+    bn = [(torch.rand(c, device=cuda, generator=g) + 0.5, t(c, scale=0.1)) for c in (C4, C, C4, C, C4)]
+    ho = HW // 2 if ds else HW
+    gy = t(N, C4, ho, ho).to(torch.bfloat16).contiguous(memory_format=CL)
+    gy2 = t(N, C4, ho, ho).to(torch.bfloat16).contiguous(memory_format=CL)
     used = []
     ok = nc._dres_ok
     monkeypatch.setattr(nc, "_dres_ok", lambda d, x: used.append(ok(d, x)) or used[-1])
@@ -275,8 +281,8 @@ def test_block_tail_backward_folded_into_dgrad_epilogue(cuda, monkeypatch):
         nc.BN_BWD_FUSE = fuse
         monkeypatch.setattr(fbn, "BNR_FUSE", fuse)
         xi, ri = (v.detach().clone().requires_grad_(True) for v in (x0, r0))
-        ps = [v.detach().clone().requires_grad_(True) for v in (wa, w1, w3)]
-        bp = [(a.clone().requires_grad_(True), b.clone().requires_grad_(True)) for a, b in bn]
+        ps = [v.detach().clone().requires_grad_(True) for v in ((wa, w1, w3, w2, wd) if ds else (wa, w1, w3))]
+        bp = [(a.clone().requires_grad_(True), b.clone().requires_grad_(True)) for a, b in bn[:5 if ds else 3]]
 
         def bnt(h, i, res=None, relu=True, pair=False):
             c = h.shape[1]
@@ -286,7 +292,11 @@ def test_block_tail_backward_folded_into_dgrad_epilogue(cuda, monkeypatch):
 
         yc, yi = bnt(nc.conv2d(xi, ps[0], 1, 0, bn_stats=True), 0, res=ri, pair=True)
         u = bnt(nc.conv2d(yc, ps[1], 1, 0, bn_stats=True), 1)
-        oc, oi = bnt(nc.conv2d(u, ps[2], 1, 0, bn_stats=True), 2, res=yi, pair=True)
+        ident = yi
+        if ds:  # the model's order: downsample after conv1 (models/resnet.py)
+            ident = bnt(nc.conv2d(yi, ps[4], 2, 0, bn_stats=True), 4, relu=False)
+            u = bnt(nc.conv2d(u, ps[3], 2, 1, bn_stats=True), 3)
+        oc, oi = bnt(nc.conv2d(u, ps[2], 1, 0, bn_stats=True), 2, res=ident, pair=True)
         torch.autograd.backward([oc, oi], [gy, gy2])
         grads.append([xi.grad.float(), ri.grad.float()] + [p.grad.float() for p in ps]
                      + [v.grad.float() for ab in bp for v in ab])
