@@ -317,6 +317,23 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
   return {dx, p1, p2};
 }
 
+// Stride-2 backward-data: dx [N, C, H, W] (channels_last) of y = conv2d(x, w, stride 2, pad).
+Tensor conv_dgrad_s2(Tensor dy, Tensor w, int64_t pad, int64_t H, int64_t W) {
+  check_cl_bf16(dy, "grad_output");
+  check_cl_bf16(w, "w");
+  const int Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(dy.size(1) == Cout && dpt::conv_supported(Cout, C), "conv_dgrad_s2: needs C, Cout % 64 == 0");
+  const int N = dy.size(0), Ho = dy.size(2), Wo = dy.size(3);
+  TORCH_CHECK(Ho == (H + 2 * pad - R) / 2 + 1 && Wo == (W + 2 * pad - S) / 2 + 1, "conv_dgrad_s2: geometry mismatch");
+  TORCH_CHECK((int64_t)N * H * W < (int64_t(1) << 31), "conv_dgrad_s2: too many pixels");
+  auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(dy.device().index());
+  dpt::launch_conv_dgrad_s2(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                            reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, (int)pad, (int)H, (int)W,
+                            cur_stream(dy));
+  return dx;
+}
+
 // Same through an explicitly flipped/transposed weight copy (returned too): the reference
 // path the tests compare the folded addressing against.
 std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad) {
@@ -576,7 +593,8 @@ std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t stride, int64_t pad
   return {y, idx};
 }
 
-Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64_t stride, int64_t pad) {
+Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64_t stride, int64_t pad,
+                   c10::optional<Tensor> dy2) {
   TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
               "maxpool_bwd: grad must be channels_last");
   TORCH_CHECK(idx.sizes() == dy.sizes() && idx.scalar_type() == at::kByte &&
@@ -584,10 +602,27 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64
   const int64_t B = dy.size(0), C = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
   TORCH_CHECK(C % 8 == 0 && Ho == (H + 2 * pad - k) / stride + 1 && Wo == (W + 2 * pad - k) / stride + 1,
               "maxpool_bwd: geometry mismatch");
+  const bool two = dy2.has_value() && dy2->defined();
+  if (two)
+    TORCH_CHECK(dy2->sizes() == dy.sizes() && dy2->scalar_type() == dy.scalar_type() &&
+                    dy2->is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool_bwd: dy2 must match grad_output");
   auto dx = at::empty({B, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   c10::hip::HIPGuard guard(dy.device().index());
-  dpt::launch_maxpool_bwd(bn_dtype(dy), dy.data_ptr(), idx.data_ptr<uint8_t>(), dx.data_ptr(), B, (int)H, (int)W,
+  dpt::launch_maxpool_bwd(bn_dtype(dy), dy.data_ptr(), two ? dy2->data_ptr() : nullptr, idx.data_ptr<uint8_t>(),
+                          dx.data_ptr(), B, (int)H, (int)W,
                           (int)C, (int)Ho, (int)Wo, (int)k, (int)stride, (int)pad, cur_stream(dy));
+  return dx;
+}
+
+// dx = broadcast of g [N, C] / (H*W) over an [N, C, H, W] channels_last tensor of dtype like_dtype
+Tensor gap_bwd(Tensor g, int64_t H, int64_t W, at::ScalarType dtype) {
+  TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() && g.size(1) % 8 == 0, "gap_bwd: g must be [N, C], C % 8 == 0");
+  TORCH_CHECK(dtype == at::kFloat || dtype == at::kBFloat16 || dtype == at::kHalf, "gap_bwd: dtype");
+  const int64_t N = g.size(0), C = g.size(1);
+  TORCH_CHECK(N * H * W * (C / 8) < (int64_t(1) << 32) - 256, "gap_bwd: too large");
+  auto dx = at::empty({N, C, H, W}, g.options().dtype(dtype).memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(g.device().index());
+  dpt::launch_gap_bwd(bn_dtype(dx), bn_dtype(g), g.data_ptr(), dx.data_ptr(), N, H * W, C, cur_stream(g));
   return dx;
 }
 
@@ -814,8 +849,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_grad16", &bias_grad16, py::arg("grad"), py::arg("out_kind"));
   m.def("sum_partials", &sum_partials, py::arg("part"), py::arg("out_kind"));
   m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("stride"), py::arg("pad"));
+  m.def("gap_bwd", &gap_bwd, py::arg("g"), py::arg("H"), py::arg("W"), py::arg("dtype"));
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("grad_output"), py::arg("idx"), py::arg("H"), py::arg("W"),
-        py::arg("k"), py::arg("stride"), py::arg("pad"));
+        py::arg("k"), py::arg("stride"), py::arg("pad"), py::arg("grad_output2") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"),
         py::arg("out_h") = 0, py::arg("out_w") = 0);
   m.def("space_to_depth2", &space_to_depth2, py::arg("x"));
@@ -833,6 +869,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_partials", &bn_bwd_partials, py::arg("grad_output"), py::arg("x"), py::arg("weight"), py::arg("mean"),
         py::arg("invstd"), py::arg("coef"), py::arg("p1"), py::arg("p2"), py::arg("want_dparams"),
         py::arg("from_dz") = false);
+  m.def("conv_dgrad_s2", &conv_dgrad_s2, py::arg("grad_output"), py::arg("w"), py::arg("pad"), py::arg("H"),
+        py::arg("W"));
   m.def("conv_dgrad_flip", &conv_dgrad_flip, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
 

@@ -27,6 +27,7 @@
 // consecutive and land on the same XCD (bijective XCD remap, cdna_hip_programming.md T1).
 #include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
 
 #include "common.h"
 #include "kernels.h"
@@ -73,6 +74,11 @@ struct ConvFwdArgs {
   // next block's identity path
   const uint16_t* bny;    // its output y (ReLU mask)
   const uint16_t* bnres;  // the identity-path gradient (added before the mask)
+  // BKN tap map: GEMM tap (r, s) reads weight tap (tr0 + trs*r, ts0 + tss*s) of the Rw x Sw
+  // weight (stride-1 backward-data: the flip R-1-r; strided backward-data: one parity class)
+  int Rw, Sw, tr0, trs, ts0, tss;
+  // REMAP epilogue: GEMM output row (n, a, b) lands on row (n*oH + 2a + oph)*oW + 2b + opw
+  int oH, oW, oph, opw;
 };
 
 // K-major operands (rows of the LDS image = k) use the transposing reads and the swizzle of
@@ -103,8 +109,11 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 // whole masked gradient dz = (g + g_identity) * (y > 0) - the tail's residual-path gradient
 // and the input of its backward apply - and s1/s2 are summed from it.  Replaces the
 // tail's backward-statistics pass (4 reads + 1 write of a 4C-channel tensor) by 3 reads here.
+// REMAP (LDS epilogue): output rows scattered to one stride-2 parity class of a larger image
+// (strided backward-data); ZSIB: also write zeros to the other three positions of each 2x2
+// cell (1x1 / stride-2 backward-data, whose other classes receive no gradient).
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
-          bool BNR = false>
+          bool BNR = false, bool REMAP = false, bool ZSIB = false>
 __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
   constexpr int BM = BMT;
@@ -170,7 +179,7 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
       // fills chunk wg_slot(row, lane % chunks) of it)
       const int krow = (wid * B_PER_T + i) * KN_RPI + lane / (RBK / 16);
       const int kchunk = wg_slot<RBK>(krow, lane % (RBK / 16));
-      wrow[i] = p.w + (int64_t)krow * p.R * p.S * p.Cout + n0 + kchunk * 8;
+      wrow[i] = p.w + (int64_t)krow * p.Rw * p.Sw * p.Cout + n0 + kchunk * 8;
     } else {
       const int brow = (wid * B_PER_T + i) * 8 + (lane >> 3);
       const int bchunk = (lane & 7) ^ ((brow >> 1) & 7);
@@ -197,8 +206,8 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(a + (wid * A_PER_T + i) * 1024),
                                        16, 0, 0);
     }
-    // BKN: rows co = cb*BK + krow, flipped tap (R-1-r, S-1-s)
-    const int64_t wk = BKN ? ((int64_t)cb * BK * p.R * p.S + (p.R - 1 - r) * p.S + (p.S - 1 - s)) * p.Cout
+    // BKN: rows co = cb*BK + krow, mapped tap (tr0 + trs*r, ts0 + tss*s)
+    const int64_t wk = BKN ? ((int64_t)cb * BK * p.Rw * p.Sw + (p.tr0 + p.trs * r) * p.Sw + (p.ts0 + p.tss * s)) * p.Cout
                            : (int64_t)ks * BK;  // k = (r*S + s)*C + c: K-step ks is [64ks, 64ks+64)
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i)
@@ -406,7 +415,25 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
             }
             if (BNR) v = make_uint4(du[0], du[1], du[2], du[3]);
           }
-          *reinterpret_cast<uint4*>(p.y + m * p.Cout + n0 + oc * 8) = v;
+          if (REMAP) {
+            const uint32_t mm = (uint32_t)m, hw = (uint32_t)HoWo;
+            const uint32_t img = mm / hw, rem = mm - img * hw;
+            const int a = (int)(rem / (uint32_t)p.Wo), b = (int)(rem - (uint32_t)a * (uint32_t)p.Wo);
+            const int oy = 2 * a + p.oph, ox = 2 * b + p.opw;
+            uint16_t* orow = p.y + (((int64_t)img * p.oH + oy) * p.oW + ox) * p.Cout + n0 + oc * 8;
+            *reinterpret_cast<uint4*>(orow) = v;
+            if (ZSIB) {
+              const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+              const int64_t rs = (int64_t)p.oW * p.Cout;
+              if (ox + 1 < p.oW) *reinterpret_cast<uint4*>(orow + p.Cout) = z;
+              if (oy + 1 < p.oH) {
+                *reinterpret_cast<uint4*>(orow + rs) = z;
+                if (ox + 1 < p.oW) *reinterpret_cast<uint4*>(orow + rs + p.Cout) = z;
+              }
+            }
+          } else {
+            *reinterpret_cast<uint4*>(p.y + m * p.Cout + n0 + oc * 8) = v;
+          }
         }
       }
     }
@@ -1059,6 +1086,7 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
   a.Wo = Wo > 0 ? Wo : (W + 2 * pad - S) / stride + 1;
   a.M = (int64_t)N * a.Ho * a.Wo;
   a.m_tiles = conv_m_tiles(a.M);
+  a.Rw = R; a.Sw = S; a.tr0 = R - 1; a.trs = -1; a.ts0 = S - 1; a.tss = -1;  // BKN: flipped taps
   const bool wide = Cout % 128 == 0;
   a.n_tiles = Cout / (wide ? 128 : 64);
   a.mt256 = 0;
@@ -1106,6 +1134,60 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, i
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout, int C,
                        int R, int S, int pad, hipStream_t s) {
   conv_fwd_impl(dy, w, dx, N, Ho, Wo, Cout, C, R, S, 1, R - 1 - pad, nullptr, nullptr, true, s);
+}
+
+// Strided backward-data (stride 2, any R/S/pad) straight from the KRSC weight w [Cout,R,S,C]:
+// dx [N,H,W,C] splits into the four parity classes (h % 2, w % 2).  Class (ph, pw) is a
+// stride-1, top/left-unpadded conv of dy [N,Ho,Wo,Cout] with the taps r = r0 + 2j (r = h + pad
+// - 2i, r = ph + pad mod 2), taken in decreasing r so the dy row index increases with the GEMM
+// tap; its output rows land on (2a + ph, 2b + pw) (REMAP epilogue).  A class with no taps
+// (e.g. the odd classes of a 1x1 / stride-2 conv) gets zeros from the class-(0,0) launch (ZSIB)
+// - every dx element is written exactly once, no memset pass.
+void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout,
+                          int C, int R, int S, int pad, int H, int W, hipStream_t s) {
+  int J[2], r0[2], Js[2], s0[2], D[2], Ds[2];
+  for (int ph = 0; ph < 2; ++ph) {
+    r0[ph] = ((ph + pad) % 2 + 2) % 2;
+    J[ph] = r0[ph] < R ? (R - 1 - r0[ph]) / 2 + 1 : 0;
+    D[ph] = (ph + pad - r0[ph]) / 2;  // dy row of tap r0 for a = 0
+    s0[ph] = r0[ph];
+    Js[ph] = s0[ph] < S ? (S - 1 - s0[ph]) / 2 + 1 : 0;
+    Ds[ph] = D[ph];
+  }
+  const bool zsib = J[1] == 0 && Js[1] == 0 && J[0] > 0 && Js[0] > 0;
+  for (int ph = 0; ph < 2; ++ph) {
+    for (int pw = 0; pw < 2; ++pw) {
+      const int Ha = (H - ph + 1) / 2, Wa = (W - pw + 1) / 2;
+      if (Ha <= 0 || Wa <= 0 || J[ph] == 0 || Js[pw] == 0) continue;
+      ConvFwdArgs a;
+      a.x = dy; a.w = w; a.y = dx; a.psum = nullptr; a.psq = nullptr;
+      a.N = N; a.H = Ho; a.W = Wo; a.C = Cout; a.Cout = C; a.R = J[ph]; a.S = Js[pw]; a.stride = 1;
+      // GEMM tap jj (0..J-1) reads dy row a + D - (J-1) + jj, weight tap r0 + 2*(J-1-jj)
+      a.pad = J[ph] - 1 - D[ph];
+      if (Js[pw] - 1 - Ds[pw] != a.pad) throw std::runtime_error("conv_dgrad_s2: unequal class paddings");
+      a.Ho = Ha; a.Wo = Wa;
+      a.M = (int64_t)N * Ha * Wa;
+      a.m_tiles = conv_m_tiles(a.M);
+      a.mt256 = 0;
+      a.Rw = R; a.Sw = S;
+      a.tr0 = r0[ph] + 2 * (J[ph] - 1); a.trs = -2;
+      a.ts0 = s0[pw] + 2 * (Js[pw] - 1); a.tss = -2;
+      a.oH = H; a.oW = W; a.oph = ph; a.opw = pw;
+      a.bnx = nullptr; a.bny = nullptr; a.bnres = nullptr; a.bn_mean = nullptr; a.bn_coef = nullptr;
+      a.bp1 = nullptr; a.bp2 = nullptr;
+      const bool z = zsib && ph == 0 && pw == 0;
+      const dim3 block(conv::kThreads);
+      a.n_tiles = C % 128 == 0 ? C / 128 : C / 64;
+      const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
+      if (C % 128 == 0) {
+        if (z) hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, true, false, false, false, true, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, true, false, false, false, true, false>), grid, block, 0, s, a);
+      } else {
+        if (z) hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, true, true, false, false, false, true, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, true, true, false, false, false, true, false>), grid, block, 0, s, a);
+      }
+    }
+  }
 }
 
 static FastDiv make_fastdiv(uint32_t d) {

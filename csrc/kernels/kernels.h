@@ -74,8 +74,11 @@ void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, co
 // pool_kernels.hip  (channels_last [B,H,W,C], C % 8 == 0; idx = window-local uint8 argmax)
 void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t B, int H, int W, int C, int Ho,
                         int Wo, int K, int S, int P, hipStream_t s);
-void launch_maxpool_bwd(int dtype, const void* dy, const uint8_t* idx, void* dx, int64_t B, int H, int W, int C,
-                        int Ho, int Wo, int K, int S, int P, hipStream_t s);
+// global-average-pool backward: dx [N, HW, C] (dtype) = g [N, C] (gdtype) / HW
+void launch_gap_bwd(int dtype, int gdtype, const void* g, void* dx, int64_t N, int64_t HW, int64_t C, hipStream_t s);
+// dy2: optional second output gradient, summed in (pool output with two consumers)
+void launch_maxpool_bwd(int dtype, const void* dy, const void* dy2, const uint8_t* idx, void* dx, int64_t B, int H,
+                        int W, int C, int Ho, int Wo, int K, int S, int P, hipStream_t s);
 
 // gather_kernels.hip: up to kGatherMax tensors per launch (kernel-argument struct)
 constexpr int kGatherMax = 48;
@@ -142,6 +145,9 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
                                int C, int R, int S, int pad, const uint16_t* bnx, const float* bn_mean,
                                const float* bn_coef, float* bp1, float* bp2, hipStream_t s,
                                const uint16_t* bny = nullptr, const uint16_t* bnres = nullptr);
+// stride-2 backward-data straight from the KRSC weight w [Cout,R,S,C]: dy [N,Ho,Wo,Cout] -> dx [N,H,W,C]
+void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout,
+                          int C, int R, int S, int pad, int H, int W, hipStream_t s);
 // stride-1 backward-data straight from the KRSC weight w [Cout,R,S,C]: dy [N,Ho,Wo,Cout] -> dx [N,Ho,Wo,C]
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout, int C,
                        int R, int S, int pad, hipStream_t s);

@@ -74,14 +74,29 @@ def split_block_input(x):
 
 
 class FusedMaxPool2d(nn.MaxPool2d):
-    """``nn.MaxPool2d`` that runs the gfx950 channels-last kernels when it can."""
+    """``nn.MaxPool2d`` that runs the gfx950 channels-last kernels when it can.  With
+    ``dpt_pair`` (ResNet's stem pool, set by ``fuse_native_layers``) it returns
+    ``(y_conv, y_identity)`` aliases for the first residual block, whose two gradients the
+    backward sums while gathering."""
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    dpt_pair = False
+
+    def forward(self, x: torch.Tensor):
         if not self.return_indices and fused_pool.maxpool_supported(
                 x, self.kernel_size, self.stride, self.padding, self.dilation, self.ceil_mode):
             as_int = lambda v: v if isinstance(v, int) else v[0]
+            pair = self.dpt_pair and self.training and torch.is_grad_enabled()
             return fused_pool.max_pool2d_nhwc(x, as_int(self.kernel_size), as_int(self.stride),
-                                              as_int(self.padding))
+                                              as_int(self.padding), pair)
+        return super().forward(x)
+
+
+class FusedAdaptiveAvgPool2d(nn.AdaptiveAvgPool2d):
+    """``nn.AdaptiveAvgPool2d((1, 1))`` whose backward is the gfx950 broadcast kernel."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if fused_pool.gap_supported(x) and torch.is_grad_enabled() and x.requires_grad:
+            return fused_pool.global_avg_pool_nhwc(x)
         return super().forward(x)
 
 
@@ -117,12 +132,16 @@ def fuse_native_layers(model: nn.Module, gemm_1x1: bool = False) -> int:
             new_cls = None
             if type(child) is nn.MaxPool2d:
                 new_cls = FusedMaxPool2d
+            elif type(child) is nn.AdaptiveAvgPool2d and child.output_size in (1, (1, 1)):
+                new_cls = FusedAdaptiveAvgPool2d
             elif gemm_1x1 and type(child) is nn.Conv2d and child.kernel_size == (1, 1) \
                     and child.stride == (1, 1) and child.groups == 1 and child.bias is None:
                 new_cls = GemmConv1x1
             if new_cls is not None:
                 new = new_cls.__new__(new_cls)
                 new.__dict__ = child.__dict__
+                if new_cls is FusedMaxPool2d and name == "maxpool" and hasattr(parent, "layer1"):
+                    new.dpt_pair = True  # ResNet stem: feeds layer1's conv and identity paths
                 setattr(parent, name, new)
                 n += 1
     tag_conv_bn_pairs(model)

@@ -30,6 +30,39 @@ class _MaxPoolNHWC(torch.autograd.Function):
         return native().maxpool_bwd(dy, idx, H, W, k, s, p), None, None, None
 
 
+class _MaxPoolNHWCPair(torch.autograd.Function):
+    """Same op with two aliased outputs (ResNet's stem pool feeds layer1's conv path and its
+    downsample identity path): autograd hands the two gradients over separately and the
+    backward gather sums them while reading - no autograd add kernel (a full pass over the
+    [B, 56, 56, 64] activation gradient, twice read once written)."""
+
+    @staticmethod
+    def forward(ctx, x, k, stride, pad):
+        y, idx = native().maxpool_fwd(x, k, stride, pad)
+        ctx.save_for_backward(idx)
+        ctx.cfg = (x.shape[2], x.shape[3], k, stride, pad)
+        ctx.mark_non_differentiable(idx)
+        ctx.set_materialize_grads(False)
+        return y, y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, dy, dy2):
+        (idx,) = ctx.saved_tensors
+        H, W, k, s, p = ctx.cfg
+        if dy is None:
+            dy, dy2 = dy2, None
+        if dy is None:
+            return None, None, None, None
+        dy = _cl(dy)
+        if dy2 is not None:
+            dy2 = _cl(dy2.to(dy.dtype))
+        return native().maxpool_bwd(dy, idx, H, W, k, s, p, dy2), None, None, None
+
+
+def _cl(t: torch.Tensor) -> torch.Tensor:
+    return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
+
+
 def maxpool_supported(x: torch.Tensor, k, stride, pad, dilation, ceil_mode) -> bool:
     k, stride, pad, dilation = (v if isinstance(v, int) else (v[0] if len(set(v)) == 1 else None)
                                 for v in (k, stride, pad, dilation))
@@ -40,5 +73,35 @@ def maxpool_supported(x: torch.Tensor, k, stride, pad, dilation, ceil_mode) -> b
             and k * k <= 255 and pad <= k // 2)
 
 
-def max_pool2d_nhwc(x: torch.Tensor, k: int, stride: int, pad: int) -> torch.Tensor:
+def max_pool2d_nhwc(x: torch.Tensor, k: int, stride: int, pad: int, pair: bool = False):
+    """``pair``: return (y, y_alias) for a conv path and an identity path (see _MaxPoolNHWCPair)."""
+    if pair:
+        return _MaxPoolNHWCPair.apply(x, int(k), int(stride), int(pad))
     return _MaxPoolNHWC.apply(x, int(k), int(stride), int(pad))
+
+
+class _GlobalAvgPoolNHWC(torch.autograd.Function):
+    """adaptive_avg_pool2d(x, 1) on a channels_last activation; the backward broadcast
+    g / (H*W) is one vectorised HIP kernel (pool_kernels.hip gap_bwd) instead of ATen's
+    expand + strided copy."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.cfg = (x.shape[2], x.shape[3], x.dtype)
+        return torch.nn.functional.adaptive_avg_pool2d(x, 1)
+
+    @staticmethod
+    def backward(ctx, g):
+        H, W, dt = ctx.cfg
+        return native().gap_bwd(g.reshape(g.shape[0], g.shape[1]).contiguous(), H, W, dt)
+
+
+def gap_supported(x: torch.Tensor) -> bool:
+    return (x.is_cuda and native_available() and x.dim() == 4 and x.shape[1] % 8 == 0
+            and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def global_avg_pool_nhwc(x: torch.Tensor) -> torch.Tensor:
+    return _GlobalAvgPoolNHWC.apply(x)
+

@@ -107,7 +107,7 @@ def test_resnet_fused_matches_unfused(cuda, batch, size):
     ref = build_model("resnet50", 100, cuda, image_size=size, channels_last=True)
     fused = copy.deepcopy(ref)
     f64 = copy.deepcopy(ref).double()
-    assert fuse_native_layers(fused) == 54
+    assert fuse_native_layers(fused) == 55  # 53 BN + stem max-pool + global avg-pool
     x = torch.randn(batch, 3, size, size, device=cuda).contiguous(memory_format=torch.channels_last)
     torch.backends.cudnn.deterministic = True
     outs = []
@@ -177,5 +177,43 @@ def test_maxpool_matches_torch(cuda, dtype, shape, k, s, p):
     g = _mk(tuple(ya.shape), dtype, cuda, 22)
     ya.backward(g)
     yb.backward(g)
+    rt, at = TOL[dtype]
+    torch.testing.assert_close(xa.grad.float(), xb.grad.float(), rtol=rt, atol=at)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_maxpool_pair_sums_both_gradients(cuda, dtype):
+    """Stem-pool pair outputs: the backward gather sums the conv-path and identity-path
+    gradients (ops/pool.py _MaxPoolNHWCPair) - equal to torch's pool with the summed grad."""
+    from distributed_pytorch_training_amd.ops.pool import max_pool2d_nhwc
+
+    x = _mk((4, 64, 56, 56), dtype, cuda, 31)
+    xa = x.detach().clone().requires_grad_()
+    xb = x.detach().clone().requires_grad_()
+    y1, y2 = max_pool2d_nhwc(xa, 3, 2, 1, pair=True)
+    yb = torch.nn.functional.max_pool2d(xb, 3, 2, 1)
+    assert torch.equal(y1, yb) and torch.equal(y2, yb)
+    g1 = _mk(tuple(yb.shape), dtype, cuda, 32)
+    g2 = _mk(tuple(yb.shape), dtype, cuda, 33)
+    torch.autograd.backward([y1, y2], [g1, g2])
+    yb.backward(g1.float().add(g2.float()).to(dtype))
+    rt, at = TOL[dtype]
+    torch.testing.assert_close(xa.grad.float(), xb.grad.float(), rtol=rt, atol=2 * at)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_global_avg_pool_backward(cuda, dtype):
+    from distributed_pytorch_training_amd.ops.pool import global_avg_pool_nhwc
+
+    x = _mk((5, 2048, 7, 7), dtype, cuda, 41)
+    xa = x.detach().clone().requires_grad_()
+    xb = x.detach().clone().requires_grad_()
+    ya = global_avg_pool_nhwc(xa)
+    yb = torch.nn.functional.adaptive_avg_pool2d(xb, 1)
+    assert torch.equal(ya, yb)
+    g = _mk(tuple(yb.shape), dtype, cuda, 42)
+    ya.backward(g)
+    yb.backward(g)
+    assert xa.grad.is_contiguous(memory_format=torch.channels_last)
     rt, at = TOL[dtype]
     torch.testing.assert_close(xa.grad.float(), xb.grad.float(), rtol=rt, atol=at)
