@@ -6,7 +6,8 @@ forward   implicit-GEMM conv; with ``bn_stats`` its epilogue also emits the per-
           BatchNorm consumes instead of re-reading the activation (ops/bn.py picks them up
           from the output tensor's ``_dpt_bn_partials`` attribute).
 backward  input gradient: the same kernel on dy reading the weight as [co][ci] with flipped taps
-          through transposing LDS reads (stride 1) or MIOpen's backward-data (strided convs); weight gradient: split-K MFMA kernel
+          through transposing LDS reads (stride 1), or, stride 2, four parity-class convs whose
+          outputs are scattered onto the even/odd rows and columns of dx; weight gradient: split-K MFMA kernel
           with transposing LDS reads, bf16 (the shadow weight's dtype).
 
 Replaces the reference's cuDNN convolutions (reference
@@ -29,6 +30,8 @@ BN_BWD_FUSE = os.environ.get("DPT_BN_BWD_FUSE", "1") != "0"
 # dx.data_ptr() -> (p1, p2, shape, dres_ptr): handed from a conv's backward to the BN backward
 # that receives dx as its output gradient (ops/bn.py), consumed once
 _BNB_PARTIALS = {}
+# Stride-2 backward-data on the MFMA kernels (four parity-class convs); 0 = MIOpen
+S2_DGRAD = os.environ.get("DPT_S2_DGRAD", "1") != "0"
 # The im2col stem path is correct but measured slower than MIOpen on ResNet-50's 7x7/2 stem at
 # batch 256 (the [3.2M x 192] bf16 patch matrix is 1.2 GB written and read twice): opt-in only.
 STEM_ENABLED = os.environ.get("DPT_NATIVE_STEM", "0") == "1"
@@ -70,6 +73,8 @@ def _backward(ctx, dy):
             _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), dres.data_ptr())
         elif s == 1:
             dx = native().conv_dgrad_flip(dy, w, p)[0]
+        elif s == 2 and S2_DGRAD and x.dim() == 4:
+            dx = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3])
         else:
             dx = torch.ops.aten.convolution_backward(dy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
                                                      (True, False, False))[0]

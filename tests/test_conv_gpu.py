@@ -67,6 +67,28 @@ def test_conv_dgrad_matches_fp32(cuda, shape):
     torch.testing.assert_close(dx2.float(), ref, rtol=1e-2, atol=2e-2)
 
 
+S2_SHAPES = [s for s in SHAPES if s[6] == 2] + [
+    (3, 64, 9, 9, 64, 1, 2, 0),        # odd image: the zero-filled classes stop at the border
+    (2, 128, 16, 16, 128, 3, 2, 1),
+    (2, 64, 11, 12, 128, 3, 2, 1),     # odd rows, even cols
+    (2, 64, 12, 12, 64, 7, 2, 3),      # 7x7 / 2 (four non-empty classes of 3-4 taps)
+]
+
+
+@pytest.mark.parametrize("shape", S2_SHAPES)
+def test_conv_dgrad_stride2_matches_fp32(cuda, shape):
+    """Stride-2 backward-data as four parity-class convs (conv_kernels.hip launch_conv_dgrad_s2):
+    every dx element written exactly once, zeros where no tap reaches."""
+    N, C, H, W, Cout, k, s, p = shape
+    x, w = _operands(cuda, N, C, H, W, Cout, k, seed=2)
+    Ho, Wo = (H + 2 * p - k) // 2 + 1, (W + 2 * p - k) // 2 + 1
+    gy = torch.randn(N, Cout, Ho, Wo, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    dx = ops.native().conv_dgrad_s2(gy, w, p, H, W)
+    ref = torch.nn.grad.conv2d_input(x.shape, w.float(), gy.float(), stride=2, padding=p)
+    assert dx.shape == ref.shape and dx.is_contiguous(memory_format=CL)
+    torch.testing.assert_close(dx.float(), ref, rtol=1e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("fp32_out", [True, False])
 @pytest.mark.parametrize("wvariant", [0, 1], ids=["1stage", "2stage"])
