@@ -278,7 +278,8 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t pad) {
 // the tail's whole masked gradient (dx + bn_res) * (bn_y > 0) and p1/p2 are summed from it.
 std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor bn_x, Tensor bn_mean,
                                        c10::optional<Tensor> bn_coef,
-                                       c10::optional<Tensor> bn_y, c10::optional<Tensor> bn_res) {
+                                       c10::optional<Tensor> bn_y, c10::optional<Tensor> bn_res,
+                                       c10::optional<Tensor> w_flipped) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
   check_cl_bf16(bn_x, "bn_x");
@@ -298,15 +299,22 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
     TORCH_CHECK(bn_y->sizes() == bn_x.sizes() && bn_res->sizes() == bn_x.sizes(),
                 "conv_dgrad_bnstats: bn_y / bn_res must match bn_x");
   }
-  auto wt = at::empty({C, Cout, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const bool pre = w_flipped.has_value() && w_flipped->defined();
+  if (pre) {
+    check_cl_bf16(*w_flipped, "w_flipped");
+    TORCH_CHECK(w_flipped->size(0) == C && w_flipped->size(1) == Cout && w_flipped->size(2) == R &&
+                    w_flipped->size(3) == S, "conv_dgrad_bnstats: w_flipped must be [C, Cout, R, S]");
+  }
+  auto wt = pre ? *w_flipped : at::empty({C, Cout, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int mt = dpt::conv_m_tiles((int64_t)N * H * W);
   auto p1 = at::empty({C, mt}, dy.options().dtype(at::kFloat));
   auto p2 = at::empty({C, mt}, dy.options().dtype(at::kFloat));
   c10::hip::HIPGuard guard(dy.device().index());
   auto st = cur_stream(dy);
-  dpt::launch_conv_wt_flip(reinterpret_cast<const uint16_t*>(w.data_ptr()), reinterpret_cast<uint16_t*>(wt.data_ptr()),
-                           Cout, R, S, C, st);
+  if (!pre)
+    dpt::launch_conv_wt_flip(reinterpret_cast<const uint16_t*>(w.data_ptr()), reinterpret_cast<uint16_t*>(wt.data_ptr()),
+                             Cout, R, S, C, st);
   dpt::launch_conv_dgrad_bnstats(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                                  reinterpret_cast<const uint16_t*>(wt.data_ptr()), reinterpret_cast<uint16_t*>(dx.data_ptr()),
                                  N, Ho, Wo, Cout, C, R, S, (int)pad, reinterpret_cast<const uint16_t*>(bn_x.data_ptr()),
@@ -331,6 +339,52 @@ Tensor conv_dgrad_s2(Tensor dy, Tensor w, int64_t pad, int64_t H, int64_t W) {
   dpt::launch_conv_dgrad_s2(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
                             reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, (int)pad, (int)H, (int)W,
                             cur_stream(dy));
+  return dx;
+}
+
+// Flip/transpose many KRSC weights [Cout, C, R, S] (channels_last) into [C, Cout, R, S]
+// (channels_last, taps flipped) in one launch.
+std::vector<Tensor> conv_wt_flip_multi(std::vector<Tensor> ws) {
+  std::vector<Tensor> out;
+  out.reserve(ws.size());
+  if (ws.empty()) return out;
+  c10::hip::HIPGuard guard(ws[0].device().index());
+  auto st = cur_stream(ws[0]);
+  dpt::WtFlipBatch b;
+  b.count = 0;
+  for (size_t i = 0; i < ws.size(); ++i) {
+    const Tensor& w = ws[i];
+    check_cl_bf16(w, "w");
+    const int Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+    TORCH_CHECK(Cout % 8 == 0 && (int64_t)Cout * C * R * S < (int64_t(1) << 31), "conv_wt_flip_multi: bad weight");
+    auto wt = at::empty({C, Cout, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+    out.push_back(wt);
+    const int k = b.count++;
+    b.w[k] = reinterpret_cast<const uint16_t*>(w.data_ptr());
+    b.wt[k] = reinterpret_cast<uint16_t*>(wt.data_ptr());
+    b.Cout[k] = Cout; b.R[k] = R; b.S[k] = S; b.C[k] = C;
+    if (b.count == dpt::kWtFlipMax || i + 1 == ws.size()) {
+      dpt::launch_conv_wt_flip_multi(b, st);
+      b.count = 0;
+    }
+  }
+  return out;
+}
+
+// Stride-1 backward-data through an already flipped/transposed weight (conv_wt_flip_multi).
+Tensor conv_dgrad_preflipped(Tensor dy, Tensor wt, int64_t pad) {
+  check_cl_bf16(dy, "grad_output");
+  check_cl_bf16(wt, "w_flipped");
+  const int C = wt.size(0), Cout = wt.size(1), R = wt.size(2), S = wt.size(3);
+  TORCH_CHECK(dy.size(1) == Cout && dpt::conv_supported(Cout, C), "conv_dgrad_preflipped: bad shapes");
+  TORCH_CHECK(R - 1 - pad >= 0 && S == R, "conv_dgrad_preflipped: needs square kernel and pad <= R-1");
+  const int N = dy.size(0), Ho = dy.size(2), Wo = dy.size(3);
+  auto dx = at::empty({N, C, Ho + R - 1 - 2 * (int)pad, Wo + S - 1 - 2 * (int)pad},
+                      dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(dy.device().index());
+  dpt::launch_conv_fwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(wt.data_ptr()),
+                       reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, 1, (int)(R - 1 - pad),
+                       nullptr, nullptr, cur_stream(dy));
   return dx;
 }
 
@@ -865,7 +919,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("conv_dgrad_bnstats", &conv_dgrad_bnstats, py::arg("grad_output"), py::arg("w"), py::arg("pad"),
         py::arg("bn_x"), py::arg("bn_mean"), py::arg("bn_coef"), py::arg("bn_y") = py::none(),
-        py::arg("bn_res") = py::none());
+        py::arg("bn_res") = py::none(), py::arg("w_flipped") = py::none());
+  m.def("conv_wt_flip_multi", &conv_wt_flip_multi, py::arg("ws"));
+  m.def("conv_dgrad_preflipped", &conv_dgrad_preflipped, py::arg("grad_output"), py::arg("w_flipped"), py::arg("pad"));
   m.def("bn_bwd_partials", &bn_bwd_partials, py::arg("grad_output"), py::arg("x"), py::arg("weight"), py::arg("mean"),
         py::arg("invstd"), py::arg("coef"), py::arg("p1"), py::arg("p2"), py::arg("want_dparams"),
         py::arg("from_dz") = false);

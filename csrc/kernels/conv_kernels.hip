@@ -1009,6 +1009,46 @@ __global__ __launch_bounds__(kBlock) void conv_wt_flip_kernel(const uint16_t* __
   }
 }
 
+// Every conv weight of a step flipped in ONE launch (ops/conv.py flip cache): blocks are dealt
+// to the descriptors in order; each thread writes 8 consecutive co of one (ci, r', s') row
+// (16-byte store) gathered from w[co][R-1-r'][S-1-s'][ci].  32-bit index math.
+__global__ __launch_bounds__(kBlock) void conv_wt_flip_multi_kernel(WtFlipBatch b) {
+  int i = 0;
+  while (i + 1 < b.count && (int)blockIdx.x >= b.blk0[i + 1]) ++i;
+  const int Cout = b.Cout[i], R = b.R[i], S = b.S[i], C = b.C[i];
+  const uint32_t rows8 = (uint32_t)C * R * S * (Cout / 8);
+  const uint32_t t = (uint32_t)(blockIdx.x - b.blk0[i]) * kBlock + threadIdx.x;
+  if (t >= rows8) return;
+  const uint32_t cog = t % (uint32_t)(Cout / 8);
+  uint32_t q = t / (uint32_t)(Cout / 8);
+  const int s = (int)(q % (uint32_t)S);
+  q /= (uint32_t)S;
+  const int r = (int)(q % (uint32_t)R);
+  const int ci = (int)(q / (uint32_t)R);
+  const uint16_t* w = b.w[i];
+  const uint32_t cstride = (uint32_t)R * S * C;
+  const uint32_t base = ((uint32_t)(R - 1 - r) * S + (S - 1 - s)) * C + ci + cog * 8 * cstride;
+  uint16_t v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = w[base + k * cstride];
+  uint4 o;
+  o.x = v[0] | ((uint32_t)v[1] << 16);
+  o.y = v[2] | ((uint32_t)v[3] << 16);
+  o.z = v[4] | ((uint32_t)v[5] << 16);
+  o.w = v[6] | ((uint32_t)v[7] << 16);
+  *reinterpret_cast<uint4*>(b.wt[i] + (int64_t)t * 8) = o;
+}
+
+void launch_conv_wt_flip_multi(WtFlipBatch b, hipStream_t s) {
+  int blocks = 0;
+  for (int i = 0; i < b.count; ++i) {
+    b.blk0[i] = blocks;
+    const int64_t rows8 = (int64_t)b.C[i] * b.R[i] * b.S[i] * (b.Cout[i] / 8);
+    blocks += (int)((rows8 + kBlock - 1) / kBlock);
+  }
+  if (blocks > 0) hipLaunchKernelGGL(conv_wt_flip_multi_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, b);
+}
+
 bool conv_supported(int C, int Cout) { return C % 64 == 0 && Cout % 64 == 0; }
 
 // Narrow inputs (C = 16 or 32) need the taps of one K-step to be consecutive along s.

@@ -145,6 +145,16 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
                                int C, int R, int S, int pad, const uint16_t* bnx, const float* bn_mean,
                                const float* bn_coef, float* bp1, float* bp2, hipStream_t s,
                                const uint16_t* bny = nullptr, const uint16_t* bnres = nullptr);
+// many weights flipped/transposed (wt[ci][R-1-r][S-1-s][co] = w[co][r][s][ci]) in one launch
+constexpr int kWtFlipMax = 64;
+struct WtFlipBatch {
+  const uint16_t* w[kWtFlipMax];
+  uint16_t* wt[kWtFlipMax];
+  int Cout[kWtFlipMax], R[kWtFlipMax], S[kWtFlipMax], C[kWtFlipMax];
+  int blk0[kWtFlipMax];
+  int count;
+};
+void launch_conv_wt_flip_multi(WtFlipBatch b, hipStream_t s);
 // stride-2 backward-data straight from the KRSC weight w [Cout,R,S,C]: dy [N,Ho,Wo,Cout] -> dx [N,H,W,C]
 void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout,
                           int C, int R, int S, int pad, int H, int W, hipStream_t s);

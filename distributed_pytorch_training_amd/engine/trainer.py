@@ -28,6 +28,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..amp import DeviceGradScaler, autocast
+from ..ops import conv as native_conv
 from ..profiling.timeline import StepTimeline, roctx_range
 
 
@@ -77,6 +78,7 @@ class Trainer:
         self._accum_fresh = True
         self.roctx = bool(getattr(args, "roctx", False))
         self.graphed = None
+        self._native_conv_cache = False
         if self.impl == "native":
             self._init_native(model, comm)
         else:
@@ -91,9 +93,10 @@ class Trainer:
         if (getattr(args, "fused_bn", True) and self.device.type == "cuda"
                 and getattr(args, "channels_last", False)):
             from ..models.layers import fuse_native_layers
-            from ..ops import conv as native_conv
             fuse_native_layers(model)
             native_conv.ENABLED = bool(getattr(args, "native_conv", True))
+        # per-step flip cache of the stride-1 backward-data weights (ops/conv.py)
+        self._native_conv_cache = self.device.type == "cuda" and native_conv.ENABLED
         params_in_order = [p for p in model.parameters() if p.requires_grad]
         self.scaler = DeviceGradScaler(self.device, enabled=self.amp)
         shadow = None
@@ -156,6 +159,8 @@ class Trainer:
     def _native_step(self, images, targets, sync: bool = True):
         tl = self.timeline
         tl.mark("start")
+        if self._native_conv_cache:
+            native_conv.begin_step()  # weights changed since the last step: new flip cache
         ctx = self.ddp.no_sync() if not sync else contextlib.nullcontext()
         rx = self.roctx
         with ctx:
@@ -165,7 +170,11 @@ class Trainer:
             tl.mark("fwd")
             scaled = loss / self.grad_accum if self.grad_accum > 1 else loss
             with roctx_range("backward+allreduce", rx):
-                (self.scaler.scale(scaled) if self.amp else scaled).backward()
+                try:
+                    (self.scaler.scale(scaled) if self.amp else scaled).backward()
+                finally:
+                    if self._native_conv_cache:
+                        native_conv.end_caching()
         tl.mark("bwd")
         if not sync:
             ops.accumulate_metrics(outputs, targets, loss, self.metrics)

@@ -60,19 +60,20 @@ def _backward(ctx, dy):
     if ctx.needs_input_grad[0]:
         src = ctx.bn_src if (s == 1 and BN_BWD_FUSE) else None
         dres = None
+        wt = _flipped(w) if s == 1 else None
         if src is not None and not isinstance(src[2], dict):  # BN+ReLU: (x, mean, coef)
             bn_x, bn_mean, bn_coef = src
-            dx, p1, p2 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, bn_coef)
+            dx, p1, p2 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, bn_coef, w_flipped=wt)
             _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), None)
         elif src is not None and _dres_ok(dres := src[2].pop("dres", None), x):  # (x, mean, slot)
             # block-tail BN+add+ReLU (ops/bn.py pair outputs): the next block's tail already
             # produced the identity-path gradient dres; dx becomes the tail's masked total
             # gradient, the conv's input x is the tail's output y (the ReLU mask)
             bn_x, bn_mean, _ = src
-            dx, p1, p2 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, None, x, dres)
+            dx, p1, p2 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, None, x, dres, wt)
             _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), dres.data_ptr())
         elif s == 1:
-            dx = native().conv_dgrad_flip(dy, w, p)[0]
+            dx = native().conv_dgrad_flip(dy, w, p)[0] if wt is None else native().conv_dgrad_preflipped(dy, wt, p)
         elif s == 2 and S2_DGRAD and x.dim() == 4:
             dx = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3])
         else:
@@ -85,6 +86,41 @@ def _backward(ctx, dy):
         # identity-path gradient to the tail's conv-path consumer (see ops/bn.py)
         ctx.res_slot["dres"] = dx
     return dx, dw
+
+
+# Per-step flip cache: the stride-1 backward-data reads a flipped/transposed weight copy
+# wt[ci][R-1-r][S-1-s][co].  With the cache on (the trainer calls begin_step() each step) the
+# forward registers every such weight and the first backward-data of the step flips them all
+# in ONE launch (46 launches per ResNet-50 step otherwise).
+_FLIP = {"on": False, "pending": {}, "done": {}}
+
+
+def begin_step() -> None:
+    _FLIP["on"] = True
+    _FLIP["pending"].clear()
+    _FLIP["done"].clear()
+
+
+def end_caching() -> None:
+    _FLIP["on"] = False
+    _FLIP["pending"].clear()
+    _FLIP["done"].clear()
+
+
+def _flipped(w: torch.Tensor):
+    if not _FLIP["on"]:
+        return None
+    key = (w.data_ptr(), tuple(w.shape))
+    wt = _FLIP["done"].get(key)
+    if wt is None:
+        pend = _FLIP["pending"]
+        pend.setdefault(key, w)
+        keys = list(pend.keys())
+        for k, t in zip(keys, native().conv_wt_flip_multi([pend[k] for k in keys])):
+            _FLIP["done"][k] = t
+        pend.clear()
+        wt = _FLIP["done"][key]
+    return wt
 
 
 def _dres_ok(dres, x) -> bool:
@@ -126,6 +162,8 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bo
     BatchNorm partial sums as ``y._dpt_bn_partials`` (consumed by ops/bn.py).  ``out_hw``:
     explicit output size (asymmetric padding: top/left ``pad``, bottom/right what fits)."""
     w = _cl(w)
+    if _FLIP["on"] and int(stride) == 1 and x.requires_grad:
+        _FLIP["pending"].setdefault((w.data_ptr(), tuple(w.shape)), w)
     # (BN input, mean, coef) of the fused BN+ReLU that produced x, if any (ops/bn.py)
     bn_src = x.__dict__.get("_dpt_bn_src")
     # x is the identity alias of a fused block tail (this conv is a downsample)

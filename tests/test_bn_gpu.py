@@ -49,7 +49,11 @@ def test_fused_bn_train_matches_reference(cuda, dtype, shape, relu, res):
     y.backward(gy)
     # reference backward through the same (rounded) output mask
     yr.backward(gy.float())
-    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=rt * 4, atol=at * 4)
+    # ...and the backward recomputes the mask as fma(x, a, b) > 0 in fp32 (ops/bn.py), which can
+    # still disagree with the rounded y at |z| ~ 0 (e.g. a positive z that rounds to +0): those
+    # elements' own gradients are a tie, not compared (their effect on the sums is negligible)
+    keep = zr.detach().abs() > 1e-2 if relu else torch.ones_like(zr, dtype=torch.bool)
+    torch.testing.assert_close(x.grad.float()[keep], xr.grad[keep], rtol=rt * 4, atol=at * 4)
     torch.testing.assert_close(bn.weight.grad, w.grad, rtol=rt * 4, atol=at * 20 * (shape[0] * shape[2] * shape[3]) ** 0.5)
     torch.testing.assert_close(bn.bias.grad, b.grad, rtol=rt * 4, atol=at * 20 * (shape[0] * shape[2] * shape[3]) ** 0.5)
     if res:

@@ -327,3 +327,21 @@ def test_block_tail_backward_folded_into_dgrad_epilogue(cuda, monkeypatch, ds):
     assert not nc._BNB_PARTIALS
     for a, b in zip(*grads):
         torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item() + 1e-6)
+
+
+def test_weight_flip_multi_and_preflipped_dgrad(cuda):
+    """The per-step flip cache (ops/conv.py): every weight flipped in one launch equals the
+    per-weight flip, and backward-data through it equals the flip-copy path."""
+    shapes = [(64, 64, 1), (128, 64, 3), (256, 128, 1), (64, 192, 3), (2048, 512, 1)]
+    ws = []
+    for i, (co, ci, k) in enumerate(shapes):
+        g = torch.Generator(device=cuda).manual_seed(40 + i)
+        ws.append(torch.randn(co, ci, k, k, device=cuda, generator=g).to(torch.bfloat16)
+                  .contiguous(memory_format=CL))
+    wts = ops.native().conv_wt_flip_multi(ws)
+    for w, wt in zip(ws, wts):
+        assert wt.is_contiguous(memory_format=CL)
+        assert torch.equal(wt, w.flip(2, 3).transpose(0, 1).contiguous(memory_format=CL))
+    w, wt = ws[1], wts[1]
+    gy = torch.randn(2, 128, 9, 9, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    assert torch.equal(ops.native().conv_dgrad_preflipped(gy, wt, 1), ops.native().conv_dgrad_flip(gy, w, 1)[0])
