@@ -279,7 +279,8 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t pad) {
 std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor bn_x, Tensor bn_mean,
                                        c10::optional<Tensor> bn_coef,
                                        c10::optional<Tensor> bn_y, c10::optional<Tensor> bn_res,
-                                       c10::optional<Tensor> w_flipped) {
+                                       c10::optional<Tensor> w_flipped, c10::optional<Tensor> bn_x2,
+                                       c10::optional<Tensor> bn_mean2) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
   check_cl_bf16(bn_x, "bn_x");
@@ -310,6 +311,13 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
   const int mt = dpt::conv_m_tiles((int64_t)N * H * W);
   auto p1 = at::empty({C, mt}, dy.options().dtype(at::kFloat));
   auto p2 = at::empty({C, mt}, dy.options().dtype(at::kFloat));
+  const bool two = bn_x2.has_value() && bn_x2->defined();
+  if (two) {
+    TORCH_CHECK(res, "conv_dgrad_bnstats: bn_x2 needs bn_y / bn_res");
+    check_cl_bf16(*bn_x2, "bn_x2");
+    TORCH_CHECK(bn_x2->sizes() == bn_x.sizes(), "conv_dgrad_bnstats: bn_x2 must match bn_x");
+  }
+  auto p3 = at::empty({two ? C : 0, two ? mt : 0}, dy.options().dtype(at::kFloat));
   c10::hip::HIPGuard guard(dy.device().index());
   auto st = cur_stream(dy);
   if (!pre)
@@ -321,8 +329,11 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
                                  f32_param(bn_mean, C, "bn_mean"), f32_param(bn_coef, 2 * C, "bn_coef"),
                                  p1.data_ptr<float>(), p2.data_ptr<float>(), st,
                                  res ? reinterpret_cast<const uint16_t*>(bn_y->data_ptr()) : nullptr,
-                                 res ? reinterpret_cast<const uint16_t*>(bn_res->data_ptr()) : nullptr);
-  return {dx, p1, p2};
+                                 res ? reinterpret_cast<const uint16_t*>(bn_res->data_ptr()) : nullptr,
+                                 two ? reinterpret_cast<const uint16_t*>(bn_x2->data_ptr()) : nullptr,
+                                 two ? f32_param(bn_mean2, C, "bn_mean2") : nullptr,
+                                 two ? p3.data_ptr<float>() : nullptr);
+  return {dx, p1, p2, p3};
 }
 
 // Stride-2 backward-data: dx [N, C, H, W] (channels_last) of y = conv2d(x, w, stride 2, pad).
@@ -509,7 +520,7 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::
                                  c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
                                  c10::optional<Tensor> running_var, c10::optional<Tensor> num_batches,
                                  double momentum, double eps, bool relu, c10::optional<Tensor> psum,
-                                 c10::optional<Tensor> psq) {
+                                 c10::optional<Tensor> psq, bool apply) {
   auto [M, C] = bn_rows(x, "x");
   TORCH_CHECK(dpt::bn_supported(C), "fused BN: unsupported channel count ", C);
   const void* rp = nullptr;
@@ -523,7 +534,9 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::
     TORCH_CHECK(num_batches->is_cuda() && num_batches->scalar_type() == at::kLong, "num_batches must be int64 GPU");
     nb = num_batches->data_ptr<int64_t>();
   }
-  auto y = at::empty_like(x);
+  // apply = false: statistics, running-stat update and coefficients only (y is empty)
+  auto y = apply ? at::empty_like(x) : at::empty({0}, x.options());
+  void* yp = apply ? y.data_ptr() : nullptr;
   auto fopt = x.options().dtype(at::kFloat);
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
   auto coef = at::empty({2 * C}, fopt);  // [a | b]: y = relu(x*a + b [+ r]); lets bn_bwd skip reading y
@@ -534,7 +547,7 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::
     TORCH_CHECK(psum->is_cuda() && psum->scalar_type() == at::kFloat && psum->dim() == 2 && psum->size(0) == C &&
                     psum->is_contiguous() && psq->sizes() == psum->sizes() && psq->is_contiguous(),
                 "bn_fwd_train: partials must be contiguous fp32 [C, chunks]");
-    dpt::launch_bn_fwd_from_partials(bn_dtype(x), x.data_ptr(), rp, y.data_ptr(), M, C, psum->data_ptr<float>(),
+    dpt::launch_bn_fwd_from_partials(bn_dtype(x), x.data_ptr(), rp, yp, M, C, psum->data_ptr<float>(),
                                      psq->data_ptr<float>(), (int)psum->size(1), f32_param(weight, C, "weight"),
                                      f32_param(bias, C, "bias"), (float)eps, (float)momentum,
                                      f32_param(running_mean, C, "running_mean"),
@@ -543,12 +556,57 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::
     return {y, mean, invstd, coef};
   }
   auto ws = at::empty({dpt::bn_workspace_floats(M, C)}, fopt);
-  dpt::launch_bn_fwd_train(bn_dtype(x), x.data_ptr(), rp, y.data_ptr(), M, C, f32_param(weight, C, "weight"),
+  dpt::launch_bn_fwd_train(bn_dtype(x), x.data_ptr(), rp, yp, M, C, f32_param(weight, C, "weight"),
                            f32_param(bias, C, "bias"), (float)eps, (float)momentum,
                            f32_param(running_mean, C, "running_mean"), f32_param(running_var, C, "running_var"), nb,
                            mean.data_ptr<float>(), invstd.data_ptr<float>(), coef.data_ptr<float>(),
                            ws.data_ptr<float>(), relu, cur_stream(x));
   return {y, mean, invstd, coef};
+}
+
+// y = relu(x*a + b + x2*a2 + b2), coef = [a | b], coef2 = [a2 | b2] (bn_fwd_train coefficients)
+Tensor bn_apply_aff(Tensor x, Tensor x2, Tensor coef, Tensor coef2) {
+  auto [M, C] = bn_rows(x, "x");
+  TORCH_CHECK(dpt::bn_supported(C), "fused BN: unsupported channel count ", C);
+  TORCH_CHECK(x2.sizes() == x.sizes() && x2.scalar_type() == x.scalar_type(), "bn_apply_aff: x2 mismatch");
+  bn_rows(x2, "x2");
+  const float* a = f32_param(coef, 2 * C, "coef");
+  const float* a2 = f32_param(coef2, 2 * C, "coef2");
+  auto y = at::empty_like(x);
+  c10::hip::HIPGuard guard(x.device().index());
+  dpt::launch_bn_apply_aff(bn_dtype(x), x.data_ptr(), x2.data_ptr(), y.data_ptr(), M, C, a, a + C, a2, a2 + C,
+                           cur_stream(x));
+  return y;
+}
+
+// Backward of bn_apply_aff + ReLU from dgrad-epilogue partials (dz already masked): {dx, dx2,
+// dgamma, dbeta, dgamma2, dbeta2}.
+std::vector<Tensor> bn2_bwd_partials(Tensor dz, Tensor x, Tensor x2, c10::optional<Tensor> weight,
+                                     c10::optional<Tensor> weight2, Tensor mean, Tensor invstd, Tensor mean2,
+                                     Tensor invstd2, Tensor p1, Tensor p2, Tensor p3, bool want_dparams) {
+  auto [M, C] = bn_rows(x, "x");
+  TORCH_CHECK(dz.sizes() == x.sizes() && x2.sizes() == x.sizes() && dz.scalar_type() == x.scalar_type() &&
+                  x2.scalar_type() == x.scalar_type(), "bn2_bwd_partials: shape/dtype mismatch");
+  bn_rows(dz, "dz");
+  bn_rows(x2, "x2");
+  for (const Tensor* t : {&p1, &p2, &p3})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->dim() == 2 && t->size(0) == C &&
+                    t->is_contiguous() && t->sizes() == p1.sizes(), "bn2_bwd_partials: partials must be fp32 [C, chunks]");
+  auto fopt = x.options().dtype(at::kFloat);
+  auto dx = at::empty_like(x), dx2 = at::empty_like(x2);
+  Tensor dg = want_dparams ? at::empty({C}, fopt) : Tensor(), db = want_dparams ? at::empty({C}, fopt) : Tensor();
+  Tensor dg2 = want_dparams ? at::empty({C}, fopt) : Tensor(), db2 = want_dparams ? at::empty({C}, fopt) : Tensor();
+  auto kbuf = at::empty({6 * C}, fopt);
+  c10::hip::HIPGuard guard(x.device().index());
+  dpt::launch_bn2_bwd_from_partials(
+      bn_dtype(x), dz.data_ptr(), x.data_ptr(), x2.data_ptr(), M, C, f32_param(weight, C, "weight"),
+      f32_param(mean, C, "mean"), f32_param(invstd, C, "invstd"), f32_param(weight2, C, "weight2"),
+      f32_param(mean2, C, "mean2"), f32_param(invstd2, C, "invstd2"), p1.data_ptr<float>(), p2.data_ptr<float>(),
+      p3.data_ptr<float>(), (int)p1.size(1), want_dparams ? dg.data_ptr<float>() : nullptr,
+      want_dparams ? db.data_ptr<float>() : nullptr, want_dparams ? dg2.data_ptr<float>() : nullptr,
+      want_dparams ? db2.data_ptr<float>() : nullptr, dx.data_ptr(), dx2.data_ptr(), kbuf.data_ptr<float>(),
+      cur_stream(x));
+  return {dx, dx2, dg, db, dg2, db2};
 }
 
 Tensor bn_apply(Tensor x, c10::optional<Tensor> residual, Tensor a, Tensor b, bool relu) {
@@ -887,8 +945,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_supported", [](int64_t C) { return dpt::bn_supported(C); });
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("residual"), py::arg("weight"), py::arg("bias"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches"), py::arg("momentum"), py::arg("eps"),
-        py::arg("relu"), py::arg("psum") = py::none(), py::arg("psq") = py::none());
+        py::arg("relu"), py::arg("psum") = py::none(), py::arg("psq") = py::none(), py::arg("apply") = true);
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("residual"), py::arg("a"), py::arg("b"), py::arg("relu"));
+  m.def("bn_apply_aff", &bn_apply_aff, py::arg("x"), py::arg("x2"), py::arg("coef"), py::arg("coef2"));
+  m.def("bn2_bwd_partials", &bn2_bwd_partials, py::arg("dz"), py::arg("x"), py::arg("x2"), py::arg("weight"),
+        py::arg("weight2"), py::arg("mean"), py::arg("invstd"), py::arg("mean2"), py::arg("invstd2"), py::arg("p1"),
+        py::arg("p2"), py::arg("p3"), py::arg("want_dparams"));
   m.def("bn_bwd", &bn_bwd, py::arg("grad_output"), py::arg("grad_output2"), py::arg("y"), py::arg("x"),
         py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("relu"), py::arg("want_dz"),
         py::arg("want_dparams"), py::arg("coef") = py::none());
@@ -919,7 +981,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("conv_dgrad_bnstats", &conv_dgrad_bnstats, py::arg("grad_output"), py::arg("w"), py::arg("pad"),
         py::arg("bn_x"), py::arg("bn_mean"), py::arg("bn_coef"), py::arg("bn_y") = py::none(),
-        py::arg("bn_res") = py::none(), py::arg("w_flipped") = py::none());
+        py::arg("bn_res") = py::none(), py::arg("w_flipped") = py::none(), py::arg("bn_x2") = py::none(),
+        py::arg("bn_mean2") = py::none());
   m.def("conv_wt_flip_multi", &conv_wt_flip_multi, py::arg("ws"));
   m.def("conv_dgrad_preflipped", &conv_dgrad_preflipped, py::arg("grad_output"), py::arg("w_flipped"), py::arg("pad"));
   m.def("bn_bwd_partials", &bn_bwd_partials, py::arg("grad_output"), py::arg("x"), py::arg("weight"), py::arg("mean"),

@@ -267,18 +267,27 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_finalize_wide_kernel(
 }
 
 // ---- forward apply: y = relu(x*a + b [+ r]) --------------------------------------------------
-template <typename IO, bool RELU, bool RES>
+// AFF: the residual is itself a BatchNorm input (a residual block's downsample branch): y =
+// relu(x*a + b + r*a2 + b2) - the downsample BN's output is never materialised.
+template <typename IO, bool RELU, bool RES, bool AFF = false>
 __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(const void* __restrict__ x,
                                                               const void* __restrict__ res,
                                                               void* __restrict__ y,
                                                               const float* __restrict__ coef_a,
                                                               const float* __restrict__ coef_b,
-                                                              int64_t M, int C, int rev) {
+                                                              int64_t M, int C, int rev,
+                                                              const float* __restrict__ coef_a2 = nullptr,
+                                                              const float* __restrict__ coef_b2 = nullptr) {
   const int tpr = C >> 3, rpi = kBlock / tpr;
   const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
-  float a[8], b[8];
+  float a[8], b[8], a2[8], b2[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { a[k] = coef_a[cg * 8 + k]; b[k] = coef_b[cg * 8 + k]; }
+  for (int k = 0; k < 8; ++k) {
+    a[k] = coef_a[cg * 8 + k];
+    b[k] = coef_b[cg * 8 + k];
+    a2[k] = AFF ? coef_a2[cg * 8 + k] : 0.f;
+    b2[k] = AFF ? coef_b2[cg * 8 + k] : 0.f;
+  }
   const int64_t stride = (int64_t)gridDim.x * rpi;
   for (int64_t rf = (int64_t)blockIdx.x * rpi + rr; rf < M; rf += 2 * stride) {
     const bool two = rf + stride < M;
@@ -297,7 +306,13 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(const void* __rest
     for (int k = 0; k < 8; ++k) {
       float o0 = __builtin_fmaf(v0[k], a[k], b[k]);  // bwd mask-from-x recomputes exactly this
       float o1 = __builtin_fmaf(v1[k], a[k], b[k]);
-      if (RES) { o0 += q0[k]; o1 += q1[k]; }
+      if (RES && AFF) {
+        o0 += __builtin_fmaf(q0[k], a2[k], b2[k]);
+        o1 += __builtin_fmaf(q1[k], a2[k], b2[k]);
+      } else if (RES) {
+        o0 += q0[k];
+        o1 += q1[k];
+      }
       if (RELU) {  // NaN-propagating like torch.relu (a NaN must still reach the AMP check)
         o0 = o0 < 0.0f ? 0.0f : o0;
         o1 = o1 < 0.0f ? 0.0f : o1;
@@ -479,6 +494,46 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const void* __rest
   }
 }
 
+// Block tail with a downsample branch (ops/bn.py _BN2AddReLUPair): one pass over dz writes both
+// BatchNorms' input gradients, dx = k1*dz + k2*(x - mean) + k3 and dx2 = j1*dz + j2*(x2 - mean2) + j3.
+template <typename IO>
+__global__ __launch_bounds__(kBlock) void bn_bwd_apply2_kernel(const void* __restrict__ dz,
+                                                               const void* __restrict__ x,
+                                                               const void* __restrict__ x2,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ mean2,
+                                                               const float* __restrict__ k,
+                                                               const float* __restrict__ j, void* dx, void* dx2,
+                                                               int64_t M, int C, int rev) {
+  const int tpr = C >> 3, rpi = kBlock / tpr;
+  const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
+  float mu[8], mu2[8], c1[8], c2[8], c3[8], e1[8], e2[8], e3[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int c = cg * 8 + q;
+    mu[q] = mean[c];
+    mu2[q] = mean2[c];
+    c1[q] = k[c]; c2[q] = k[C + c]; c3[q] = k[2 * C + c];
+    e1[q] = j[c]; e2[q] = j[C + c]; e3[q] = j[2 * C + c];
+  }
+  const int64_t stride = (int64_t)gridDim.x * rpi;
+  for (int64_t rf = (int64_t)blockIdx.x * rpi + rr; rf < M; rf += stride) {
+    const int64_t r = rev ? M - 1 - rf : rf;
+    const int64_t off = r * C + cg * 8;
+    float g[8], xv[8], x2v[8], o[8], o2[8];
+    IO::load8(dz, off, g);
+    IO::load8(x, off, xv);
+    IO::load8(x2, off, x2v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      o[q] = c1[q] * g[q] + c2[q] * (xv[q] - mu[q]) + c3[q];
+      o2[q] = e1[q] * g[q] + e2[q] * (x2v[q] - mu2[q]) + e3[q];
+    }
+    IO::store8(dx, off, o);
+    IO::store8(dx2, off, o2);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
@@ -546,6 +601,7 @@ void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int
   }
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, psum, psq, g.chunks, (int)C, M,
                      gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd, ca, cb);
+  if (y == nullptr) return;  // statistics only (the apply is fused elsewhere)
   switch (dtype) {
     case 0: fwd_apply_dispatch<F32>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
     case 1: fwd_apply_dispatch<BF16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
@@ -570,6 +626,7 @@ void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), dim3(kBlock), 0, s, psum, psq, chunks,
                        (int)C, M, gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd,
                        ca, cb);
+  if (y == nullptr) return;  // statistics only (the apply is fused elsewhere)
   switch (dtype) {
     case 0: fwd_apply_dispatch<F32>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
     case 1: fwd_apply_dispatch<BF16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
@@ -719,6 +776,48 @@ void launch_bn_bwd_from_partials(int dtype, const void* dy, const void* x, int64
     case 0: hipLaunchKernelGGL((bn_bwd_apply_kernel<F32, true, false, true>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
     case 1: hipLaunchKernelGGL((bn_bwd_apply_kernel<BF16, true, false, true>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
     default: hipLaunchKernelGGL((bn_bwd_apply_kernel<F16, true, false, true>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
+  }
+}
+
+void launch_bn_apply_aff(int dtype, const void* x, const void* x2, void* y, int64_t M, int64_t C, const float* a,
+                         const float* b, const float* a2, const float* b2, hipStream_t s) {
+  BnGeometry g = bn_geometry(M, C);
+  dim3 gr(g.apply_blocks), bl(kBlock);
+  switch (dtype) {
+    case 0: hipLaunchKernelGGL((bn_fwd_apply_kernel<F32, true, true, true>), gr, bl, 0, s, x, x2, y, a, b, M, (int)C, kBnReverse, a2, b2); break;
+    case 1: hipLaunchKernelGGL((bn_fwd_apply_kernel<BF16, true, true, true>), gr, bl, 0, s, x, x2, y, a, b, M, (int)C, kBnReverse, a2, b2); break;
+    default: hipLaunchKernelGGL((bn_fwd_apply_kernel<F16, true, true, true>), gr, bl, 0, s, x, x2, y, a, b, M, (int)C, kBnReverse, a2, b2); break;
+  }
+}
+
+// Two BatchNorms fed the same (masked) output gradient dz: the block tail (input x, statistics
+// s1 = sum dz, s2 = sum dz*(x - mean)) and its downsample branch (input x2, s1 and s3 = sum
+// dz*(x2 - mean2)), partials [C][chunks] from the consuming conv's dgrad epilogue.
+void launch_bn2_bwd_from_partials(int dtype, const void* dz, const void* x, const void* x2, int64_t M, int64_t C,
+                                  const float* gamma, const float* mean, const float* invstd, const float* gamma2,
+                                  const float* mean2, const float* invstd2, const float* p1, const float* p2,
+                                  const float* p3, int chunks, float* dgamma, float* dbeta, float* dgamma2,
+                                  float* dbeta2, void* dx, void* dx2, float* kbuf, hipStream_t s) {
+  BnGeometry g = bn_geometry(M, C);
+  float* k = kbuf;          // [3C] tail
+  float* j = kbuf + 3 * C;  // [3C] downsample
+  dim3 bl(kBlock);
+  if (chunks > 256) {
+    hipLaunchKernelGGL(bn_bwd_finalize_wide_kernel, dim3((unsigned)C), bl, 0, s, p1, p2, chunks, (int)C, M, gamma,
+                       invstd, dgamma, dbeta, k, k + C, k + 2 * C);
+    hipLaunchKernelGGL(bn_bwd_finalize_wide_kernel, dim3((unsigned)C), bl, 0, s, p1, p3, chunks, (int)C, M, gamma2,
+                       invstd2, dgamma2, dbeta2, j, j + C, j + 2 * C);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p2, chunks, (int)C, M,
+                       gamma, invstd, dgamma, dbeta, k, k + C, k + 2 * C);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p3, chunks, (int)C, M,
+                       gamma2, invstd2, dgamma2, dbeta2, j, j + C, j + 2 * C);
+  }
+  dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
+  switch (dtype) {
+    case 0: hipLaunchKernelGGL(bn_bwd_apply2_kernel<F32>, ga, bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, kBnReverse); break;
+    case 1: hipLaunchKernelGGL(bn_bwd_apply2_kernel<BF16>, ga, bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, kBnReverse); break;
+    default: hipLaunchKernelGGL(bn_bwd_apply2_kernel<F16>, ga, bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, kBnReverse); break;
   }
 }
 

@@ -74,6 +74,11 @@ struct ConvFwdArgs {
   // next block's identity path
   const uint16_t* bny;    // its output y (ReLU mask)
   const uint16_t* bnres;  // the identity-path gradient (added before the mask)
+  // BNR with a downsample branch: the block's identity path was BN2(x2) (folded into the tail,
+  // ops/bn.py _BN2AddReLUPair): also sum s3 = sum dz*(x2 - mean2) for that BatchNorm
+  const uint16_t* bnx2;
+  const float* bn_mean2;
+  float* bp3;
   // BKN tap map: GEMM tap (r, s) reads weight tap (tr0 + trs*r, ts0 + tss*s) of the Rw x Sw
   // weight (stride-1 backward-data: the flip R-1-r; strided backward-data: one parity class)
   int Rw, Sw, tr0, trs, ts0, tss;
@@ -112,8 +117,9 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 // REMAP (LDS epilogue): output rows scattered to one stride-2 parity class of a larger image
 // (strided backward-data); ZSIB: also write zeros to the other three positions of each 2x2
 // cell (1x1 / stride-2 backward-data, whose other classes receive no gradient).
+// BNR2 (with BNR): the downsample-branch statistic s3 too (p.bnx2 / bn_mean2 / bp3).
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
-          bool BNR = false, bool REMAP = false, bool ZSIB = false>
+          bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false>
 __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
   constexpr int BM = BMT;
@@ -348,7 +354,8 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
     // store of the group (the output may alias nothing, but the compiler cannot know that)
     constexpr int GRP = NPASS < 4 ? NPASS : 4;
     const int oc = tid % CPR, orow = tid / CPR;
-    float ba[8], bb[8], bm[8], s1[8], s2[8];
+    float ba[8], bb[8], bm[8], s1[8], s2[8], bm2[8], s3[8];
+    constexpr bool two = BNR && BNR2;
     if (BNB) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -356,13 +363,15 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
         ba[k] = BNR ? 0.f : p.bn_coef[c];
         bb[k] = BNR ? 0.f : p.bn_coef[p.Cout + c];
         bm[k] = p.bn_mean[c];
+        bm2[k] = two ? p.bn_mean2[c] : 0.f;
         s1[k] = 0.f;
         s2[k] = 0.f;
+        s3[k] = 0.f;
       }
     }
 #pragma unroll
     for (int g0 = 0; g0 < NPASS; g0 += GRP) {
-      uint4 xv[GRP], yv[GRP], rv[GRP];
+      uint4 xv[GRP], yv[GRP], rv[GRP], x2v[GRP];
       if (BNB) {
 #pragma unroll
         for (int q = 0; q < GRP; ++q) {
@@ -372,6 +381,8 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
           if (BNR) {
             yv[q] = *reinterpret_cast<const uint4*>(p.bny + off);
             rv[q] = *reinterpret_cast<const uint4*>(p.bnres + off);
+            if (two) x2v[q] = *reinterpret_cast<const uint4*>(p.bnx2 + off);
+            else x2v[q] = make_uint4(0u, 0u, 0u, 0u);
           }
         }
       }
@@ -386,6 +397,7 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
             const uint32_t xu[4] = {xv[q].x, xv[q].y, xv[q].z, xv[q].w};
             const uint32_t yu[4] = {yv[q].x, yv[q].y, yv[q].z, yv[q].w};
             const uint32_t ru[4] = {rv[q].x, rv[q].y, rv[q].z, rv[q].w};
+            const uint32_t x2u[4] = {x2v[q].x, x2v[q].y, x2v[q].z, x2v[q].w};
             uint32_t du[4];
 #pragma unroll
             for (int k2 = 0; k2 < 4; ++k2) {
@@ -407,6 +419,10 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
                 dzp[h] = dz;
                 s1[k] += dz;
                 s2[k] = __builtin_fmaf(dz, x - bm[k], s2[k]);
+                if (two) {
+                  const float x2 = __uint_as_float((x2u[k2] << sh) & 0xffff0000u);
+                  s3[k] = __builtin_fmaf(dz, x2 - bm2[k], s3[k]);
+                }
               }
               if (BNR) {
                 const f32x2_t d2 = {dzp[0], dzp[1]};
@@ -446,24 +462,32 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
         for (int off = CPR; off < 64; off <<= 1) {
           s1[k] += __shfl_xor(s1[k], off, 64);
           s2[k] += __shfl_xor(s2[k], off, 64);
+          if (two) s3[k] += __shfl_xor(s3[k], off, 64);
         }
       }
       __syncthreads();
-      float* bred = reinterpret_cast<float*>(lds);  // [4 waves][2][BN]
+      constexpr int NS3 = two ? 3 : 2;
+      float* bred = reinterpret_cast<float*>(lds);  // [4 waves][NS3][BN]
       if (lane < CPR) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          bred[(wid * 2) * BN + oc * 8 + k] = s1[k];
-          bred[(wid * 2 + 1) * BN + oc * 8 + k] = s2[k];
+          bred[(wid * NS3) * BN + oc * 8 + k] = s1[k];
+          bred[(wid * NS3 + 1) * BN + oc * 8 + k] = s2[k];
+          if (two) bred[(wid * NS3 + 2) * BN + oc * 8 + k] = s3[k];
         }
       }
       __syncthreads();
       if (tid < BN) {
-        float a = 0.f, b = 0.f;
+        float a = 0.f, b = 0.f, c3 = 0.f;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) { a += bred[(w * 2) * BN + tid]; b += bred[(w * 2 + 1) * BN + tid]; }
+        for (int w = 0; w < 4; ++w) {
+          a += bred[(w * NS3) * BN + tid];
+          b += bred[(w * NS3 + 1) * BN + tid];
+          if (two) c3 += bred[(w * NS3 + 2) * BN + tid];
+        }
         p.bp1[(int64_t)(n0 + tid) * p.m_tiles + mt] = a;
         p.bp2[(int64_t)(n0 + tid) * p.m_tiles + mt] = b;
+        if (two) p.bp3[(int64_t)(n0 + tid) * p.m_tiles + mt] = c3;
       }
     }
   }
@@ -1140,7 +1164,8 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
 void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int Ho, int Wo, int Cout,
                                int C, int R, int S, int pad, const uint16_t* bnx, const float* bn_mean,
                                const float* bn_coef, float* bp1, float* bp2, hipStream_t s,
-                               const uint16_t* bny, const uint16_t* bnres) {
+                               const uint16_t* bny, const uint16_t* bnres, const uint16_t* bnx2,
+                               const float* bn_mean2, float* bp3) {
   ConvFwdArgs a;
   a.x = dy; a.w = wt; a.y = dx; a.psum = nullptr; a.psq = nullptr;
   a.N = N; a.H = Ho; a.W = Wo; a.C = Cout; a.Cout = C; a.R = R; a.S = S; a.stride = 1; a.pad = R - 1 - pad;
@@ -1151,15 +1176,19 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
   a.mt256 = 0;
   a.bnx = bnx; a.bn_mean = bn_mean; a.bn_coef = bn_coef; a.bp1 = bp1; a.bp2 = bp2;
   a.bny = bny; a.bnres = bnres;
+  a.bnx2 = bnx2; a.bn_mean2 = bn_mean2; a.bp3 = bp3;
   const bool res = bny != nullptr;
   const dim3 block(conv::kThreads);
   a.n_tiles = C % 128 == 0 ? C / 128 : C / 64;
   const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
+  const bool two = res && bnx2 != nullptr;
   if (C % 128 == 0) {
-    if (res) hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, false, false, true, true>), grid, block, 0, s, a);
+    if (two) hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, false, false, true, true, false, false, true>), grid, block, 0, s, a);
+    else if (res) hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, false, false, true, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, false, false, true>), grid, block, 0, s, a);
   } else {
-    if (res) hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, true, false, false, true, true>), grid, block, 0, s, a);
+    if (two) hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, true, false, false, true, true, false, false, true>), grid, block, 0, s, a);
+    else if (res) hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, true, false, false, true, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, true, false, false, true>), grid, block, 0, s, a);
   }
 }
@@ -1214,6 +1243,7 @@ void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, i
       a.ts0 = s0[pw] + 2 * (Js[pw] - 1); a.tss = -2;
       a.oH = H; a.oW = W; a.oph = ph; a.opw = pw;
       a.bnx = nullptr; a.bny = nullptr; a.bnres = nullptr; a.bn_mean = nullptr; a.bn_coef = nullptr;
+      a.bnx2 = nullptr; a.bn_mean2 = nullptr; a.bp3 = nullptr;
       a.bp1 = nullptr; a.bp2 = nullptr;
       const bool z = zsib && ph == 0 && pw == 0;
       const dim3 block(conv::kThreads);

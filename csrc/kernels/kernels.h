@@ -65,6 +65,16 @@ void launch_bn_bwd_from_partials(int dtype, const void* dy, const void* x, int64
                                  const float* mean, const float* invstd, const float* coef, const float* p1,
                                  const float* p2, int chunks, float* dgamma, float* dbeta, void* dx, float* kbuf,
                                  hipStream_t s, bool from_dz = false);
+// y = relu(x*a + b + x2*a2 + b2) (block tail with its downsample BatchNorm folded in)
+void launch_bn_apply_aff(int dtype, const void* x, const void* x2, void* y, int64_t M, int64_t C, const float* a,
+                         const float* b, const float* a2, const float* b2, hipStream_t s);
+// backward of that: finalize both BNs from dgrad-epilogue partials (p1 shared), one apply pass
+// writing dx and dx2; kbuf: 6C floats
+void launch_bn2_bwd_from_partials(int dtype, const void* dz, const void* x, const void* x2, int64_t M, int64_t C,
+                                  const float* gamma, const float* mean, const float* invstd, const float* gamma2,
+                                  const float* mean2, const float* invstd2, const float* p1, const float* p2,
+                                  const float* p3, int chunks, float* dgamma, float* dbeta, float* dgamma2,
+                                  float* dbeta2, void* dx, void* dx2, float* kbuf, hipStream_t s);
 void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                      const float* coef_a, const float* coef_b, bool relu, hipStream_t s);
 void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, const void* x, int64_t M,
@@ -144,7 +154,9 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
 void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int Ho, int Wo, int Cout,
                                int C, int R, int S, int pad, const uint16_t* bnx, const float* bn_mean,
                                const float* bn_coef, float* bp1, float* bp2, hipStream_t s,
-                               const uint16_t* bny = nullptr, const uint16_t* bnres = nullptr);
+                               const uint16_t* bny = nullptr, const uint16_t* bnres = nullptr,
+                               const uint16_t* bnx2 = nullptr, const float* bn_mean2 = nullptr,
+                               float* bp3 = nullptr);
 // many weights flipped/transposed (wt[ci][R-1-r][S-1-s][co] = w[co][r][s][ci]) in one launch
 constexpr int kWtFlipMax = 64;
 struct WtFlipBatch {

@@ -10,6 +10,7 @@ unchanged.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -55,14 +56,48 @@ def bn_act(bn: nn.Module, x: torch.Tensor, relu: bool = True,
     return F.relu(out, inplace=True) if relu else out
 
 
-def bn_act_block_out(bn: nn.Module, x: torch.Tensor, residual: torch.Tensor):
+class DeferredBN:
+    """A downsample branch whose BatchNorm is not applied yet: ``bn(x)`` is folded into the block
+    tail by ``bn_act_block_out`` (ops/bn.py ``_BN2AddReLUPair``) and never materialised."""
+
+    __slots__ = ("bn", "x")
+
+    def __init__(self, bn: nn.Module, x: torch.Tensor) -> None:
+        self.bn, self.x = bn, x
+
+    def materialize(self) -> torch.Tensor:
+        return self.bn(self.x)
+
+
+# 0 disables folding the downsample BatchNorm into the block tail (A/B)
+DS_FUSE = os.environ.get("DPT_DS_FUSE", "1") != "0"
+
+
+def downsample_branch(ds: nn.Module, x: torch.Tensor, tail_bn: nn.Module):
+    """``ds(x)`` for a (conv, BatchNorm) downsample; a ``DeferredBN`` when the block tail can
+    apply that BatchNorm itself (both fused BNs, training)."""
+    if (DS_FUSE and isinstance(ds, nn.Sequential) and len(ds) == 2 and isinstance(ds[1], FusedBatchNorm2d)
+            and isinstance(tail_bn, FusedBatchNorm2d) and ds[1].training and tail_bn.training
+            and torch.is_grad_enabled()):
+        h = ds[0](x)
+        return DeferredBN(ds[1], h) if ds[1].can_fuse(h) else ds[1](h)
+    return ds(x)
+
+
+def bn_act_block_out(bn: nn.Module, x: torch.Tensor, residual):
     """Residual-block tail ``relu(bn(x) + residual)``.
 
     With a fused BN it returns ``(y_conv, y_identity)``: two aliases of the output whose
     gradients reach the fused backward separately (see ops/bn.py ``_BNActTrainPair``); the
     next block feeds the first to its conv path and the second to its identity path.
-    Otherwise it returns the plain tensor.
+    Otherwise it returns the plain tensor.  ``residual`` may be a ``DeferredBN`` (downsample
+    branch): both BatchNorms then run as one fused op.
     """
+    if isinstance(residual, DeferredBN):
+        if (isinstance(bn, FusedBatchNorm2d) and bn.can_fuse(x) and bn.training
+                and residual.x.shape == x.shape and residual.x.dtype == x.dtype):
+            return fused_bn.bn2_add_relu_train(x, bn, residual.x, residual.bn)
+        residual = residual.materialize()
     if isinstance(bn, FusedBatchNorm2d) and bn.can_fuse(x):
         return bn.act(x, True, residual, pair=True)
     return bn_act(bn, x, True, residual)

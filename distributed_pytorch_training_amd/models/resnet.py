@@ -25,7 +25,7 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
-from .layers import bn_act, bn_act_block_out, split_block_input
+from .layers import bn_act, bn_act_block_out, downsample_branch, split_block_input
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -55,7 +55,7 @@ class BasicBlock(nn.Module):
         out = bn_act(self.bn1, self.conv1(xc))
         # downsample after conv1 (same values): autograd then runs its backward before conv1's,
         # so conv1's backward-data sees the whole identity-path gradient (ops/bn.py block tails)
-        identity = xi if self.downsample is None else self.downsample(xi)
+        identity = xi if self.downsample is None else downsample_branch(self.downsample, xi, self.bn2)
         return bn_act_block_out(self.bn2, self.conv2(out), identity)
 
 
@@ -82,7 +82,7 @@ class Bottleneck(nn.Module):
         out = bn_act(self.bn1, self.conv1(xc))
         # downsample after conv1 (same values): autograd then runs its backward before conv1's,
         # so conv1's backward-data sees the whole identity-path gradient (ops/bn.py block tails)
-        identity = xi if self.downsample is None else self.downsample(xi)
+        identity = xi if self.downsample is None else downsample_branch(self.downsample, xi, self.bn3)
         out = bn_act(self.bn2, self.conv2(out))
         return bn_act_block_out(self.bn3, self.conv3(out), identity)
 

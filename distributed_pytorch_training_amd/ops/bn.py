@@ -105,6 +105,8 @@ def _bwd(ctx, dy, dy2):
             return (dx, None, dg if want_params else None, db if want_params else None)
     if dy2 is not None and ctx.relu and ctx.has_res:
         part = take_bnb_partials(dy)
+        if part is not None and part[3] is not None:
+            raise RuntimeError("fused block-tail backward: unexpected downsample statistic")
         if part is not None:
             # the consuming conv's dgrad epilogue already formed dz = (dy + dy2) * (y > 0) in dy's
             # storage and summed its statistics (ops/conv.py); dz is also the residual gradient
@@ -121,6 +123,80 @@ def _bwd(ctx, dy, dy2):
     if want_dz and ctx.res_slot is not None:
         ctx.res_slot["dres"] = dz  # picked up by the dgrad of the conv that consumed that alias
     return (dx, dz if want_dz else None, dg if want_params else None, db if want_params else None)
+
+
+class _BN2AddReLUPair(torch.autograd.Function):
+    """Residual-block tail whose identity path is a downsample BatchNorm:
+    ``relu(bn(x) + bn2(x2))`` with both BNs in training mode, as ONE op.
+
+    Forward: both BNs' statistics (from the producing convs' epilogue partials), running-stat
+    updates and coefficients, then one apply pass ``relu(x*a + b + x2*a2 + b2)`` - the
+    downsample BN's output is never written (the unfused chain writes it and reads it back).
+    Backward: both BNs see the same masked gradient dz = (dy + dy2) * (y > 0).  When the
+    consuming conv's dgrad epilogue formed dz (ops/conv.py BNR) it also summed
+    s3 = sum dz*(x2 - mean2), so the downsample BN needs no statistics pass either, and one
+    apply pass reads dz once and writes both input gradients.  Pair outputs as
+    ``_BNActTrainPair``."""
+
+    @staticmethod
+    def forward(ctx, x, x2, w, b, rm, rv, nb, w2, b2, rm2, rv2, nb2, momentum, eps, momentum2, eps2,
+                partials, partials2, own_slot):
+        C = native()
+        ps, pq = partials if partials is not None else (None, None)
+        ps2, pq2 = partials2 if partials2 is not None else (None, None)
+        _, mean, invstd, coef = C.bn_fwd_train(x, None, w, b, rm, rv, nb, float(momentum), float(eps), True,
+                                               ps, pq, False)
+        _, mean2, invstd2, coef2 = C.bn_fwd_train(x2, None, w2, b2, rm2, rv2, nb2, float(momentum2), float(eps2),
+                                                  False, ps2, pq2, False)
+        y = C.bn_apply_aff(x, x2, coef, coef2)
+        ctx.save_for_backward(x, x2, y, w, w2, mean, invstd, mean2, invstd2)
+        ctx.set_materialize_grads(False)
+        if own_slot is not None:
+            y._dpt_bn_src = (x, mean, own_slot, x2, mean2)
+        return y, y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, dy, dy2):
+        x, x2, y, w, w2, mean, invstd, mean2, invstd2 = ctx.saved_tensors
+        if dy is None:
+            dy, dy2 = dy2, None
+        if dy is None:
+            return (None,) * 19
+        want = [ctx.needs_input_grad[i] for i in (2, 3, 7, 8)]
+        want_params = any(want)
+        C = native()
+        part = take_bnb_partials(dy) if dy2 is not None else None
+        if part is not None and part[3] is not None:
+            if part[2] != dy2.data_ptr():
+                raise RuntimeError("fused block-tail backward: the identity-path gradient folded into the "
+                                   "conv's dgrad is not the one autograd delivered (alias used twice?)")
+            dx, dx2, dg, db, dg2, db2 = C.bn2_bwd_partials(dy, x, x2, w, w2, mean, invstd, mean2, invstd2,
+                                                           part[0], part[1], part[3], bool(want_params))
+        else:
+            if part is not None:
+                raise RuntimeError("fused block-tail backward: partials without the downsample statistic")
+            dx, dg, db, dz = C.bn_bwd(_cl(dy), None if dy2 is None else _cl(dy2), y, x, w, mean, invstd,
+                                      True, True, bool(want_params), None)
+            dx2, dg2, db2, _ = C.bn_bwd(dz, None, None, x2, w2, mean2, invstd2, False, False,
+                                        bool(want_params), None)
+        g = [dg, db, dg2, db2]
+        g = [t if (want_params and want[i]) else None for i, t in enumerate(g)]
+        return (dx, dx2, g[0], g[1], None, None, None, g[2], g[3]) + (None,) * 10
+
+
+def bn2_add_relu_train(x, bn, x2, bn2):
+    """Block tail ``relu(bn(x) + bn2(x2))`` in training mode (both ``FusedBatchNorm2d``), pair
+    outputs (conv path, identity path) - see _BN2AddReLUPair."""
+    x2 = _cl(x2.to(x.dtype))
+    partials = x.__dict__.pop("_dpt_bn_partials", None)
+    partials2 = x2.__dict__.pop("_dpt_bn_partials", None)
+    own_slot = {} if (BNR_FUSE and x.dtype == torch.bfloat16) else None
+    out = _BN2AddReLUPair.apply(x, x2, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                                bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var, bn2.num_batches_tracked,
+                                bn.momentum, bn.eps, bn2.momentum, bn2.eps, partials, partials2, own_slot)
+    if own_slot is not None:
+        out[1]._dpt_res_slot = own_slot
+    return out
 
 
 def bn_act_supported(x: torch.Tensor, num_features: int) -> bool:

@@ -27,7 +27,7 @@ ENABLED = os.environ.get("DPT_NATIVE_CONV", "1") != "0"
 # Backward-data of a conv fed by a fused BN+ReLU also sums that BN's backward statistics in its
 # epilogue (the BN backward then skips its statistics pass).
 BN_BWD_FUSE = os.environ.get("DPT_BN_BWD_FUSE", "1") != "0"
-# dx.data_ptr() -> (p1, p2, shape, dres_ptr): handed from a conv's backward to the BN backward
+# dx.data_ptr() -> (p1, p2, shape, dres_ptr, p3): handed from a conv's backward to the BN backward
 # that receives dx as its output gradient (ops/bn.py), consumed once
 _BNB_PARTIALS = {}
 # Stride-2 backward-data on the MFMA kernels (four parity-class convs); 0 = MIOpen
@@ -63,15 +63,18 @@ def _backward(ctx, dy):
         wt = _flipped(w) if s == 1 else None
         if src is not None and not isinstance(src[2], dict):  # BN+ReLU: (x, mean, coef)
             bn_x, bn_mean, bn_coef = src
-            dx, p1, p2 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, bn_coef, w_flipped=wt)
-            _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), None)
+            dx, p1, p2, _ = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, bn_coef, w_flipped=wt)
+            _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), None, None)
         elif src is not None and _dres_ok(dres := src[2].pop("dres", None), x):  # (x, mean, slot)
             # block-tail BN+add+ReLU (ops/bn.py pair outputs): the next block's tail already
             # produced the identity-path gradient dres; dx becomes the tail's masked total
             # gradient, the conv's input x is the tail's output y (the ReLU mask)
-            bn_x, bn_mean, _ = src
-            dx, p1, p2 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, None, x, dres, wt)
-            _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), dres.data_ptr())
+            bn_x, bn_mean = src[0], src[1]
+            # (x, mean, slot, x2, mean2): the tail's identity path was a downsample BatchNorm
+            # folded into it (ops/bn.py _BN2AddReLUPair) - also sum that BN's statistic
+            x2, mean2 = (src[3], src[4]) if len(src) > 3 else (None, None)
+            dx, p1, p2, p3 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, None, x, dres, wt, x2, mean2)
+            _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), dres.data_ptr(), p3 if x2 is not None else None)
         elif s == 1:
             dx = native().conv_dgrad_flip(dy, w, p)[0] if wt is None else native().conv_dgrad_preflipped(dy, wt, p)
         elif s == 2 and S2_DGRAD and x.dim() == 4:
@@ -176,15 +179,16 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bo
 
 
 def take_bnb_partials(dy: torch.Tensor):
-    """(p1, p2, dres_ptr) the backward of the conv that consumed a BN output summed for ``dy``,
-    once; dres_ptr is None for BN+ReLU, else the data pointer of the identity-path gradient
-    that was folded into ``dy`` (block tails)."""
+    """(p1, p2, dres_ptr, p3) the backward of the conv that consumed a BN output summed for
+    ``dy``, once; dres_ptr is None for BN+ReLU, else the data pointer of the identity-path
+    gradient that was folded into ``dy`` (block tails); p3: the folded downsample BN's statistic
+    (tails with a downsample branch), else None."""
     if not _BNB_PARTIALS:
         return None
     ent = _BNB_PARTIALS.pop(dy.data_ptr(), None)
     if ent is None or ent[2] != tuple(dy.shape):
         return None
-    return ent[0], ent[1], ent[3]
+    return ent[0], ent[1], ent[3], ent[4]
 
 
 def take_bn_partials(x: torch.Tensor):

@@ -345,3 +345,94 @@ def test_weight_flip_multi_and_preflipped_dgrad(cuda):
     w, wt = ws[1], wts[1]
     gy = torch.randn(2, 128, 9, 9, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
     assert torch.equal(ops.native().conv_dgrad_preflipped(gy, wt, 1), ops.native().conv_dgrad_flip(gy, w, 1)[0])
+
+
+def test_downsample_bn_folded_into_block_tail(cuda, monkeypatch):
+    """Block tail relu(bn3(h3) + bnd(hd)) as ONE op (ops/bn.py _BN2AddReLUPair).
+    (a) the op against an fp32 composition of the same bf16 inputs (forward, running stats,
+        and the backward through our own ReLU mask);
+    (b) in a conv chain, the backward statistics summed by the next conv's dgrad epilogue (BNR
+        with the downsample statistic) against the op's own statistics passes.  (Fused vs the
+        unfused two-op chain differ by bf16 rounding of the downsample output, which flips ReLU
+        masks downstream - not compared elementwise.)"""
+    import copy
+
+    from distributed_pytorch_training_amd.models.layers import FusedBatchNorm2d
+    from distributed_pytorch_training_amd.ops import bn as fbn
+    from distributed_pytorch_training_amd.ops import conv as nc
+
+    g = torch.Generator(device=cuda).manual_seed(9)
+    N, Cin, C4, C, HW = 4, 128, 256, 64, 14
+
+    def t(*s, scale=1.0):
+        return torch.randn(*s, device=cuda, generator=g) * scale
+
+    def bnmods(chans):
+        out = []
+        for c in chans:
+            m = FusedBatchNorm2d(c).to(cuda)
+            with torch.no_grad():
+                m.weight.uniform_(0.5, 1.5, generator=g)
+                m.bias.uniform_(-0.3, 0.3, generator=g)
+            out.append(m)
+        return out
+
+    # (a) the op alone
+    h3 = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    hd = (t(N, C4, HW, HW) * 1.5 + 0.2).to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    b3, bd = bnmods((C4, C4))
+    r3, rd = copy.deepcopy(b3), copy.deepcopy(bd)
+    yc, yi = fbn.bn2_add_relu_train(h3, b3, hd, bd)
+    x3r, xdr = h3.detach().float().requires_grad_(True), hd.detach().float().requires_grad_(True)
+    p3 = [r3.weight.detach().clone().requires_grad_(True), r3.bias.detach().clone().requires_grad_(True)]
+    pd = [rd.weight.detach().clone().requires_grad_(True), rd.bias.detach().clone().requires_grad_(True)]
+    F = torch.nn.functional
+    z = (F.batch_norm(x3r, r3.running_mean, r3.running_var, p3[0], p3[1], True, 0.1, 1e-5)
+         + F.batch_norm(xdr, rd.running_mean, rd.running_var, pd[0], pd[1], True, 0.1, 1e-5))
+    torch.testing.assert_close(yc.float(), torch.relu(z), rtol=2e-2, atol=2e-2)
+    assert torch.equal(yc, yi)
+    for m, r in ((b3, r3), (bd, rd)):
+        torch.testing.assert_close(m.running_mean, r.running_mean, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(m.running_var, r.running_var, rtol=1e-4, atol=1e-5)
+    gy = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
+    gy2 = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
+    torch.autograd.backward([yc, yi], [gy, gy2])
+    (z * (yc.detach() > 0).float()).backward(gy.float() + gy2.float())
+    keep = z.detach().abs() > 1e-2
+    torch.testing.assert_close(h3.grad.float()[keep], x3r.grad[keep], rtol=8e-2, atol=8e-2)
+    torch.testing.assert_close(hd.grad.float()[keep], xdr.grad[keep], rtol=8e-2, atol=8e-2)
+    for a, b in ((b3.weight.grad, p3[0].grad), (b3.bias.grad, p3[1].grad), (bd.weight.grad, pd[0].grad),
+                 (bd.bias.grad, pd[1].grad)):
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item())
+
+    # (b) in a conv chain: dgrad-epilogue statistics vs the op's own statistics passes
+    x0 = t(N, Cin, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
+    ws0 = [t(C4, Cin, 1, 1, scale=0.08), t(C4, Cin, 1, 1, scale=0.08), t(C, C4, 1, 1, scale=0.06),
+           t(C4, C4, 1, 1, scale=0.06)]
+    ws0 = [w.to(torch.bfloat16).contiguous(memory_format=CL) for w in ws0]
+    gu = t(N, C, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
+    gv = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
+    bns0 = bnmods((C4, C4, C))
+    used = []
+    ok = nc._dres_ok
+    monkeypatch.setattr(nc, "_dres_ok", lambda d, x: used.append(ok(d, x)) or used[-1])
+    res = []
+    for bnr in (True, False):
+        nc.BN_BWD_FUSE = bnr
+        bns = [copy.deepcopy(m) for m in bns0]
+        xi = x0.detach().clone().requires_grad_(True)
+        ps = [v.detach().clone().requires_grad_(True) for v in ws0]
+        yc, yi = fbn.bn2_add_relu_train(nc.conv2d(xi, ps[0], 1, 0, bn_stats=True), bns[0],
+                                        nc.conv2d(xi, ps[1], 1, 0, bn_stats=True), bns[1])
+        u = bns[2].act(nc.conv2d(yc, ps[2], 1, 0, bn_stats=True), True, None)
+        # identity-path consumer created last: its backward runs first and hands its input
+        # gradient to the tail through the alias's slot (as a downsample conv does)
+        v = nc.conv2d(yi, ps[3], 1, 0)
+        torch.autograd.backward([u, v], [gu, gv])
+        res.append([xi.grad.float()] + [p.grad.float() for p in ps]
+                   + [v.grad.float() for m in bns for v in (m.weight, m.bias)])
+    nc.BN_BWD_FUSE = True
+    assert used == [True]  # the fused pass took the dgrad-epilogue path
+    assert not nc._BNB_PARTIALS
+    for a, b in zip(*res):
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item() + 1e-6)
