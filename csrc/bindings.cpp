@@ -337,7 +337,8 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
 }
 
 // Stride-2 backward-data: dx [N, C, H, W] (channels_last) of y = conv2d(x, w, stride 2, pad).
-Tensor conv_dgrad_s2(Tensor dy, Tensor w, int64_t pad, int64_t H, int64_t W) {
+std::vector<Tensor> conv_dgrad_s2(Tensor dy, Tensor w, int64_t pad, int64_t H, int64_t W, c10::optional<Tensor> bn_x,
+                                  c10::optional<Tensor> bn_mean, c10::optional<Tensor> bn_coef) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
   const int Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
@@ -346,11 +347,24 @@ Tensor conv_dgrad_s2(Tensor dy, Tensor w, int64_t pad, int64_t H, int64_t W) {
   TORCH_CHECK(Ho == (H + 2 * pad - R) / 2 + 1 && Wo == (W + 2 * pad - S) / 2 + 1, "conv_dgrad_s2: geometry mismatch");
   TORCH_CHECK((int64_t)N * H * W < (int64_t(1) << 31), "conv_dgrad_s2: too many pixels");
   auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const bool bnb = bn_x.has_value() && bn_x->defined();
+  Tensor p1, p2;
+  if (bnb) {
+    check_cl_bf16(*bn_x, "bn_x");
+    TORCH_CHECK(bn_x->sizes() == dx.sizes(), "conv_dgrad_s2: bn_x must match the conv input");
+    const int chunks = dpt::conv_dgrad_s2_chunks(N, (int)H, (int)W, R, S, (int)pad);
+    p1 = at::empty({C, chunks}, dy.options().dtype(at::kFloat));
+    p2 = at::empty({C, chunks}, dy.options().dtype(at::kFloat));
+  }
   c10::hip::HIPGuard guard(dy.device().index());
   dpt::launch_conv_dgrad_s2(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
                             reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, (int)pad, (int)H, (int)W,
-                            cur_stream(dy));
-  return dx;
+                            cur_stream(dy), bnb ? reinterpret_cast<const uint16_t*>(bn_x->data_ptr()) : nullptr,
+                            bnb ? f32_param(bn_mean, C, "bn_mean") : nullptr,
+                            bnb ? f32_param(bn_coef, 2 * C, "bn_coef") : nullptr,
+                            bnb ? p1.data_ptr<float>() : nullptr, bnb ? p2.data_ptr<float>() : nullptr);
+  if (!bnb) return {dx};
+  return {dx, p1, p2};
 }
 
 // Flip/transpose many KRSC weights [Cout, C, R, S] (channels_last) into [C, Cout, R, S]
@@ -989,7 +1003,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("invstd"), py::arg("coef"), py::arg("p1"), py::arg("p2"), py::arg("want_dparams"),
         py::arg("from_dz") = false);
   m.def("conv_dgrad_s2", &conv_dgrad_s2, py::arg("grad_output"), py::arg("w"), py::arg("pad"), py::arg("H"),
-        py::arg("W"));
+        py::arg("W"), py::arg("bn_x") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_coef") = py::none());
   m.def("conv_dgrad_flip", &conv_dgrad_flip, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
 

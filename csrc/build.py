@@ -109,7 +109,21 @@ def build(jobs: int = 4, force: bool = False, debug: bool = False, verbose: bool
         if verbose:
             print(" ".join(link), flush=True)
         _run(link)
+        _check_undefined(out)
     return out
+
+
+def _check_undefined(so: Path) -> None:
+    """A shared library links with unresolved symbols; catch our own (a declaration whose
+    definition changed signature) here instead of at import time on the GPU box."""
+    nm = ROCM / "lib" / "llvm" / "bin" / "llvm-nm"
+    if not nm.exists():
+        return
+    r = subprocess.run([str(nm), "-u", "-C", str(so)], capture_output=True, text=True)
+    bad = [l.strip() for l in r.stdout.splitlines() if "dpt::" in l]
+    if bad:
+        so.unlink()
+        raise RuntimeError("unresolved framework symbols in the extension:\n  " + "\n  ".join(bad))
 
 
 def main(argv=None) -> int:

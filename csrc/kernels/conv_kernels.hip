@@ -84,6 +84,9 @@ struct ConvFwdArgs {
   int Rw, Sw, tr0, trs, ts0, tss;
   // REMAP epilogue: GEMM output row (n, a, b) lands on row (n*oH + 2a + oph)*oW + 2b + opw
   int oH, oW, oph, opw;
+  // BNB partials: column mt + bp_off of a [Cout][bp_ld] array (the strided backward-data's
+  // parity classes write consecutive column ranges of one array)
+  int bp_ld, bp_off;
 };
 
 // K-major operands (rows of the LDS image = k) use the transposing reads and the swizzle of
@@ -369,6 +372,14 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
         s3[k] = 0.f;
       }
     }
+    // destination row of GEMM row m (REMAP: its pixel in one parity class of the larger image)
+    auto grow = [&](int64_t m) -> int64_t {
+      if (!REMAP) return m;
+      const uint32_t mm = (uint32_t)m, hw = (uint32_t)HoWo;
+      const uint32_t img = mm / hw, rem = mm - img * hw;
+      const int a = (int)(rem / (uint32_t)p.Wo), b = (int)(rem - (uint32_t)a * (uint32_t)p.Wo);
+      return ((int64_t)img * p.oH + 2 * a + p.oph) * p.oW + 2 * b + p.opw;
+    };
 #pragma unroll
     for (int g0 = 0; g0 < NPASS; g0 += GRP) {
       uint4 xv[GRP], yv[GRP], rv[GRP], x2v[GRP];
@@ -376,7 +387,7 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
 #pragma unroll
         for (int q = 0; q < GRP; ++q) {
           const int64_t m = m0 + (g0 + q) * RPP + orow;
-          const int64_t off = (m < p.M ? m : 0) * p.Cout + n0 + oc * 8;
+          const int64_t off = grow(m < p.M ? m : 0) * p.Cout + n0 + oc * 8;
           xv[q] = *reinterpret_cast<const uint4*>(p.bnx + off);
           if (BNR) {
             yv[q] = *reinterpret_cast<const uint4*>(p.bny + off);
@@ -432,11 +443,9 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
             if (BNR) v = make_uint4(du[0], du[1], du[2], du[3]);
           }
           if (REMAP) {
-            const uint32_t mm = (uint32_t)m, hw = (uint32_t)HoWo;
-            const uint32_t img = mm / hw, rem = mm - img * hw;
-            const int a = (int)(rem / (uint32_t)p.Wo), b = (int)(rem - (uint32_t)a * (uint32_t)p.Wo);
-            const int oy = 2 * a + p.oph, ox = 2 * b + p.opw;
-            uint16_t* orow = p.y + (((int64_t)img * p.oH + oy) * p.oW + ox) * p.Cout + n0 + oc * 8;
+            const int64_t gr = grow(m);
+            const int oy = (int)((gr / p.oW) % p.oH), ox = (int)(gr % p.oW);
+            uint16_t* orow = p.y + gr * p.Cout + n0 + oc * 8;
             *reinterpret_cast<uint4*>(orow) = v;
             if (ZSIB) {
               const uint4 z = make_uint4(0u, 0u, 0u, 0u);
@@ -485,9 +494,10 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
           b += bred[(w * NS3 + 1) * BN + tid];
           if (two) c3 += bred[(w * NS3 + 2) * BN + tid];
         }
-        p.bp1[(int64_t)(n0 + tid) * p.m_tiles + mt] = a;
-        p.bp2[(int64_t)(n0 + tid) * p.m_tiles + mt] = b;
-        if (two) p.bp3[(int64_t)(n0 + tid) * p.m_tiles + mt] = c3;
+        const int64_t pc = (int64_t)(n0 + tid) * p.bp_ld + p.bp_off + mt;
+        p.bp1[pc] = a;
+        p.bp2[pc] = b;
+        if (two) p.bp3[pc] = c3;
       }
     }
   }
@@ -1177,6 +1187,7 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
   a.bnx = bnx; a.bn_mean = bn_mean; a.bn_coef = bn_coef; a.bp1 = bp1; a.bp2 = bp2;
   a.bny = bny; a.bnres = bnres;
   a.bnx2 = bnx2; a.bn_mean2 = bn_mean2; a.bp3 = bp3;
+  a.bp_ld = a.m_tiles; a.bp_off = 0;
   const bool res = bny != nullptr;
   const dim3 block(conv::kThreads);
   a.n_tiles = C % 128 == 0 ? C / 128 : C / 64;
@@ -1212,8 +1223,23 @@ void launch_conv_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int 
 // tap; its output rows land on (2a + ph, 2b + pw) (REMAP epilogue).  A class with no taps
 // (e.g. the odd classes of a 1x1 / stride-2 conv) gets zeros from the class-(0,0) launch (ZSIB)
 // - every dx element is written exactly once, no memset pass.
+int conv_dgrad_s2_chunks(int N, int H, int W, int R, int S, int pad) {
+  int chunks = 0;
+  for (int ph = 0; ph < 2; ++ph)
+    for (int pw = 0; pw < 2; ++pw) {
+      const int r0 = ((ph + pad) % 2 + 2) % 2, s0 = ((pw + pad) % 2 + 2) % 2;
+      const int Ha = (H - ph + 1) / 2, Wa = (W - pw + 1) / 2;
+      if (Ha > 0 && Wa > 0 && r0 < R && s0 < S) chunks += conv_m_tiles((int64_t)N * Ha * Wa);
+    }
+  return chunks;
+}
+
 void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout,
-                          int C, int R, int S, int pad, int H, int W, hipStream_t s) {
+                          int C, int R, int S, int pad, int H, int W, hipStream_t s, const uint16_t* bnx,
+                          const float* bn_mean, const float* bn_coef, float* bp1, float* bp2) {
+  const bool bnb = bnx != nullptr;
+  const int bp_ld = bnb ? conv_dgrad_s2_chunks(N, H, W, R, S, pad) : 0;
+  int bp_off = 0;
   int J[2], r0[2], Js[2], s0[2], D[2], Ds[2];
   for (int ph = 0; ph < 2; ++ph) {
     r0[ph] = ((ph + pad) % 2 + 2) % 2;
@@ -1242,13 +1268,22 @@ void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, i
       a.tr0 = r0[ph] + 2 * (J[ph] - 1); a.trs = -2;
       a.ts0 = s0[pw] + 2 * (Js[pw] - 1); a.tss = -2;
       a.oH = H; a.oW = W; a.oph = ph; a.opw = pw;
-      a.bnx = nullptr; a.bny = nullptr; a.bnres = nullptr; a.bn_mean = nullptr; a.bn_coef = nullptr;
+      a.bnx = bnx; a.bny = nullptr; a.bnres = nullptr; a.bn_mean = bn_mean; a.bn_coef = bn_coef;
       a.bnx2 = nullptr; a.bn_mean2 = nullptr; a.bp3 = nullptr;
-      a.bp1 = nullptr; a.bp2 = nullptr;
+      a.bp1 = bp1; a.bp2 = bp2; a.bp_ld = bp_ld; a.bp_off = bp_off;
+      bp_off += a.m_tiles;
       const bool z = zsib && ph == 0 && pw == 0;
       const dim3 block(conv::kThreads);
       a.n_tiles = C % 128 == 0 ? C / 128 : C / 64;
       const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
+      if (bnb) {
+        // zero classes (ZSIB) only arise for 1x1 kernels, whose input is never a fused BN+ReLU
+        // output in the models here: BNB and ZSIB are not combined
+        if (z) throw std::runtime_error("conv_dgrad_s2: BN statistics with zero-filled classes unsupported");
+        if (C % 128 == 0) hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, true, false, true, false, true, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, true, true, false, true, false, true, false>), grid, block, 0, s, a);
+        continue;
+      }
       if (C % 128 == 0) {
         if (z) hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, true, false, false, false, true, true>), grid, block, 0, s, a);
         else hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, true, false, false, false, true, false>), grid, block, 0, s, a);

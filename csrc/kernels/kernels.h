@@ -169,7 +169,11 @@ struct WtFlipBatch {
 void launch_conv_wt_flip_multi(WtFlipBatch b, hipStream_t s);
 // stride-2 backward-data straight from the KRSC weight w [Cout,R,S,C]: dy [N,Ho,Wo,Cout] -> dx [N,H,W,C]
 void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout,
-                          int C, int R, int S, int pad, int H, int W, hipStream_t s);
+                          int C, int R, int S, int pad, int H, int W, hipStream_t s, const uint16_t* bnx = nullptr,
+                          const float* bn_mean = nullptr, const float* bn_coef = nullptr, float* bp1 = nullptr,
+                          float* bp2 = nullptr);
+// [C][chunks] partial columns the BN-statistics variant of launch_conv_dgrad_s2 writes
+int conv_dgrad_s2_chunks(int N, int H, int W, int R, int S, int pad);
 // stride-1 backward-data straight from the KRSC weight w [Cout,R,S,C]: dy [N,Ho,Wo,Cout] -> dx [N,Ho,Wo,C]
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout, int C,
                        int R, int S, int pad, hipStream_t s);

@@ -78,7 +78,13 @@ def _backward(ctx, dy):
         elif s == 1:
             dx = native().conv_dgrad_flip(dy, w, p)[0] if wt is None else native().conv_dgrad_preflipped(dy, wt, p)
         elif s == 2 and S2_DGRAD and x.dim() == 4:
-            dx = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3])
+            src = ctx.bn_src if BN_BWD_FUSE else None
+            if src is not None and not isinstance(src[2], dict) and w.shape[2] > 1:
+                # BN+ReLU input: its backward statistics from the parity-class epilogues too
+                dx, p1, p2 = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3], src[0], src[1], src[2])
+                _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), None, None)
+            else:
+                dx = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3])[0]
         else:
             dx = torch.ops.aten.convolution_backward(dy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
                                                      (True, False, False))[0]

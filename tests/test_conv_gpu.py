@@ -83,7 +83,7 @@ def test_conv_dgrad_stride2_matches_fp32(cuda, shape):
     x, w = _operands(cuda, N, C, H, W, Cout, k, seed=2)
     Ho, Wo = (H + 2 * p - k) // 2 + 1, (W + 2 * p - k) // 2 + 1
     gy = torch.randn(N, Cout, Ho, Wo, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
-    dx = ops.native().conv_dgrad_s2(gy, w, p, H, W)
+    dx = ops.native().conv_dgrad_s2(gy, w, p, H, W)[0]
     ref = torch.nn.grad.conv2d_input(x.shape, w.float(), gy.float(), stride=2, padding=p)
     assert dx.shape == ref.shape and dx.is_contiguous(memory_format=CL)
     torch.testing.assert_close(dx.float(), ref, rtol=1e-2, atol=2e-2)
@@ -234,8 +234,8 @@ def test_s2d_stem_matches_fp32(cuda, xdtype, hw):
     torch.testing.assert_close(w.grad.float(), wref, rtol=2e-2, atol=2e-2 * wref.abs().max().item())
 
 
-@pytest.mark.parametrize("k2", [1, 3])
-def test_bn_backward_stats_from_dgrad_epilogue(cuda, k2):
+@pytest.mark.parametrize("k2,s2", [(1, 1), (3, 1), (3, 2)])
+def test_bn_backward_stats_from_dgrad_epilogue(cuda, k2, s2):
     """conv -> fused BN+ReLU -> conv: the second conv's backward-data epilogue sums the BN's
     backward statistics; gradients must equal the unfused path's (same math, other order)."""
     from distributed_pytorch_training_amd.ops import bn as fbn
@@ -258,8 +258,8 @@ def test_bn_backward_stats_from_dgrad_epilogue(cuda, k2):
         nb = torch.zeros((), dtype=torch.long, device=cuda)
         h = nc.conv2d(xi, ps[0], 1, 0, bn_stats=True)
         z = fbn.bn_act_train(h, None, ps[2], ps[3], rm, rv, nb, 0.1, 1e-5, True)
-        y = nc.conv2d(z, ps[1], 1, k2 // 2)
-        y.backward(gy)
+        y = nc.conv2d(z, ps[1], s2, k2 // 2)
+        y.backward(gy if s2 == 1 else gy[:, :, ::2, ::2].contiguous(memory_format=CL))
         grads.append([xi.grad.float()] + [p.grad.float() for p in ps])
     nc.BN_BWD_FUSE = True
     assert not nc._BNB_PARTIALS  # every handed-over partial was consumed
