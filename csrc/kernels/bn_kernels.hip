@@ -219,6 +219,39 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_finalize_kernel(
 
 // Same finalize for MANY partials per channel (the conv epilogue writes one per 128 rows: up
 // to ~6k at ResNet-50's 56x56 layers): one 256-thread block per channel, fp64 block reduce.
+// Wave-reduced fp64 sums of two contiguous fp32 rows of `chunks` partials (one block per
+// channel): 8 loads of each row in flight per thread - the finalize is a latency chain of
+// chunks / (kBlock * U) dependent round trips, not a bandwidth problem.
+__device__ __forceinline__ void block_row_sum2(const float* __restrict__ q1, const float* __restrict__ q2,
+                                               int chunks, double& s, double& q) {
+  constexpr int U = 8;
+  double a[U], b[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) { a[u] = 0.0; b[u] = 0.0; }
+  int k = threadIdx.x;
+  for (; k + (U - 1) * kBlock < chunks; k += U * kBlock) {
+    float x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) { x[u] = q1[k + u * kBlock]; y[u] = q2[k + u * kBlock]; }
+#pragma unroll
+    for (int u = 0; u < U; ++u) { a[u] += (double)x[u]; b[u] += (double)y[u]; }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int kk = k + u * kBlock;
+    if (kk < chunks) { a[u] += (double)q1[kk]; b[u] += (double)q2[kk]; }
+  }
+  s = 0.0;
+  q = 0.0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) { s += a[u]; q += b[u]; }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off, 64);
+    q += __shfl_xor(q, off, 64);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void bn_fwd_finalize_wide_kernel(
     const float* __restrict__ psum, const float* __restrict__ psq, int chunks, int C, int64_t M,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
@@ -227,21 +260,8 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_finalize_wide_kernel(
   __shared__ double red[2][kBlock / 64];
   const int c = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (c == 0 && threadIdx.x == 0 && num_batches) num_batches[0] += 1;
-  const float* q1 = psum + (int64_t)c * chunks;
-  const float* q2 = psq + (int64_t)c * chunks;
-  double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
-  int k = threadIdx.x;
-  for (; k + kBlock < chunks; k += 2 * kBlock) {
-    const float x0 = q1[k], x1 = q1[k + kBlock], y0 = q2[k], y1 = q2[k + kBlock];
-    a0 += (double)x0; a1 += (double)x1; b0 += (double)y0; b1 += (double)y1;
-  }
-  if (k < chunks) { a0 += (double)q1[k]; b0 += (double)q2[k]; }
-  double s = a0 + a1, q = b0 + b1;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    s += __shfl_xor(s, off, 64);
-    q += __shfl_xor(q, off, 64);
-  }
+  double s, q;
+  block_row_sum2(psum + (int64_t)c * chunks, psq + (int64_t)c * chunks, chunks, s, q);
   if (lane == 0) { red[0][wave] = s; red[1][wave] = q; }
   __syncthreads();
   if (threadIdx.x != 0) return;
@@ -713,21 +733,8 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_wide_kernel(
     float* k1, float* k2, float* k3) {
   __shared__ double red[2][kBlock / 64];
   const int c = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const float* q1 = p1 + (int64_t)c * chunks;
-  const float* q2 = p2 + (int64_t)c * chunks;
-  double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
-  int k = threadIdx.x;
-  for (; k + kBlock < chunks; k += 2 * kBlock) {
-    const float x0 = q1[k], x1 = q1[k + kBlock], y0 = q2[k], y1 = q2[k + kBlock];
-    a0 += (double)x0; a1 += (double)x1; b0 += (double)y0; b1 += (double)y1;
-  }
-  if (k < chunks) { a0 += (double)q1[k]; b0 += (double)q2[k]; }
-  double s1 = a0 + a1, s2 = b0 + b1;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    s1 += __shfl_xor(s1, off, 64);
-    s2 += __shfl_xor(s2, off, 64);
-  }
+  double s1, s2;
+  block_row_sum2(p1 + (int64_t)c * chunks, p2 + (int64_t)c * chunks, chunks, s1, s2);
   if (lane == 0) { red[0][wave] = s1; red[1][wave] = s2; }
   __syncthreads();
   if (threadIdx.x != 0) return;
