@@ -719,8 +719,9 @@ std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t stride, int64_t pad
   return {y, idx};
 }
 
-Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64_t stride, int64_t pad,
-                   c10::optional<Tensor> dy2) {
+std::vector<Tensor> maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64_t stride, int64_t pad,
+                                c10::optional<Tensor> dy2, c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mean,
+                                c10::optional<Tensor> bn_coef) {
   TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
               "maxpool_bwd: grad must be channels_last");
   TORCH_CHECK(idx.sizes() == dy.sizes() && idx.scalar_type() == at::kByte &&
@@ -733,11 +734,26 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64
     TORCH_CHECK(dy2->sizes() == dy.sizes() && dy2->scalar_type() == dy.scalar_type() &&
                     dy2->is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool_bwd: dy2 must match grad_output");
   auto dx = at::empty({B, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const bool bns = bn_x.has_value() && bn_x->defined();
+  Tensor p1, p2;
+  if (bns) {
+    TORCH_CHECK(k == 3 && stride == 2 && pad == 1, "maxpool_bwd: BN statistics only for the 3x3/2/1 pool");
+    TORCH_CHECK(C <= 512 && (C & (C - 1)) == 0, "maxpool_bwd: BN statistics need a power-of-two C <= 512");
+    TORCH_CHECK(bn_x->sizes() == dx.sizes() && bn_x->scalar_type() == dy.scalar_type() &&
+                    bn_x->is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool_bwd: bn_x must match dx");
+    const int chunks = dpt::maxpool_bwd_bn_chunks(B, (int)H, (int)W, (int)C);
+    p1 = at::empty({C, chunks}, dy.options().dtype(at::kFloat));
+    p2 = at::empty({C, chunks}, dy.options().dtype(at::kFloat));
+  }
   c10::hip::HIPGuard guard(dy.device().index());
   dpt::launch_maxpool_bwd(bn_dtype(dy), dy.data_ptr(), two ? dy2->data_ptr() : nullptr, idx.data_ptr<uint8_t>(),
                           dx.data_ptr(), B, (int)H, (int)W,
-                          (int)C, (int)Ho, (int)Wo, (int)k, (int)stride, (int)pad, cur_stream(dy));
-  return dx;
+                          (int)C, (int)Ho, (int)Wo, (int)k, (int)stride, (int)pad, cur_stream(dy), bns ? bn_x->data_ptr() : nullptr,
+                          bns ? f32_param(bn_mean, C, "bn_mean") : nullptr, bns ? f32_param(bn_coef, 2 * C, "bn_coef") : nullptr,
+                          bns ? p1.data_ptr<float>() : nullptr, bns ? p2.data_ptr<float>() : nullptr);
+  if (bns) return {dx, p1, p2};
+  
+  return {dx};
 }
 
 // dx = broadcast of g [N, C] / (H*W) over an [N, C, H, W] channels_last tensor of dtype like_dtype
@@ -981,7 +997,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("stride"), py::arg("pad"));
   m.def("gap_bwd", &gap_bwd, py::arg("g"), py::arg("H"), py::arg("W"), py::arg("dtype"));
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("grad_output"), py::arg("idx"), py::arg("H"), py::arg("W"),
-        py::arg("k"), py::arg("stride"), py::arg("pad"), py::arg("grad_output2") = py::none());
+        py::arg("k"), py::arg("stride"), py::arg("pad"), py::arg("grad_output2") = py::none(),
+        py::arg("bn_x") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_coef") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"),
         py::arg("out_h") = 0, py::arg("out_w") = 0);
   m.def("space_to_depth2", &space_to_depth2, py::arg("x"));

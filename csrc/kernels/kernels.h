@@ -87,8 +87,13 @@ void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t
 // global-average-pool backward: dx [N, HW, C] (dtype) = g [N, C] (gdtype) / HW
 void launch_gap_bwd(int dtype, int gdtype, const void* g, void* dx, int64_t N, int64_t HW, int64_t C, hipStream_t s);
 // dy2: optional second output gradient, summed in (pool output with two consumers)
+// bnx/bn_mean/bn_coef (3x3/2/1 pools only): the input was relu(bn(bnx)); also write that BN's
+// backward-statistics partials [C][maxpool_bwd_bn_chunks(...)] to bp1/bp2
 void launch_maxpool_bwd(int dtype, const void* dy, const void* dy2, const uint8_t* idx, void* dx, int64_t B, int H,
-                        int W, int C, int Ho, int Wo, int K, int S, int P, hipStream_t s);
+                        int W, int C, int Ho, int Wo, int K, int S, int P, hipStream_t s, const void* bnx = nullptr,
+                        const float* bn_mean = nullptr, const float* bn_coef = nullptr, float* bp1 = nullptr,
+                        float* bp2 = nullptr);
+int maxpool_bwd_bn_chunks(int64_t B, int H, int W, int C);
 
 // gather_kernels.hip: up to kGatherMax tensors per launch (kernel-argument struct)
 constexpr int kGatherMax = 48;

@@ -211,14 +211,26 @@ __global__ __launch_bounds__(kBlock) void maxpool3_fwd_kernel(const void* __rest
 // pixels are covered exactly by windows {a, a+1} x {b, b+1}: each is read once per block (vs
 // 2.25 window reads per pixel, data-dependent trip counts and branches in the general gather)
 // and the window-local argmax decides which pixel receives its gradient.
-template <int DT>
+// BNS: the pool input was relu(bn(x)) (ResNet's stem BatchNorm+ReLU): also sum that BN's
+// backward statistics s1 = sum dz, s2 = sum dz*(x - mean), dz = dx * (fma(x, a, b) > 0), per
+// block into [C][gridDim.x] partials (C = 8 * groups, kBlock % (C / 8) == 0) - the BN backward
+// then skips its statistics pass over the two largest tensors of the network.
+template <int DT, bool BNS = false>
 __global__ __launch_bounds__(kBlock) void maxpool3s2_bwd_kernel(const void* __restrict__ dy,
                                                                 const void* __restrict__ dy2,
                                                                 const uint8_t* __restrict__ idx,
                                                                 void* __restrict__ dx, int H, int W, int C, int Ho,
-                                                                int Wo, int Ha, int Wa, uint32_t total) {
+                                                                int Wo, int Ha, int Wa, uint32_t total,
+                                                                const void* __restrict__ bnx = nullptr,
+                                                                const float* __restrict__ bn_mean = nullptr,
+                                                                const float* __restrict__ bn_coef = nullptr,
+                                                                float* __restrict__ bp1 = nullptr,
+                                                                float* __restrict__ bp2 = nullptr) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  if (t >= total) return;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+  if (t < total) {
   const uint32_t cg8 = (uint32_t)C >> 3;
   const int cg = (int)(t % cg8);
   uint32_t q = t / cg8;
@@ -264,6 +276,24 @@ __global__ __launch_bounds__(kBlock) void maxpool3s2_bwd_kernel(const void* __re
       }
     }
   }
+  float bm[8], ba[8], bb[8], xq[4][8];
+  if (BNS) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bm[k] = bn_mean[cg * 8 + k];
+      ba[k] = bn_coef[cg * 8 + k];
+      bb[k] = bn_coef[C + cg * 8 + k];
+    }
+    // BN inputs of the block's four pixels, loaded before any store (the compiler cannot move
+    // loads above stores it cannot prove disjoint)
+#pragma unroll
+    for (int py = 0; py < 2; ++py)
+#pragma unroll
+      for (int px = 0; px < 2; ++px) {
+        const int iy = min(2 * a + py, H - 1), ix = min(2 * b + px, W - 1);
+        pool_load8(DT, bnx, ((n * H + iy) * W + ix) * C + cg * 8, xq[py * 2 + px]);
+      }
+  }
 #pragma unroll
   for (int py = 0; py < 2; ++py) {
     const int iy = 2 * a + py;
@@ -272,7 +302,48 @@ __global__ __launch_bounds__(kBlock) void maxpool3s2_bwd_kernel(const void* __re
     for (int px = 0; px < 2; ++px) {
       const int ix = 2 * b + px;
       if (ix >= W) continue;
-      pool_store8(DT, dx, ((n * H + iy) * W + ix) * C + cg * 8, acc[py * 2 + px]);
+      const int64_t off = ((n * H + iy) * W + ix) * C + cg * 8;
+      pool_store8(DT, dx, off, acc[py * 2 + px]);
+      if (BNS) {
+        // statistics from the values the BN backward will read (rounded to the storage type)
+        float g[8];
+        const float* xv = xq[py * 2 + px];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          g[k] = acc[py * 2 + px][k];
+          if (DT != 0) g[k] = DT == 1 ? bf16_to_f32(f32_to_bf16(g[k])) : f16_to_f32(pool_to16(2, g[k]));
+          const float dz = __builtin_fmaf(xv[k], ba[k], bb[k]) > 0.0f ? g[k] : 0.0f;
+          s1[k] += dz;
+          s2[k] = __builtin_fmaf(dz, xv[k] - bm[k], s2[k]);
+        }
+      }
+    }
+  }
+  }  // t < total
+  if (BNS) {
+    // threads of one channel group: t % (C/8) equal -> lanes l, l + C/8, ... then the 4 waves
+    __shared__ float red[2][kBlock / 64][64 * 8];
+    const int cg8 = C >> 3, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      for (int off = cg8; off < 64; off <<= 1) {
+        s1[k] += __shfl_xor(s1[k], off, 64);
+        s2[k] += __shfl_xor(s2[k], off, 64);
+      }
+    if (lane < cg8) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[0][wave][lane * 8 + k] = s1[k];
+        red[1][wave][lane * 8 + k] = s2[k];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += kBlock) {
+      float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < kBlock / 64; ++w) { a1 += red[0][w][c]; a2 += red[1][w][c]; }
+      bp1[(int64_t)c * gridDim.x + blockIdx.x] = a1;
+      bp2[(int64_t)c * gridDim.x + blockIdx.x] = a2;
     }
   }
 }
@@ -317,14 +388,28 @@ void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t
   else maxpool_fwd_dispatch<uint64_t>(dtype, grid, x, y, idx, B, H, W, C, Ho, Wo, K, S, P, s);
 }
 
+int maxpool_bwd_bn_chunks(int64_t B, int H, int W, int C) {
+  const int64_t total2 = B * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+  return (int)((total2 + kBlock - 1) / kBlock);
+}
+
 void launch_maxpool_bwd(int dtype, const void* dy, const void* dy2, const uint8_t* idx, void* dx, int64_t B, int H,
-                        int W, int C, int Ho, int Wo, int K, int S, int P, hipStream_t s) {
+                        int W, int C, int Ho, int Wo, int K, int S, int P, hipStream_t s, const void* bnx,
+                        const float* bn_mean, const float* bn_coef, float* bp1, float* bp2) {
   const int64_t total = B * H * W * (C / 8);
   if (total == 0) return;
   const int Ha = (H + 1) / 2, Wa = (W + 1) / 2;
   const int64_t total2 = B * Ha * Wa * (C / 8);
   if (K == 3 && S == 2 && P == 1 && Ho == Ha && Wo == Wa && total2 + kBlock < (int64_t(1) << 32)) {
     const dim3 g2((unsigned)((total2 + kBlock - 1) / kBlock)), block(kBlock);
+    if (bnx != nullptr) {
+      switch (dtype) {
+        case 0: hipLaunchKernelGGL((maxpool3s2_bwd_kernel<0, true>), g2, block, 0, s, dy, dy2, idx, dx, H, W, C, Ho, Wo, Ha, Wa, (uint32_t)total2, bnx, bn_mean, bn_coef, bp1, bp2); break;
+        case 1: hipLaunchKernelGGL((maxpool3s2_bwd_kernel<1, true>), g2, block, 0, s, dy, dy2, idx, dx, H, W, C, Ho, Wo, Ha, Wa, (uint32_t)total2, bnx, bn_mean, bn_coef, bp1, bp2); break;
+        default: hipLaunchKernelGGL((maxpool3s2_bwd_kernel<2, true>), g2, block, 0, s, dy, dy2, idx, dx, H, W, C, Ho, Wo, Ha, Wa, (uint32_t)total2, bnx, bn_mean, bn_coef, bp1, bp2); break;
+      }
+      return;
+    }
     switch (dtype) {
       case 0: hipLaunchKernelGGL(maxpool3s2_bwd_kernel<0>, g2, block, 0, s, dy, dy2, idx, dx, H, W, C, Ho, Wo, Ha, Wa, (uint32_t)total2); break;
       case 1: hipLaunchKernelGGL(maxpool3s2_bwd_kernel<1>, g2, block, 0, s, dy, dy2, idx, dx, H, W, C, Ho, Wo, Ha, Wa, (uint32_t)total2); break;

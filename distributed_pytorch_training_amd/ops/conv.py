@@ -184,6 +184,12 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bo
     return y
 
 
+def register_bnb_partials(dx: torch.Tensor, p1: torch.Tensor, p2: torch.Tensor) -> None:
+    """Hand BN+ReLU backward-statistics partials summed by dx's producer to the BN backward
+    that receives dx as its output gradient (other producers than convs: the stem pool)."""
+    _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), None, None)
+
+
 def take_bnb_partials(dy: torch.Tensor):
     """(p1, p2, dres_ptr, p3) the backward of the conv that consumed a BN output summed for
     ``dy``, once; dres_ptr is None for BN+ReLU, else the data pointer of the identity-path

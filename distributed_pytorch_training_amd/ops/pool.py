@@ -27,7 +27,7 @@ class _MaxPoolNHWC(torch.autograd.Function):
         H, W, k, s, p = ctx.cfg
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
-        return native().maxpool_bwd(dy, idx, H, W, k, s, p), None, None, None
+        return native().maxpool_bwd(dy, idx, H, W, k, s, p)[0], None, None, None
 
 
 class _MaxPoolNHWCPair(torch.autograd.Function):
@@ -37,26 +37,37 @@ class _MaxPoolNHWCPair(torch.autograd.Function):
     [B, 56, 56, 64] activation gradient, twice read once written)."""
 
     @staticmethod
-    def forward(ctx, x, k, stride, pad):
+    def forward(ctx, x, k, stride, pad, bn_src):
         y, idx = native().maxpool_fwd(x, k, stride, pad)
         ctx.save_for_backward(idx)
         ctx.cfg = (x.shape[2], x.shape[3], k, stride, pad)
+        # (BN input, mean, coef) of the fused BN+ReLU that produced x (the ResNet stem): the
+        # backward gather also sums that BN's backward statistics (ops/bn.py picks them up)
+        ctx.bn_src = bn_src if (bn_src is not None and (k, stride, pad) == (3, 2, 1)) else None
         ctx.mark_non_differentiable(idx)
         ctx.set_materialize_grads(False)
         return y, y.view_as(y)
 
     @staticmethod
     def backward(ctx, dy, dy2):
+        from .conv import BN_BWD_FUSE, register_bnb_partials
+
         (idx,) = ctx.saved_tensors
         H, W, k, s, p = ctx.cfg
         if dy is None:
             dy, dy2 = dy2, None
         if dy is None:
-            return None, None, None, None
+            return None, None, None, None, None
         dy = _cl(dy)
         if dy2 is not None:
             dy2 = _cl(dy2.to(dy.dtype))
-        return native().maxpool_bwd(dy, idx, H, W, k, s, p, dy2), None, None, None
+        src = ctx.bn_src if BN_BWD_FUSE else None
+        if src is not None and src[0].dtype == dy.dtype:
+            dx, p1, p2 = native().maxpool_bwd(dy, idx, H, W, k, s, p, dy2, src[0], src[1], src[2])
+            register_bnb_partials(dx, p1, p2)
+        else:
+            dx = native().maxpool_bwd(dy, idx, H, W, k, s, p, dy2)[0]
+        return dx, None, None, None, None
 
 
 def _cl(t: torch.Tensor) -> torch.Tensor:
@@ -76,7 +87,7 @@ def maxpool_supported(x: torch.Tensor, k, stride, pad, dilation, ceil_mode) -> b
 def max_pool2d_nhwc(x: torch.Tensor, k: int, stride: int, pad: int, pair: bool = False):
     """``pair``: return (y, y_alias) for a conv path and an identity path (see _MaxPoolNHWCPair)."""
     if pair:
-        return _MaxPoolNHWCPair.apply(x, int(k), int(stride), int(pad))
+        return _MaxPoolNHWCPair.apply(x, int(k), int(stride), int(pad), x.__dict__.get("_dpt_bn_src"))
     return _MaxPoolNHWC.apply(x, int(k), int(stride), int(pad))
 
 

@@ -221,3 +221,33 @@ def test_global_avg_pool_backward(cuda, dtype):
     assert xa.grad.is_contiguous(memory_format=torch.channels_last)
     rt, at = TOL[dtype]
     torch.testing.assert_close(xa.grad.float(), xb.grad.float(), rtol=rt, atol=at)
+
+
+def test_stem_bn_statistics_from_pool_backward(cuda):
+    """ResNet stem: BN+ReLU -> 3x3/2 max-pool (pair outputs).  The pool's backward gather also
+    sums the BN's backward statistics (pool_kernels.hip BNS); gradients must equal the BN's own
+    statistics pass."""
+    from distributed_pytorch_training_amd.ops import bn as fbn
+    from distributed_pytorch_training_amd.ops import conv as nc
+    from distributed_pytorch_training_amd.ops.pool import max_pool2d_nhwc
+
+    x0 = _mk((4, 64, 30, 30), torch.bfloat16, cuda, 51)
+    g1 = _mk((4, 64, 15, 15), torch.bfloat16, cuda, 52)
+    g2 = _mk((4, 64, 15, 15), torch.bfloat16, cuda, 53)
+    w0 = torch.rand(64, device=cuda) + 0.5
+    b0 = torch.randn(64, device=cuda) * 0.2
+    grads = []
+    for fuse in (True, False):
+        nc.BN_BWD_FUSE = fuse
+        x = x0.detach().clone().requires_grad_(True)
+        w, b = w0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        rm, rv = torch.zeros(64, device=cuda), torch.ones(64, device=cuda)
+        nb = torch.zeros((), dtype=torch.long, device=cuda)
+        y = fbn.bn_act_train(x, None, w, b, rm, rv, nb, 0.1, 1e-5, True)
+        p1, p2 = max_pool2d_nhwc(y, 3, 2, 1, pair=True)
+        torch.autograd.backward([p1, p2], [g1, g2])
+        grads.append([x.grad.float(), w.grad, b.grad])
+    nc.BN_BWD_FUSE = True
+    assert not nc._BNB_PARTIALS
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item() + 1e-6)
