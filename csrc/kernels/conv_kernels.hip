@@ -87,7 +87,6 @@ struct ConvFwdArgs {
   // BNB partials: column mt + bp_off of a [Cout][bp_ld] array (the strided backward-data's
   // parity classes write consecutive column ranges of one array)
   int bp_ld, bp_off;
-  int no_pstore;  // measurement knob (DPT_CONV_NO_PSTORE=1): compute but do not store the partials
 };
 
 // K-major operands (rows of the LDS image = k) use the transposing reads and the swizzle of
@@ -344,7 +343,7 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
 #pragma unroll
       for (int w = st * WPS; w < (st + 1) * WPS; ++w) { s += red[w * BN + tid]; q += red[WM * BN + w * BN + tid]; }
       const int sub = mt * SUB + st;
-      if ((int64_t)sub * 128 < p.M && !p.no_pstore) {
+      if ((int64_t)sub * 128 < p.M) {
         p.psum[(int64_t)(n0 + tid) * p.m_tiles + sub] = s;
         p.psq[(int64_t)(n0 + tid) * p.m_tiles + sub] = q;
       }
@@ -1162,8 +1161,6 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
   a.M = (int64_t)N * a.Ho * a.Wo;
   a.m_tiles = conv_m_tiles(a.M);
   a.Rw = R; a.Sw = S; a.tr0 = R - 1; a.trs = -1; a.ts0 = S - 1; a.tss = -1;  // BKN: flipped taps
-  static const int no_pstore = std::getenv("DPT_CONV_NO_PSTORE") ? std::atoi(std::getenv("DPT_CONV_NO_PSTORE")) : 0;
-  a.no_pstore = no_pstore;
   const bool wide = Cout % 128 == 0;
   a.n_tiles = Cout / (wide ? 128 : 64);
   a.mt256 = 0;
