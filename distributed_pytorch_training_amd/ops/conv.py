@@ -37,6 +37,14 @@ S2_DGRAD = os.environ.get("DPT_S2_DGRAD", "1") != "0"
 STEM_ENABLED = os.environ.get("DPT_NATIVE_STEM", "0") == "1"
 
 
+# Convs with fewer output pixels than this go to MIOpen (default: none).  A 128-row tile grid
+# that small cannot fill 256 CUs - ResNet-18 on 32x32 inputs has 128-2048 output pixels in
+# layer2-4 at batch 128 - and with the launches hidden by a hipGraph MIOpen's small-shape
+# kernels win (3072: 46.5k -> 60.7k img/s), but eagerly the native path is faster (41.6k vs
+# 28.6k img/s; BASELINE.md ResNet-18 table), so the default keeps every supported conv native.
+MIN_PIXELS = int(os.environ.get("DPT_CONV_MIN_PIXELS", "0"))
+
+
 def supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups) -> bool:
     if not (ENABLED and x.is_cuda and native_available() and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and x.dim() == 4 and groups == 1):
@@ -44,8 +52,10 @@ def supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, group
     if tuple(dilation) != (1, 1) or stride[0] != stride[1] or padding[0] != padding[1]:
         return False
     cout, cin, r, s = w.shape
+    ho = (x.shape[2] + 2 * padding[0] - r) // stride[0] + 1
+    wo = (x.shape[3] + 2 * padding[1] - s) // stride[1] + 1
     return (cin % 64 == 0 and cout % 64 == 0 and r == s and x.shape[1] == cin
-            and x.is_contiguous(memory_format=_CL))
+            and x.shape[0] * ho * wo >= MIN_PIXELS and x.is_contiguous(memory_format=_CL))
 
 
 def _cl(t: torch.Tensor) -> torch.Tensor:
