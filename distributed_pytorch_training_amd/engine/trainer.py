@@ -18,6 +18,7 @@ Two engines share that contract:
 from __future__ import annotations
 
 import contextlib
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
@@ -95,6 +96,9 @@ class Trainer:
             from ..models.layers import fuse_native_layers
             fuse_native_layers(model)
             native_conv.ENABLED = bool(getattr(args, "native_conv", True))
+            if getattr(args, "cuda_graph", False) and "DPT_CONV_MIN_PIXELS" not in os.environ:
+                # launches hidden by the graph: tiny convs are faster on MIOpen (ops/conv.py)
+                native_conv.MIN_PIXELS = 3072
         # per-step flip cache of the stride-1 backward-data weights (ops/conv.py)
         self._native_conv_cache = self.device.type == "cuda" and native_conv.ENABLED
         params_in_order = [p for p in model.parameters() if p.requires_grad]
