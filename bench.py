@@ -73,8 +73,7 @@ def train_args(a):
             "--grad-dtype", a.grad_dtype, "--lr", "0.1", "--momentum", "0.9", "--weight-decay", "5e-4"]
     if not a.no_amp:
         argv.append("--amp")
-    if not a.no_channels_last:
-        argv.append("--channels-last")
+    argv.append("--no-channels-last" if a.no_channels_last else "--channels-last")
     if a.no_fused_bn:
         argv.append("--no-fused-bn")
     if a.cuda_graph:

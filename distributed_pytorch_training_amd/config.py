@@ -74,8 +74,11 @@ def build_parser() -> argparse.ArgumentParser:
                    help="do not broadcast BN buffers from rank 0 before each forward")
     g.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
                    help="all-reduce wire dtype (bf16 = gradient compression, native only)")
-    g.add_argument("--channels-last", action="store_true",
-                   help="NHWC activations/weights (MIOpen's fast layout on gfx950)")
+    g.add_argument("--channels-last", dest="channels_last", action="store_true", default=None,
+                   help="NHWC activations/weights (default: on for the native engine on a GPU - the "
+                        "layout every fused gfx950 kernel and MIOpen's fast convs use; same math)")
+    g.add_argument("--no-channels-last", dest="channels_last", action="store_false",
+                   help="keep the reference's NCHW layout")
     g.add_argument("--no-fused-bn", dest="fused_bn", action="store_false",
                    help="native impl: keep MIOpen BatchNorm + separate ReLU/add instead of the fused "
                         "gfx950 BN(+add)(+ReLU) kernels (channels_last GPU runs)")
@@ -116,6 +119,10 @@ def parse_args(argv: Optional[Sequence[str]] = None) -> argparse.Namespace:
 
 def finalize(args: argparse.Namespace) -> argparse.Namespace:
     """Fill the data-dependent defaults."""
+    if args.channels_last is None:
+        import torch
+
+        args.channels_last = args.impl == "native" and torch.cuda.is_available()
     if args.image_size is None:
         args.image_size = 32 if args.dataset == "cifar10" else 224
     if args.num_classes is None:
