@@ -213,12 +213,16 @@ float* f32_param(const c10::optional<Tensor>& t, int64_t C, const char* name) {
   return t->data_ptr<float>();
 }
 
-// ---- channels_last bf16 implicit-GEMM convolutions ----------------------------------------
+// ---- channels_last bf16 / fp16 implicit-GEMM convolutions --------------------------------
 void check_cl_bf16(const Tensor& t, const char* name) {
-  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4, name,
-              " must be a 4-d bf16 GPU tensor");
+  TORCH_CHECK(t.is_cuda() && (t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf) && t.dim() == 4, name,
+              " must be a 4-d bf16/fp16 GPU tensor");
   TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name, " must be channels_last contiguous");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+bool is_f16(const Tensor& t) { return t.scalar_type() == at::kHalf; }
+void same_16(const Tensor& a, const Tensor& b, const char* op) {
+  TORCH_CHECK(a.scalar_type() == b.scalar_type(), op, ": operands must share one 16-bit dtype (bf16 or fp16)");
 }
 
 // Returns {y, psum, psq} (psum/psq empty unless want_stats): y = conv2d(x, w, stride, pad).
@@ -228,6 +232,7 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bo
                              int64_t out_w) {
   check_cl_bf16(x, "x");
   check_cl_bf16(w, "w");
+  same_16(x, w, "conv_fwd");
   const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int Cout = w.size(0), R = w.size(2), S = w.size(3);
   TORCH_CHECK(w.size(1) == C, "conv_fwd: channel mismatch");
@@ -248,7 +253,7 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bo
   dpt::launch_conv_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()), N, H, W, C, Cout, R, S, (int)stride, (int)pad,
                        want_stats ? ps.data_ptr<float>() : nullptr, want_stats ? pq.data_ptr<float>() : nullptr,
-                       cur_stream(x), Ho, Wo);
+                       cur_stream(x), Ho, Wo, is_f16(x));
   return {y, ps, pq};
 }
 
@@ -257,6 +262,7 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bo
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t pad) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
+  same_16(dy, w, "conv_dgrad");
   const int Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
   TORCH_CHECK(dy.size(1) == Cout, "conv_dgrad: channel mismatch");
   TORCH_CHECK(dpt::conv_supported(Cout, C), "conv_dgrad: needs C % 64 == 0 and Cout % 64 == 0");
@@ -267,7 +273,8 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t pad) {
                       dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   c10::hip::HIPGuard guard(dy.device().index());
   dpt::launch_conv_dgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
-                         reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, (int)pad, cur_stream(dy));
+                         reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, (int)pad, cur_stream(dy),
+                         is_f16(dy));
   return dx;
 }
 
@@ -284,6 +291,8 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
   check_cl_bf16(bn_x, "bn_x");
+  same_16(dy, w, "conv_dgrad_bnstats");
+  same_16(dy, bn_x, "conv_dgrad_bnstats");
   const int Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
   TORCH_CHECK(dy.size(1) == Cout && dpt::conv_supported(Cout, C), "conv_dgrad_bnstats: bad shapes");
   TORCH_CHECK(R - 1 - pad >= 0 && S == R, "conv_dgrad_bnstats: needs square kernel and pad <= R-1");
@@ -297,12 +306,15 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
   if (res) {
     check_cl_bf16(*bn_y, "bn_y");
     check_cl_bf16(*bn_res, "bn_res");
+    same_16(dy, *bn_y, "conv_dgrad_bnstats");
+    same_16(dy, *bn_res, "conv_dgrad_bnstats");
     TORCH_CHECK(bn_y->sizes() == bn_x.sizes() && bn_res->sizes() == bn_x.sizes(),
                 "conv_dgrad_bnstats: bn_y / bn_res must match bn_x");
   }
   const bool pre = w_flipped.has_value() && w_flipped->defined();
   if (pre) {
     check_cl_bf16(*w_flipped, "w_flipped");
+    same_16(dy, *w_flipped, "conv_dgrad_bnstats");
     TORCH_CHECK(w_flipped->size(0) == C && w_flipped->size(1) == Cout && w_flipped->size(2) == R &&
                     w_flipped->size(3) == S, "conv_dgrad_bnstats: w_flipped must be [C, Cout, R, S]");
   }
@@ -315,6 +327,7 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
   if (two) {
     TORCH_CHECK(res, "conv_dgrad_bnstats: bn_x2 needs bn_y / bn_res");
     check_cl_bf16(*bn_x2, "bn_x2");
+    same_16(dy, *bn_x2, "conv_dgrad_bnstats");
     TORCH_CHECK(bn_x2->sizes() == bn_x.sizes(), "conv_dgrad_bnstats: bn_x2 must match bn_x");
   }
   auto p3 = at::empty({two ? C : 0, two ? mt : 0}, dy.options().dtype(at::kFloat));
@@ -332,7 +345,7 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
                                  res ? reinterpret_cast<const uint16_t*>(bn_res->data_ptr()) : nullptr,
                                  two ? reinterpret_cast<const uint16_t*>(bn_x2->data_ptr()) : nullptr,
                                  two ? f32_param(bn_mean2, C, "bn_mean2") : nullptr,
-                                 two ? p3.data_ptr<float>() : nullptr);
+                                 two ? p3.data_ptr<float>() : nullptr, is_f16(dy));
   return {dx, p1, p2, p3};
 }
 
@@ -341,6 +354,7 @@ std::vector<Tensor> conv_dgrad_s2(Tensor dy, Tensor w, int64_t pad, int64_t H, i
                                   c10::optional<Tensor> bn_mean, c10::optional<Tensor> bn_coef) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
+  same_16(dy, w, "conv_dgrad_s2");
   const int Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
   TORCH_CHECK(dy.size(1) == Cout && dpt::conv_supported(Cout, C), "conv_dgrad_s2: needs C, Cout % 64 == 0");
   const int N = dy.size(0), Ho = dy.size(2), Wo = dy.size(3);
@@ -351,6 +365,7 @@ std::vector<Tensor> conv_dgrad_s2(Tensor dy, Tensor w, int64_t pad, int64_t H, i
   Tensor p1, p2;
   if (bnb) {
     check_cl_bf16(*bn_x, "bn_x");
+    same_16(dy, *bn_x, "conv_dgrad_s2");
     TORCH_CHECK(bn_x->sizes() == dx.sizes(), "conv_dgrad_s2: bn_x must match the conv input");
     const int chunks = dpt::conv_dgrad_s2_chunks(N, (int)H, (int)W, R, S, (int)pad);
     p1 = at::empty({C, chunks}, dy.options().dtype(at::kFloat));
@@ -362,7 +377,7 @@ std::vector<Tensor> conv_dgrad_s2(Tensor dy, Tensor w, int64_t pad, int64_t H, i
                             cur_stream(dy), bnb ? reinterpret_cast<const uint16_t*>(bn_x->data_ptr()) : nullptr,
                             bnb ? f32_param(bn_mean, C, "bn_mean") : nullptr,
                             bnb ? f32_param(bn_coef, 2 * C, "bn_coef") : nullptr,
-                            bnb ? p1.data_ptr<float>() : nullptr, bnb ? p2.data_ptr<float>() : nullptr);
+                            bnb ? p1.data_ptr<float>() : nullptr, bnb ? p2.data_ptr<float>() : nullptr, is_f16(dy));
   if (!bnb) return {dx};
   return {dx, p1, p2};
 }
@@ -400,6 +415,7 @@ std::vector<Tensor> conv_wt_flip_multi(std::vector<Tensor> ws) {
 Tensor conv_dgrad_preflipped(Tensor dy, Tensor wt, int64_t pad) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(wt, "w_flipped");
+  same_16(dy, wt, "conv_dgrad_preflipped");
   const int C = wt.size(0), Cout = wt.size(1), R = wt.size(2), S = wt.size(3);
   TORCH_CHECK(dy.size(1) == Cout && dpt::conv_supported(Cout, C), "conv_dgrad_preflipped: bad shapes");
   TORCH_CHECK(R - 1 - pad >= 0 && S == R, "conv_dgrad_preflipped: needs square kernel and pad <= R-1");
@@ -409,7 +425,7 @@ Tensor conv_dgrad_preflipped(Tensor dy, Tensor wt, int64_t pad) {
   c10::hip::HIPGuard guard(dy.device().index());
   dpt::launch_conv_fwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                        reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, 1, (int)(R - 1 - pad),
-                       nullptr, nullptr, cur_stream(dy));
+                       nullptr, nullptr, cur_stream(dy), 0, 0, is_f16(dy));
   return dx;
 }
 
@@ -418,6 +434,7 @@ Tensor conv_dgrad_preflipped(Tensor dy, Tensor wt, int64_t pad) {
 std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
+  same_16(dy, w, "conv_dgrad_flip");
   const int Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
   TORCH_CHECK(dy.size(1) == Cout, "conv_dgrad: channel mismatch");
   TORCH_CHECK(dpt::conv_supported(Cout, C), "conv_dgrad: needs C % 64 == 0 and Cout % 64 == 0");
@@ -431,7 +448,7 @@ std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad) {
   auto dx = at::empty({N, C, Ho, Wo}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   dpt::launch_conv_fwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                        reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, 1, (int)(R - 1 - pad),
-                       nullptr, nullptr, st);
+                       nullptr, nullptr, st, 0, 0, is_f16(dy));
   return {dx, wt};
 }
 
@@ -439,6 +456,7 @@ std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad) {
 Tensor conv_wgrad(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stride, int64_t pad, bool fp32_out) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(x, "x");
+  same_16(dy, x, "conv_wgrad");
   TORCH_CHECK(wshape.size() == 4, "conv_wgrad: weight shape must be [Cout, C, R, S]");
   const int Cout = wshape[0], C = wshape[1], R = wshape[2], S = wshape[3];
   const int N = x.size(0), H = x.size(2), W = x.size(3);
@@ -451,14 +469,14 @@ Tensor conv_wgrad(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stri
   // the output size comes from dy (covers asymmetric padding)
   auto pl = dpt::conv_wgrad_plan(N, H, W, C, Cout, R, S, (int)stride, (int)pad, (int)dy.size(2), (int)dy.size(3));
   TORCH_CHECK((int64_t)N * pl.Ho * pl.Wo < (1ll << 31), "conv_wgrad: too many pixels");
-  auto dw = at::empty({Cout, C, R, S}, x.options().dtype(fp32_out ? at::kFloat : at::kBFloat16)
+  auto dw = at::empty({Cout, C, R, S}, x.options().dtype(fp32_out ? at::kFloat : x.scalar_type())
                                           .memory_format(at::MemoryFormat::ChannelsLast));
   const int64_t pf = pl.splits == 1 && !fp32_out ? (int64_t)Cout * C * R * S : pl.part_floats;
   auto part = at::empty({std::max<int64_t>(pf, 4)}, x.options().dtype(at::kFloat));
   c10::hip::HIPGuard guard(x.device().index());
   dpt::launch_conv_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                         part.data_ptr<float>(), dw.data_ptr(), fp32_out ? 0 : 1, N, H, W, C, Cout, R, S, (int)stride,
-                         (int)pad, pl, cur_stream(x));
+                         part.data_ptr<float>(), dw.data_ptr(), fp32_out ? 0 : (is_f16(x) ? 2 : 1), N, H, W, C, Cout, R,
+                         S, (int)stride, (int)pad, pl, cur_stream(x), is_f16(x));
   return dw;
 }
 
@@ -517,16 +535,17 @@ Tensor attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, int64_t heads, 
 
 // 2x2 space-to-depth of a channels_last [N, C<=4, H, W] fp32/bf16 image -> channels_last bf16
 // [N, 16, H/2, W/2] (channel (a*2 + b)*4 + c)
-Tensor space_to_depth2(Tensor x) {
+Tensor space_to_depth2(Tensor x, bool out_f16) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
               "space_to_depth2: x must be a 4-d fp32/bf16 GPU tensor");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "space_to_depth2: x must be channels_last");
   const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   TORCH_CHECK(C <= 4 && H % 2 == 0 && W % 2 == 0, "space_to_depth2: needs C <= 4 and even H, W");
-  auto a = at::empty({N, 16, H / 2, W / 2}, x.options().dtype(at::kBFloat16).memory_format(at::MemoryFormat::ChannelsLast));
+  auto a = at::empty({N, 16, H / 2, W / 2},
+                     x.options().dtype(out_f16 ? at::kHalf : at::kBFloat16).memory_format(at::MemoryFormat::ChannelsLast));
   c10::hip::HIPGuard guard(x.device().index());
   dpt::launch_space_to_depth2(x.data_ptr(), x.scalar_type() == at::kBFloat16, reinterpret_cast<uint16_t*>(a.data_ptr()),
-                              N, H, W, C, cur_stream(x));
+                              N, H, W, C, cur_stream(x), out_f16);
   return a;
 }
 
@@ -1001,7 +1020,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn_x") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_coef") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"),
         py::arg("out_h") = 0, py::arg("out_w") = 0);
-  m.def("space_to_depth2", &space_to_depth2, py::arg("x"));
+  m.def("space_to_depth2", &space_to_depth2, py::arg("x"), py::arg("out_f16") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("grad_output"), py::arg("x"), py::arg("weight_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("fp32_out"));
   m.def("im2col", &im2col, py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("Kp"));

@@ -142,8 +142,9 @@ void conv_set_variant(int v);
 // Ho/Wo > 0: explicit output size (padding applied on top/left only beyond what it needs)
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
                      int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s, int Ho = 0,
-                     int Wo = 0);
-// backward-weight: dw [Cout,R,S,C] (kind 0 f32 / 1 bf16) = sum over pixels of dy x x-shifted;
+                     int Wo = 0, bool f16 = false);
+// f16: fp16 operands/outputs throughout (bf16 otherwise) - every conv launcher below takes it.
+// backward-weight: dw [Cout,R,S,C] (kind 0 f32 / 1 bf16 / 2 f16) = sum over pixels of dy x x-shifted;
 // part: plan.part_floats floats of split-K scratch.  C % 64 == 0, Cout % 64 == 0.
 struct ConvWgradPlan {
   int Ho, Wo, bmw, bnw, splits, steps_per_split;
@@ -153,7 +154,7 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
                               int Wo = 0);
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void* dw, int dw_kind, int N, int H,
                        int W, int C, int Cout, int R, int S, int stride, int pad, const ConvWgradPlan& plan,
-                       hipStream_t s);
+                       hipStream_t s, bool f16 = false);
 // stride-1 backward-data (flipped weight wt [C,R,S,Cout]) + the backward statistics of the
 // BatchNorm+ReLU (input bnx, mean, coef [a|b]) that produced the conv's input: bp1/bp2 [C][m_tiles]
 void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int Ho, int Wo, int Cout,
@@ -161,7 +162,7 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
                                const float* bn_coef, float* bp1, float* bp2, hipStream_t s,
                                const uint16_t* bny = nullptr, const uint16_t* bnres = nullptr,
                                const uint16_t* bnx2 = nullptr, const float* bn_mean2 = nullptr,
-                               float* bp3 = nullptr);
+                               float* bp3 = nullptr, bool f16 = false);
 // many weights flipped/transposed (wt[ci][R-1-r][S-1-s][co] = w[co][r][s][ci]) in one launch
 constexpr int kWtFlipMax = 64;
 struct WtFlipBatch {
@@ -176,15 +177,16 @@ void launch_conv_wt_flip_multi(WtFlipBatch b, hipStream_t s);
 void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout,
                           int C, int R, int S, int pad, int H, int W, hipStream_t s, const uint16_t* bnx = nullptr,
                           const float* bn_mean = nullptr, const float* bn_coef = nullptr, float* bp1 = nullptr,
-                          float* bp2 = nullptr);
+                          float* bp2 = nullptr, bool f16 = false);
 // [C][chunks] partial columns the BN-statistics variant of launch_conv_dgrad_s2 writes
 int conv_dgrad_s2_chunks(int N, int H, int W, int R, int S, int pad);
 // stride-1 backward-data straight from the KRSC weight w [Cout,R,S,C]: dy [N,Ho,Wo,Cout] -> dx [N,Ho,Wo,C]
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout, int C,
-                       int R, int S, int pad, hipStream_t s);
+                       int R, int S, int pad, hipStream_t s, bool f16 = false);
 // space-to-depth stem input: x [N,H,W,C] fp32/bf16 (channels_last, H, W even, C <= 4) ->
 // a [N, H/2, W/2, 16] bf16 with channel (a*2 + b)*4 + c = x[2i + a][2j + b][c] (zero for c >= C)
-void launch_space_to_depth2(const void* x, bool x_bf16, uint16_t* a, int N, int H, int W, int C, hipStream_t s);
+void launch_space_to_depth2(const void* x, bool x_bf16, uint16_t* a, int N, int H, int W, int C, hipStream_t s,
+                            bool out_f16 = false);
 // im2col for narrow-input convs: a [N*Ho*Wo, Kp] bf16 (k = (r*S+s)*C + c, zero past R*S*C)
 void launch_im2col(const void* x, bool x_bf16, uint16_t* a, int N, int H, int W, int C, int R, int S, int stride,
                    int pad, int Kp, hipStream_t s);

@@ -190,7 +190,7 @@ def bn2_add_relu_train(x, bn, x2, bn2):
     x2 = _cl(x2.to(x.dtype))
     partials = x.__dict__.pop("_dpt_bn_partials", None)
     partials2 = x2.__dict__.pop("_dpt_bn_partials", None)
-    own_slot = {} if (BNR_FUSE and x.dtype == torch.bfloat16) else None
+    own_slot = {} if (BNR_FUSE and x.dtype in (torch.bfloat16, torch.float16)) else None
     out = _BN2AddReLUPair.apply(x, x2, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
                                 bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var, bn2.num_batches_tracked,
                                 bn.momentum, bn.eps, bn2.momentum, bn2.eps, partials, partials2, own_slot)
@@ -218,7 +218,8 @@ def bn_act_train(x: torch.Tensor, residual: Optional[torch.Tensor], weight, bias
     partials = x.__dict__.pop("_dpt_bn_partials", None)
     # block tails: own_slot receives the identity-path gradient from the next block's tail
     # backward (which runs before the backward of the conv consuming our conv-path output)
-    own_slot = {} if (pair and relu and residual is not None and BNR_FUSE and x.dtype == torch.bfloat16) else None
+    own_slot = {} if (pair and relu and residual is not None and BNR_FUSE
+                      and x.dtype in (torch.bfloat16, torch.float16)) else None
     fn = _BNActTrainPair if pair else _BNActTrain
     out = fn.apply(x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
                    partials, (own_slot, res_slot))

@@ -1,4 +1,4 @@
-"""Channels-last bf16 convolution autograd op on the hand-written MFMA kernels
+"""Channels-last bf16 / fp16 convolution autograd op on the hand-written MFMA kernels
 (csrc/kernels/conv_kernels.hip).
 
 forward   implicit-GEMM conv; with ``bn_stats`` its epilogue also emits the per-channel
@@ -23,6 +23,8 @@ import torch
 from . import native, native_available
 
 _CL = torch.channels_last
+# element types of the MFMA kernels (bf16 and fp16 operands, fp32 accumulation)
+_DT16 = (torch.bfloat16, torch.float16)
 ENABLED = os.environ.get("DPT_NATIVE_CONV", "1") != "0"
 # Backward-data of a conv fed by a fused BN+ReLU also sums that BN's backward statistics in its
 # epilogue (the BN backward then skips its statistics pass).
@@ -46,8 +48,8 @@ MIN_PIXELS = int(os.environ.get("DPT_CONV_MIN_PIXELS", "0"))
 
 
 def supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups) -> bool:
-    if not (ENABLED and x.is_cuda and native_available() and x.dtype == torch.bfloat16
-            and w.dtype == torch.bfloat16 and x.dim() == 4 and groups == 1):
+    if not (ENABLED and x.is_cuda and native_available() and x.dtype in _DT16
+            and w.dtype == x.dtype and x.dim() == 4 and groups == 1):
         return False
     if tuple(dilation) != (1, 1) or stride[0] != stride[1] or padding[0] != padding[1]:
         return False
@@ -64,7 +66,7 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
 
 def _backward(ctx, dy):
     x, w = ctx.saved_tensors
-    dy = _cl(dy.to(torch.bfloat16))
+    dy = _cl(dy.to(x.dtype))
     s, p = ctx.stride, ctx.pad
     dx = dw = None
     if ctx.needs_input_grad[0]:
@@ -143,7 +145,7 @@ def _flipped(w: torch.Tensor):
 
 
 def _dres_ok(dres, x) -> bool:
-    return (dres is not None and dres.dtype == torch.bfloat16 and dres.shape == x.shape
+    return (dres is not None and dres.dtype == x.dtype and dres.shape == x.shape
             and dres.is_contiguous(memory_format=_CL))
 
 
@@ -222,7 +224,7 @@ def take_bn_partials(x: torch.Tensor):
 def s2d_stem_supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups) -> bool:
     """ResNet's 7x7/2 pad-3 stem on <= 4 input channels: space-to-depth + 4x4 MFMA conv."""
     if not (ENABLED and x.is_cuda and native_available() and x.dim() == 4 and groups == 1
-            and x.dtype in (torch.float32, torch.bfloat16) and w.dtype == torch.bfloat16):
+            and x.dtype in (torch.float32, torch.bfloat16) and w.dtype in _DT16):
         return False
     cout, cin, r, s = w.shape
     return (cin <= 4 and cout % 64 == 0 and (r, s) == (7, 7) and tuple(stride) == (2, 2)
@@ -242,7 +244,7 @@ def s2d_stem_conv2d(x: torch.Tensor, w: torch.Tensor, bn_stats: bool = False) ->
     input path), top/left padding 2, output H/2 x W/2.  The weight re-indexing is plain torch ops,
     so autograd maps the 4x4 weight gradient back onto the 7x7 one."""
     cout, cin = w.shape[0], w.shape[1]
-    x2 = native().space_to_depth2(x)
+    x2 = native().space_to_depth2(x, w.dtype == torch.float16)
     wk = torch.nn.functional.pad(w.permute(0, 2, 3, 1), (0, 4 - cin, 1, 0, 1, 0))       # [Co, 8, 8, 4]
     w2 = wk.reshape(cout, 4, 2, 4, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(cout, 4, 4, 16)
     w2 = w2.permute(0, 3, 1, 2)                                                         # [Co, 16, 4, 4] cl

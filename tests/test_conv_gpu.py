@@ -439,3 +439,77 @@ def test_downsample_bn_folded_into_block_tail(cuda, monkeypatch):
     assert not nc._BNB_PARTIALS
     for a, b in zip(*res):
         torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item() + 1e-6)
+
+
+F16_SHAPES = [(2, 64, 8, 8, 64, 1, 1, 0), (2, 128, 9, 9, 256, 3, 1, 1), (2, 64, 15, 15, 128, 3, 2, 1),
+              (2, 256, 14, 14, 128, 1, 2, 0)]
+
+
+@pytest.mark.parametrize("shape", F16_SHAPES)
+def test_conv_fp16_matches_fp32(cuda, shape):
+    """fp16 operands on the same kernels (v_mfma_f32_32x32x16_f16, fp16 epilogue rounding):
+    forward (+ BN partials), backward-data (stride 1 and 2), backward-weight."""
+    N, C, H, W, Cout, k, s, p = shape
+    g = torch.Generator(device=cuda).manual_seed(3)
+    x = torch.randn(N, C, H, W, device=cuda, generator=g).half().contiguous(memory_format=CL)
+    w = (torch.randn(Cout, C, k, k, device=cuda, generator=g) / (C * k * k) ** 0.5).half().contiguous(memory_format=CL)
+    y, ps, pq = ops.native().conv_fwd(x, w, s, p, True, 0, 0)
+    ref = F.conv2d(x.float(), w.float(), stride=s, padding=p)
+    assert y.dtype == torch.float16 and y.is_contiguous(memory_format=CL)
+    torch.testing.assert_close(y.float(), ref, rtol=5e-3, atol=5e-3)
+    torch.testing.assert_close(ps.sum(1), y.float().sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    gy = torch.randn(ref.shape, device=cuda, generator=g).half().contiguous(memory_format=CL)
+    if s == 1:
+        dx = ops.native().conv_dgrad_flip(gy, w, p)[0]
+    else:
+        dx = ops.native().conv_dgrad_s2(gy, w, p, H, W)[0]
+    dref = torch.nn.grad.conv2d_input(x.shape, w.float(), gy.float(), stride=s, padding=p)
+    assert dx.dtype == torch.float16
+    torch.testing.assert_close(dx.float(), dref, rtol=5e-3, atol=1e-2)
+    dw = ops.native().conv_wgrad(gy, x, list(w.shape), s, p, False)
+    wref = torch.nn.grad.conv2d_weight(x.float(), w.shape, gy.float(), stride=s, padding=p)
+    assert dw.dtype == torch.float16
+    torch.testing.assert_close(dw.float(), wref, rtol=1e-2, atol=1e-2 * wref.abs().max().item())
+
+
+def test_resnet50_fp16_native_step(cuda):
+    """Whole ResNet-50 training step under fp16 autocast (the reference's AMP dtype) on the
+    MFMA convs and fused BN: finite loss, and the update no further from fp32 than the
+    MIOpen fp16 step's is (same relative criterion as the bf16 test above)."""
+    import copy
+
+    from distributed_pytorch_training_amd.config import parse_args
+    from distributed_pytorch_training_amd.engine.trainer import Trainer
+    from distributed_pytorch_training_amd.models import build_model
+    from distributed_pytorch_training_amd.ops import conv as native_conv
+
+    torch.manual_seed(0)
+    base = build_model("resnet50", 100, cuda, image_size=64, channels_last=True)
+    common = ["--model", "resnet50", "--dataset", "synthetic", "--channels-last", "--num-classes", "100",
+              "--lr", "0.05"]
+    amp = ["--amp", "--amp-dtype", "fp16"]
+    runs = {
+        "nat": (Trainer(copy.deepcopy(base), parse_args(common + amp), 0, 1, cuda, log=lambda s: None), True),
+        "mio": (Trainer(copy.deepcopy(base), parse_args(common + amp + ["--no-native-conv"]), 0, 1, cuda,
+                        log=lambda s: None), False),
+        "f32": (Trainer(copy.deepcopy(base), parse_args(common + ["--no-native-conv"]), 0, 1, cuda,
+                        log=lambda s: None), False),
+    }
+    g = torch.Generator(device=cuda).manual_seed(7)
+    x = torch.randn(32, 3, 64, 64, device=cuda, generator=g).contiguous(memory_format=CL)
+    y = torch.randint(0, 100, (32,), device=cuda, generator=g)
+    loss = {}
+    for k, (tr, enabled) in runs.items():
+        native_conv.ENABLED = enabled
+        loss[k] = tr.train_step(x, y)[1].item()
+    native_conv.ENABLED = True
+    assert all(v == v and abs(v) < 1e4 for v in loss.values()), loss
+
+    def upd(k):
+        return torch.cat([(a.detach() - b.detach()).double().reshape(-1)
+                          for a, b in zip(runs[k][0].module.parameters(), base.parameters())])
+
+    u32 = upd("f32")
+    e_nat = ((upd("nat") - u32).norm() / u32.norm()).item()
+    e_mio = ((upd("mio") - u32).norm() / u32.norm()).item()
+    assert e_nat <= 1.5 * e_mio + 0.02, (e_nat, e_mio)

@@ -15,7 +15,9 @@ pytestmark = pytest.mark.gpu
 def _pair(cuda, model_name, extra, image=32, classes=10):
     torch.manual_seed(0)
     base = build_model(model_name, classes, cuda, image_size=image)
-    a = parse_args(["--model", model_name, "--dataset", "synthetic", *extra])
+    # engine parity (reducer, optimizer, scaler): both in the reference's NCHW layout, so the
+    # comparison is not confounded by NHWC-vs-NCHW conv algorithm differences
+    a = parse_args(["--model", model_name, "--dataset", "synthetic", "--no-channels-last", *extra])
     b = parse_args(["--model", model_name, "--dataset", "synthetic", "--impl", "torch", *extra])
     return (Trainer(copy.deepcopy(base), a, 0, 1, cuda, log=lambda s: None),
             Trainer(copy.deepcopy(base), b, 0, 1, cuda, log=lambda s: None))
