@@ -724,17 +724,20 @@ std::vector<Tensor> bn_bwd_partials(Tensor dy, Tensor x, c10::optional<Tensor> w
   return {dx, dg, db};
 }
 
-std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t stride, int64_t pad) {
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t stride, int64_t pad, c10::optional<Tensor> bn_coef) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "maxpool: x must be a 4-D channels_last GPU tensor");
   const int64_t B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(!(bn_coef.has_value() && bn_coef->defined()) || k == 3, "maxpool: the folded BN needs a 3x3 window");
   TORCH_CHECK(C % 8 == 0 && k >= 1 && k * k <= 255 && stride >= 1 && pad >= 0 && pad <= k / 2, "maxpool: bad config");
   const int64_t Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
   auto y = at::empty({B, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto idx = at::empty({B, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
   c10::hip::HIPGuard guard(x.device().index());
   dpt::launch_maxpool_fwd(bn_dtype(x), x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), B, (int)H, (int)W,
-                          (int)C, (int)Ho, (int)Wo, (int)k, (int)stride, (int)pad, cur_stream(x));
+                          (int)C, (int)Ho, (int)Wo, (int)k, (int)stride, (int)pad, cur_stream(x),
+                          bn_coef.has_value() && bn_coef->defined() ? f32_param(bn_coef, 2 * C, "bn_coef") : nullptr);
+  
   return {y, idx};
 }
 
@@ -1013,7 +1016,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("copy_rows16", &copy_rows16, py::arg("src"), py::arg("dst"));
   m.def("bias_grad16", &bias_grad16, py::arg("grad"), py::arg("out_kind"));
   m.def("sum_partials", &sum_partials, py::arg("part"), py::arg("out_kind"));
-  m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("stride"), py::arg("pad"));
+  m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("stride"), py::arg("pad"),
+        py::arg("bn_coef") = py::none());
   m.def("gap_bwd", &gap_bwd, py::arg("g"), py::arg("H"), py::arg("W"), py::arg("dtype"));
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("grad_output"), py::arg("idx"), py::arg("H"), py::arg("W"),
         py::arg("k"), py::arg("stride"), py::arg("pad"), py::arg("grad_output2") = py::none(),

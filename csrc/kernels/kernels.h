@@ -82,8 +82,9 @@ void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, co
                    float* dgamma, float* dbeta, void* dx, void* dz, float* workspace, bool relu, hipStream_t s);
 
 // pool_kernels.hip  (channels_last [B,H,W,C], C % 8 == 0; idx = window-local uint8 argmax)
+// coef (optional, 3x3 windows): [a | b] of a BatchNorm+ReLU folded into the pool's loads
 void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t B, int H, int W, int C, int Ho,
-                        int Wo, int K, int S, int P, hipStream_t s);
+                        int Wo, int K, int S, int P, hipStream_t s, const float* coef = nullptr);
 // global-average-pool backward: dx [N, HW, C] (dtype) = g [N, C] (gdtype) / HW
 void launch_gap_bwd(int dtype, int gdtype, const void* g, void* dx, int64_t N, int64_t HW, int64_t C, hipStream_t s);
 // dy2: optional second output gradient, summed in (pool output with two consumers)

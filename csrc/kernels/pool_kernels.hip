@@ -14,6 +14,8 @@
 // first window element instead of the max for the fp32 instantiation on gfx950 (bf16 was
 // right); the analytic clipped window seeded with -inf below is what tests/test_bn_gpu.py
 // verifies for every dtype.
+#include <stdexcept>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -155,10 +157,15 @@ __global__ __launch_bounds__(kBlock) void maxpool_bwd_kernel(const void* __restr
 // max scan (the general kernel's runtime-bounded loop waits for each load in turn).  Out-of-
 // image taps load a clamped in-bounds address and are skipped by the scan, which visits the
 // taps in the same (ky, kx) order - identical max / argmax / NaN semantics.
-template <int DT>
+// AFF: the pool input is relu(x*a + b) of a BatchNorm whose apply pass is folded in here (the
+// ResNet stem): every loaded element goes through the apply's exact arithmetic and rounding
+// (fma, NaN-propagating ReLU, round to the storage type) before the max, so values, argmax
+// and tie-breaking equal pooling the materialised BN output - which is never written.
+template <int DT, bool AFF = false>
 __global__ __launch_bounds__(kBlock) void maxpool3_fwd_kernel(const void* __restrict__ x, void* __restrict__ y,
                                                               uint8_t* __restrict__ idx, int H, int W, int C, int Ho,
-                                                              int Wo, int S, int P, uint32_t total) {
+                                                              int Wo, int S, int P, uint32_t total,
+                                                              const float* __restrict__ coef = nullptr) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= total) return;
   const uint32_t cg8 = (uint32_t)C >> 3;
@@ -179,6 +186,21 @@ __global__ __launch_bounds__(kBlock) void maxpool3_fwd_kernel(const void* __rest
       const int ix = min(max(ox * S - P + kx, 0), W - 1);
       pool_load8(DT, x, ((b * H + iy) * W + ix) * C + cg * 8, v[ky * 3 + kx]);
     }
+  }
+  if (AFF) {
+    float ca[8], cb[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { ca[k] = coef[cg * 8 + k]; cb[k] = coef[C + cg * 8 + k]; }
+#pragma unroll
+    for (int q = 0; q < 9; ++q)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float o = __builtin_fmaf(v[q][k], ca[k], cb[k]);
+        o = o < 0.0f ? 0.0f : o;
+        if (DT == 1) o = bf16_to_f32(f32_to_bf16(o));
+        else if (DT == 2) o = f16_to_f32(pool_to16(2, o));
+        v[q][k] = o;
+      }
   }
   float best[8];
   int arg[8];
@@ -371,12 +393,20 @@ static void maxpool_bwd_dispatch(int dtype, dim3 grid, const void* dy, const voi
 }
 
 void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t B, int H, int W, int C, int Ho,
-                        int Wo, int K, int S, int P, hipStream_t s) {
+                        int Wo, int K, int S, int P, hipStream_t s, const float* coef) {
   const int64_t total = B * Ho * Wo * (C / 8);
   if (total == 0) return;
   const dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
   if (K == 3 && total + kBlock < (int64_t(1) << 32)) {
     const dim3 block(kBlock);
+    if (coef != nullptr) {
+      switch (dtype) {
+        case 0: hipLaunchKernelGGL((maxpool3_fwd_kernel<0, true>), grid, block, 0, s, x, y, idx, H, W, C, Ho, Wo, S, P, (uint32_t)total, coef); break;
+        case 1: hipLaunchKernelGGL((maxpool3_fwd_kernel<1, true>), grid, block, 0, s, x, y, idx, H, W, C, Ho, Wo, S, P, (uint32_t)total, coef); break;
+        default: hipLaunchKernelGGL((maxpool3_fwd_kernel<2, true>), grid, block, 0, s, x, y, idx, H, W, C, Ho, Wo, S, P, (uint32_t)total, coef); break;
+      }
+      return;
+    }
     switch (dtype) {
       case 0: hipLaunchKernelGGL(maxpool3_fwd_kernel<0>, grid, block, 0, s, x, y, idx, H, W, C, Ho, Wo, S, P, (uint32_t)total); break;
       case 1: hipLaunchKernelGGL(maxpool3_fwd_kernel<1>, grid, block, 0, s, x, y, idx, H, W, C, Ho, Wo, S, P, (uint32_t)total); break;
@@ -384,6 +414,7 @@ void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t
     }
     return;
   }
+  if (coef != nullptr) throw std::runtime_error("maxpool_fwd: the folded BatchNorm apply needs a 3x3 window");
   if (total + kBlock < (int64_t(1) << 32)) maxpool_fwd_dispatch<uint32_t>(dtype, grid, x, y, idx, B, H, W, C, Ho, Wo, K, S, P, s);
   else maxpool_fwd_dispatch<uint64_t>(dtype, grid, x, y, idx, B, H, W, C, Ho, Wo, K, S, P, s);
 }

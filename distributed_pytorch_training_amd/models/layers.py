@@ -103,6 +103,21 @@ def bn_act_block_out(bn: nn.Module, x: torch.Tensor, residual):
     return bn_act(bn, x, True, residual)
 
 
+# 0 keeps the stem BN apply as its own pass (A/B)
+STEM_FUSE = os.environ.get("DPT_STEM_FUSE", "1") != "0"
+
+
+def bn_relu_maxpool(bn: nn.Module, pool: nn.Module, x: torch.Tensor):
+    """``pool(relu(bn(x)))`` - the ResNet stem.  With a fused BN and the stem's pair pool in
+    training it is one op whose BN output is never materialised (ops/pool.py
+    ``_BNReLUMaxPoolPair``); otherwise the plain composition."""
+    if (STEM_FUSE and isinstance(bn, FusedBatchNorm2d) and isinstance(pool, FusedMaxPool2d) and pool.dpt_pair
+            and bn.training and torch.is_grad_enabled() and bn.can_fuse(x)
+            and fused_pool.bn_relu_maxpool_supported(x, bn, pool)):
+        return fused_pool.bn_relu_maxpool_train(x, bn)
+    return pool(bn_act(bn, x))
+
+
 def split_block_input(x):
     """(conv-path input, identity-path input) of a residual block."""
     return x if isinstance(x, tuple) else (x, x)

@@ -25,7 +25,7 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
-from .layers import bn_act, bn_act_block_out, downsample_branch, split_block_input
+from .layers import bn_act, bn_act_block_out, bn_relu_maxpool, downsample_branch, split_block_input
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -132,7 +132,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(bn_act(self.bn1, self.conv1(x)))
+        x = bn_relu_maxpool(self.bn1, self.maxpool, self.conv1(x))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if isinstance(x, tuple):  # fused block tails hand (conv-path, identity-path) aliases along
             x = x[0]

@@ -116,3 +116,57 @@ def gap_supported(x: torch.Tensor) -> bool:
 def global_avg_pool_nhwc(x: torch.Tensor) -> torch.Tensor:
     return _GlobalAvgPoolNHWC.apply(x)
 
+
+class _BNReLUMaxPoolPair(torch.autograd.Function):
+    """ResNet stem ``maxpool3x3/2(relu(bn(x)))`` in training mode as ONE op, pair outputs.
+
+    Forward: the BN's statistics (from the stem conv's epilogue partials), running-stat update
+    and coefficients, then the pool reads x and applies the BN+ReLU to every loaded element with
+    the apply pass's exact arithmetic and rounding (pool_kernels.hip AFF) - the 112x112 BN
+    output is never written.  Backward: the pool's gather sums the two output gradients and the
+    BN's backward statistics (BNS), then the BN backward applies from those partials; the ReLU
+    mask is recomputed from x, so nothing of the BN output is needed there either."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, num_batches, momentum, eps, partials):
+        C = native()
+        ps, pq = partials if partials is not None else (None, None)
+        _, mean, invstd, coef = C.bn_fwd_train(x, None, weight, bias, running_mean, running_var, num_batches,
+                                               float(momentum), float(eps), True, ps, pq, False)
+        y, idx = C.maxpool_fwd(x, 3, 2, 1, coef)
+        ctx.save_for_backward(x, weight, mean, invstd, coef, idx)
+        ctx.mark_non_differentiable(idx)
+        ctx.set_materialize_grads(False)
+        return y, y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, dy, dy2):
+        x, weight, mean, invstd, coef, idx = ctx.saved_tensors
+        if dy is None:
+            dy, dy2 = dy2, None
+        if dy is None:
+            return (None,) * 9
+        dy = _cl(dy)
+        if dy2 is not None:
+            dy2 = _cl(dy2.to(dy.dtype))
+        C = native()
+        dz, p1, p2 = C.maxpool_bwd(dy, idx, x.shape[2], x.shape[3], 3, 2, 1, dy2, x, mean, coef)
+        want = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        dx, dg, db = C.bn_bwd_partials(dz, x, weight, mean, invstd, coef, p1, p2, bool(want))
+        return (dx, dg if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None) + (None,) * 6
+
+
+def bn_relu_maxpool_supported(x: torch.Tensor, bn, pool) -> bool:
+    as_int = lambda v: v if isinstance(v, int) else (v[0] if len(set(v)) == 1 else None)
+    C = x.shape[1] if x.dim() == 4 else 0
+    return (maxpool_supported(x, pool.kernel_size, pool.stride, pool.padding, pool.dilation, pool.ceil_mode)
+            and (as_int(pool.kernel_size), as_int(pool.stride), as_int(pool.padding)) == (3, 2, 1)
+            and not pool.return_indices and C <= 512 and (C & (C - 1)) == 0
+            and x.dtype in (torch.bfloat16, torch.float16, torch.float32))
+
+
+def bn_relu_maxpool_train(x: torch.Tensor, bn) -> tuple:
+    partials = x.__dict__.pop("_dpt_bn_partials", None)
+    return _BNReLUMaxPoolPair.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                                    bn.momentum, bn.eps, partials)
+

@@ -251,3 +251,35 @@ def test_stem_bn_statistics_from_pool_backward(cuda):
     assert not nc._BNB_PARTIALS
     for a, b in zip(*grads):
         torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item() + 1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_stem_bn_relu_maxpool_fused(cuda, dtype, monkeypatch):
+    """ResNet stem pool(relu(bn(x))) as one op (BN apply folded into the pool's loads): the
+    pooled output is bitwise the unfused chain's, running statistics equal, and gradients match
+    (the backward is the same pool-gather statistics + BN apply either way)."""
+    import copy
+
+    from distributed_pytorch_training_amd.models import layers
+
+    x0 = _mk((4, 64, 30, 30), dtype, cuda, 61)
+    g1 = _mk((4, 64, 15, 15), dtype, cuda, 62)
+    g2 = _mk((4, 64, 15, 15), dtype, cuda, 63)
+    bn0 = layers.FusedBatchNorm2d(64).to(cuda)
+    with torch.no_grad():
+        bn0.weight.uniform_(-1.0, 1.5)  # negative scales too: the pool must not assume monotone
+        bn0.bias.uniform_(-0.3, 0.3)
+    pool = layers.FusedMaxPool2d(3, 2, 1)
+    pool.dpt_pair = True
+    res = []
+    for fuse in (True, False):
+        monkeypatch.setattr(layers, "STEM_FUSE", fuse)
+        bn = copy.deepcopy(bn0)
+        x = x0.detach().clone().requires_grad_(True)
+        y1, y2 = layers.bn_relu_maxpool(bn, pool, x)
+        torch.autograd.backward([y1, y2], [g1, g2])
+        res.append((y1.detach(), x.grad.float(), bn.weight.grad, bn.bias.grad, bn.running_mean, bn.running_var))
+    (a, *ra), (b, *rb) = res
+    assert torch.equal(a, b)
+    for u, v in zip(ra, rb):
+        torch.testing.assert_close(u, v, rtol=2e-2, atol=2e-2 * v.abs().max().item() + 1e-6)
