@@ -57,8 +57,9 @@ def parse(argv=None):
     ap.add_argument("--no-native-conv", action="store_true", help="A/B: MIOpen convolutions")
     ap.add_argument("--no-weight-shadow", action="store_true",
                     help="A/B: autocast casts fp32 weights every forward (no optimizer-kept bf16 copy)")
-    ap.add_argument("--profile-steps", type=int, default=0,
-                    help="extra steps after the timed window with the hipEvent sync timeline")
+    ap.add_argument("--profile-steps", type=int, default=6,
+                    help="extra steps AFTER the timed window with the hipEvent sync timeline "
+                         "(BASELINE's second metric: %% of step in all-reduce); 0 = off")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -137,8 +138,10 @@ def main(argv=None) -> int:
     value = a.batch_size * ws * a.steps / dt
 
     prof = {}
-    if a.profile_steps > 0 and a.impl == "native":
-        trainer.timeline.enabled = device.type == "cuda"
+    if a.profile_steps > 0 and a.impl == "native" and device.type == "cuda" and trainer.graphed is None:
+        # after the timed window: per-bucket RCCL events on (every rank runs the same steps)
+        trainer.timeline.enabled = True
+        trainer.ddp.set_profile(True)
         run(a.profile_steps)
         fence()
         prof = trainer.timeline.summary(skip=1)
@@ -157,9 +160,10 @@ def main(argv=None) -> int:
                    "seq_len": None, "image_size": args.image_size, "parallelism": f"dp{ws}",
                    "impl": a.impl, "optimizer": a.optimizer, "channels_last": bool(args.channels_last),
                    "bucket_cap_mb": a.bucket_cap_mb, "grad_dtype": a.grad_dtype,
-                   "fused_bn": bool(args.fused_bn and a.impl == "native" and args.channels_last),
+                   "fused_bn": bool(args.fused_bn and a.impl == "native" and args.channels_last
+                                     and device.type == "cuda"),
                    "native_conv": bool(args.native_conv and args.fused_bn and a.impl == "native"
-                                       and args.channels_last and args.amp and args.amp_dtype == "bf16"),
+                                       and args.channels_last and args.amp and device.type == "cuda"),
                    "miopen": "find" if a.find else "immediate(find-db)",
                    "gemm_db": bool(gemm_db),
                    "weight_shadow": bool(trainer.ddp is not None and trainer.ddp.shadow_flat is not None),
@@ -168,8 +172,11 @@ def main(argv=None) -> int:
         "baseline": {"stock_torch_1gpu_img_s": base, "source": "BASELINE.md (MI355X, --impl torch)"},
         "warmup_seconds": round(warm_s, 1),
     }
+    # BASELINE's second headline number; one GPU has no all-reduce (the reducer runs local)
+    rec["pct_step_allreduce"] = (round(prof["pct_step_allreduce"], 2) if "pct_step_allreduce" in prof
+                                 else (0.0 if ws == 1 else None))
     if prof:
-        rec["sync_profile"] = {k: round(v, 4) if isinstance(v, float) else v for k, v in prof.items()}
+        rec["sync_profile"] ={k: round(v, 4) if isinstance(v, float) else v for k, v in prof.items()}
     if rank == 0:
         line = json.dumps(rec)
         print(line, flush=True)

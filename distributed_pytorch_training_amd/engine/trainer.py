@@ -191,7 +191,7 @@ class Trainer:
                                 grads_checked=self.ddp.grads_checked, shadow=self.ddp.shadow_flat)
         tl.mark("opt")
         ops.accumulate_metrics(outputs, targets, loss, self.metrics)
-        tl.end_step(self.ddp.comm_profile() if tl.enabled else None)
+        tl.end_step(self.ddp.comm_profile if tl.enabled else None)
         self.global_step += 1
         return outputs, loss
 

@@ -239,6 +239,16 @@ class NativeDDP(nn.Module):
     def bucket_sizes_mib(self) -> List[float]:
         return self.plan.sizes_mib(self.arena.param_flat.element_size()) if self.plan else []
 
+    def set_profile(self, enabled: bool) -> None:
+        """Turn the reducer's per-bucket hipEvent timing on/off after construction (the events
+        are created with the reducer, so it is rebuilt over the same arena - layout, buckets and
+        communicator unchanged).  Call between steps, never inside a captured hipGraph."""
+        if bool(enabled) == bool(self.profile):
+            return
+        self.profile = bool(enabled)
+        if self.reducer is not None:
+            self._build_reducer()
+
     def comm_profile(self):
         if self.reducer is None or self.comm is None:
             return None

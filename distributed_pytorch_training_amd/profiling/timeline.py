@@ -46,12 +46,22 @@ class StepTimeline:
         """Drop the marks of a step that did not run the optimizer (accumulation micro-batch)."""
         self._marks = {}
 
-    def end_step(self, comm_profile: Optional[dict]) -> None:
+    def end_step(self, comm_profile=None) -> None:
+        """``comm_profile``: None, a dict, or a zero-argument callable returning the reducer's
+        per-bucket times.  The reducer re-records its events every backward, so its times must
+        be read before the next step: with a callable, this step's "opt" event is waited on and
+        the times are read now (one host sync per profiled step); the compute-stream marks
+        alone stay deferred by one step."""
         if not self.enabled:
             return
         self._resolve_pending()
-        self._pending = (dict(self._marks), comm_profile)
+        marks = dict(self._marks)
         self._marks = {}
+        if callable(comm_profile):
+            if "opt" in marks:
+                marks["opt"].synchronize()
+            comm_profile = comm_profile()
+        self._pending = (marks, comm_profile)
 
     def _resolve_pending(self) -> None:
         if self._pending is None:

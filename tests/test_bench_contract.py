@@ -1,0 +1,50 @@
+"""bench.py driver contract on the CPU: one JSON line from rank 0 with the required keys,
+whole-job aggregate value, and the same line shape under torch.distributed.run (gloo, 2 ranks)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TINY = ["--model", "resnet18", "--batch-size", "4", "--image-size", "32", "--num-classes", "10",
+        "--steps", "2", "--warmup", "1"]
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config", "pct_step_allreduce"}
+
+
+def _json_lines(out: str):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def _check(rec, n):
+    assert KEYS <= set(rec), KEYS - set(rec)
+    assert rec["n_gpus"] == n and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["higher_is_better"] is True and rec["scaling"] == "weak" and rec["data"] == "synthetic"
+    cfg = rec["config"]
+    assert cfg["global_batch"] == 4 * n and cfg["parallelism"] == f"dp{n}" and "seq_len" in cfg
+    # value is the whole-job images/s: global batch / step time
+    assert rec["value"] == pytest.approx(4 * n * 1e3 / rec["ms_per_step"], rel=0.02)
+
+
+def test_bench_single_process_cpu(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *TINY], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    _check(lines[0], 1)
+    assert lines[0]["pct_step_allreduce"] == 0.0
+
+
+def test_bench_torchrun_gloo_two_ranks(tmp_path):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29531", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", *TINY]
+    r = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    _check(lines[0], 2)

@@ -148,6 +148,48 @@ def test_reducer_rccl_path_single_rank(cuda, wire, monkeypatch):
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
+def test_sync_profile_reads_rccl_bucket_times(cuda):
+    """bench.py's "% of step in all-reduce": per-bucket RCCL events switched on after
+    construction (``NativeDDP.set_profile``) are read once complete (``StepTimeline.end_step``
+    with a callable), giving a positive busy time and a percentage below 100."""
+    import subprocess
+    import sys
+    import textwrap
+
+    code = textwrap.dedent("""
+        import torch
+        from distributed_pytorch_training_amd.parallel.comm import make_comm
+        from distributed_pytorch_training_amd.parallel.ddp import NativeDDP
+        from distributed_pytorch_training_amd.profiling.timeline import StepTimeline
+        dev = torch.device("cuda:0")
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(256, 1024), torch.nn.ReLU(), torch.nn.Linear(1024, 1024),
+                                    torch.nn.ReLU(), torch.nn.Linear(1024, 10)).to(dev)
+        ddp = NativeDDP(model, rank=0, world_size=1, device=dev, bucket_cap_mb=1.0, first_bucket_mb=0.25,
+                        comm=make_comm(dev, 0, 1))
+        assert ddp.comm_profile()["bucket_ms"] == []
+        ddp.set_profile(True)
+        tl = StepTimeline(dev, enabled=True)
+        x = torch.randn(64, 256, device=dev)
+        for _ in range(5):
+            tl.mark("start")
+            out = ddp(x)
+            tl.mark("fwd")
+            out.float().pow(2).mean().backward()
+            tl.mark("bwd")
+            tl.mark("opt")
+            tl.end_step(ddp.comm_profile)
+        s = tl.summary(skip=1)
+        assert s["steps_profiled"] == 4, s
+        assert s["allreduce_busy_ms"] > 0 and 0 < s["pct_step_allreduce"] < 100, s
+        assert "exposed_comm_ms" in s and "comm_span_ms" in s, s
+        print("ok", s)
+    """)
+    env = dict(__import__("os").environ, DPT_FORCE_COLLECTIVES="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
 def test_cuda_graph_step_matches_eager(cuda):
     """hipGraph-replayed native steps produce the same parameters as eager steps."""
     import copy
