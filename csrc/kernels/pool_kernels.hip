@@ -14,10 +14,24 @@
 // first window element instead of the max for the fp32 instantiation on gfx950 (bf16 was
 // right); the analytic clipped window seeded with -inf below is what tests/test_bn_gpu.py
 // verifies for every dtype.
+#include <cstdlib>
 #include <stdexcept>
 
 #include "common.h"
 #include "kernels.h"
+
+typedef float pf32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 pbf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 pf16x2 __attribute__((ext_vector_type(2)));
+
+// DPT_POOL_BLOCK2=0: the per-output 3x3/s2 forward kernel (A/B of the 2x2-block one)
+static bool pool_block2() {
+  static const bool on = [] {
+    const char* e = std::getenv("DPT_POOL_BLOCK2");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
 
 namespace dpt {
 
@@ -91,7 +105,7 @@ __global__ __launch_bounds__(kBlock) void maxpool_fwd_kernel(const void* __restr
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         // strictly greater (first max wins), and a NaN wins unless one is already held
-        const bool take = (v[k] > best[k]) || (v[k] != v[k] && best[k] == best[k]);
+        const bool take = !(v[k] <= best[k]) && (best[k] == best[k]);
         best[k] = take ? v[k] : best[k];
         arg[k] = take ? pos : arg[k];
       }
@@ -214,7 +228,7 @@ __global__ __launch_bounds__(kBlock) void maxpool3_fwd_kernel(const void* __rest
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float vv = v[ky * 3 + kx][k];
-        const bool take = in && ((vv > best[k]) || (vv != vv && best[k] == best[k]));
+        const bool take = in && !(vv <= best[k]) && (best[k] == best[k]);  // > or NaN-over-number
         best[k] = take ? vv : best[k];
         arg[k] = take ? ky * 3 + kx : arg[k];
       }
@@ -226,6 +240,108 @@ __global__ __launch_bounds__(kBlock) void maxpool3_fwd_kernel(const void* __rest
   packed.x = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) | ((uint32_t)arg[3] << 24);
   packed.y = (uint32_t)arg[4] | ((uint32_t)arg[5] << 8) | ((uint32_t)arg[6] << 16) | ((uint32_t)arg[7] << 24);
   *reinterpret_cast<uint2*>(idx + o) = packed;
+}
+
+// 3x3 / stride 2 / pad 1 forward (the ResNet stem): one thread per 2x2 OUTPUT block x 8
+// channels.  The four windows of output rows {2a, 2a+1} x cols {2b, 2b+1} cover input rows
+// 4a-1..4a+3 and cols 4b-1..4b+3: 25 loads (and, with AFF, 25 BN+ReLU transforms) serve four
+// outputs instead of 36.  Rows are streamed top to bottom and each tap updates the windows
+// that contain it in window-local (ky, kx) order, so max / argmax / tie / NaN semantics are
+// the per-output kernel's exactly.  AFF rounding uses the hardware round-to-nearest-even
+// converts (v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32) - the same values as f32_to_bf16.
+template <int DT, bool AFF>
+__global__ __launch_bounds__(kBlock) void maxpool3s2_fwd_kernel(const void* __restrict__ x, void* __restrict__ y,
+                                                                uint8_t* __restrict__ idx, int H, int W, int C, int Ho,
+                                                                int Wo, uint32_t total,
+                                                                const float* __restrict__ coef) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= total) return;
+  const uint32_t cg8 = (uint32_t)C >> 3;
+  const int cg = (int)(t % cg8);
+  uint32_t pix = t / cg8;
+  const uint32_t Wo2 = ((uint32_t)Wo + 1) >> 1, Ho2 = ((uint32_t)Ho + 1) >> 1;
+  const int bx = (int)(pix % Wo2);
+  pix /= Wo2;
+  const int by = (int)(pix % Ho2);
+  const int64_t b = (int64_t)(pix / Ho2);
+  const int y0 = 4 * by - 1, x0 = 4 * bx - 1;
+  float ca[8], cb[8];
+  if (AFF) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { ca[k] = coef[cg * 8 + k]; cb[k] = coef[C + cg * 8 + k]; }
+  }
+  float best[4][8];
+  int arg[4][8];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    // first in-image tap of window w (the scan's argmax seed, as in the per-output kernel)
+    const int wy = y0 + 2 * (w >> 1), wx = x0 + 2 * (w & 1);
+    const int a0 = (wy < 0 ? 1 : 0) * 3 + (wx < 0 ? 1 : 0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[w][k] = -__builtin_inff(); arg[w][k] = a0; }
+  }
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int iy = y0 + r;
+    const bool yin = iy >= 0 && iy < H;
+    const int cy = min(max(iy, 0), H - 1);
+    float v[5][8];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      const int cx = min(max(x0 + c, 0), W - 1);
+      pool_load8(DT, x, ((b * H + cy) * W + cx) * C + cg * 8, v[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      if (AFF) {
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+          pf32x2 o;
+          o[0] = __builtin_fmaf(v[c][k], ca[k], cb[k]);
+          o[1] = __builtin_fmaf(v[c][k + 1], ca[k + 1], cb[k + 1]);
+          o[0] = o[0] < 0.0f ? 0.0f : o[0];
+          o[1] = o[1] < 0.0f ? 0.0f : o[1];
+          if (DT == 1) {
+            const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(o, pbf16x2));
+            o[0] = __uint_as_float(u << 16);
+            o[1] = __uint_as_float(u & 0xffff0000u);
+          } else if (DT == 2) {
+            const pf16x2 h = __builtin_convertvector(o, pf16x2);
+            o[0] = (float)h[0];
+            o[1] = (float)h[1];
+          }
+          v[c][k] = o[0];
+          v[c][k + 1] = o[1];
+        }
+      }
+      const int ix = x0 + c;
+      const bool in = yin && ix >= 0 && ix < W;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int ky = r - 2 * (w >> 1), kx = c - 2 * (w & 1);
+        if (ky < 0 || ky > 2 || kx < 0 || kx > 2) continue;  // resolved at compile time
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          // vv > best, or vv NaN while best is not: !(vv <= best) && best == best (2 compares)
+          const float vv = v[c][k];
+          const bool take = in && !(vv <= best[w][k]) && (best[w][k] == best[w][k]);
+          best[w][k] = take ? vv : best[w][k];
+          arg[w][k] = take ? ky * 3 + kx : arg[w][k];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int oy = 2 * by + (w >> 1), ox = 2 * bx + (w & 1);
+    if (oy >= Ho || ox >= Wo) continue;
+    const int64_t o = ((b * Ho + oy) * Wo + ox) * C + cg * 8;
+    pool_store8(DT, y, o, best[w]);
+    uint2 packed;
+    packed.x = (uint32_t)arg[w][0] | ((uint32_t)arg[w][1] << 8) | ((uint32_t)arg[w][2] << 16) | ((uint32_t)arg[w][3] << 24);
+    packed.y = (uint32_t)arg[w][4] | ((uint32_t)arg[w][5] << 8) | ((uint32_t)arg[w][6] << 16) | ((uint32_t)arg[w][7] << 24);
+    *reinterpret_cast<uint2*>(idx + o) = packed;
+  }
 }
 
 // 3x3 / stride 2 / pad 1 (ResNet stem) backward: one thread per 2x2 input block (rows 2a,
@@ -397,6 +513,25 @@ void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t
   const int64_t total = B * Ho * Wo * (C / 8);
   if (total == 0) return;
   const dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
+  const int64_t total2 = B * ((Ho + 1) / 2) * ((Wo + 1) / 2) * (C / 8);
+  if (K == 3 && S == 2 && P == 1 && total2 + kBlock < (int64_t(1) << 32) && pool_block2()) {
+    const dim3 grid2((unsigned)((total2 + kBlock - 1) / kBlock)), block(kBlock);
+    const uint32_t t2 = (uint32_t)total2;
+    if (coef != nullptr) {
+      switch (dtype) {
+        case 0: hipLaunchKernelGGL((maxpool3s2_fwd_kernel<0, true>), grid2, block, 0, s, x, y, idx, H, W, C, Ho, Wo, t2, coef); break;
+        case 1: hipLaunchKernelGGL((maxpool3s2_fwd_kernel<1, true>), grid2, block, 0, s, x, y, idx, H, W, C, Ho, Wo, t2, coef); break;
+        default: hipLaunchKernelGGL((maxpool3s2_fwd_kernel<2, true>), grid2, block, 0, s, x, y, idx, H, W, C, Ho, Wo, t2, coef); break;
+      }
+    } else {
+      switch (dtype) {
+        case 0: hipLaunchKernelGGL((maxpool3s2_fwd_kernel<0, false>), grid2, block, 0, s, x, y, idx, H, W, C, Ho, Wo, t2, coef); break;
+        case 1: hipLaunchKernelGGL((maxpool3s2_fwd_kernel<1, false>), grid2, block, 0, s, x, y, idx, H, W, C, Ho, Wo, t2, coef); break;
+        default: hipLaunchKernelGGL((maxpool3s2_fwd_kernel<2, false>), grid2, block, 0, s, x, y, idx, H, W, C, Ho, Wo, t2, coef); break;
+      }
+    }
+    return;
+  }
   if (K == 3 && total + kBlock < (int64_t(1) << 32)) {
     const dim3 block(kBlock);
     if (coef != nullptr) {

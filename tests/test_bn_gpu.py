@@ -167,6 +167,7 @@ def test_pair_outputs_sum_gradients(cuda, use):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("shape,k,s,p", [((8, 64, 112, 112), 3, 2, 1), ((2, 16, 9, 7), 3, 2, 1),
+                                         ((2, 16, 10, 11), 3, 2, 1), ((3, 8, 5, 6), 3, 2, 1), ((1, 8, 1, 2), 3, 2, 1),
                                          ((2, 8, 8, 8), 2, 2, 0), ((3, 24, 10, 10), 3, 1, 1)])
 def test_maxpool_matches_torch(cuda, dtype, shape, k, s, p):
     from distributed_pytorch_training_amd.ops.pool import max_pool2d_nhwc
@@ -262,7 +263,7 @@ def test_stem_bn_relu_maxpool_fused(cuda, dtype, monkeypatch):
 
     from distributed_pytorch_training_amd.models import layers
 
-    x0 = _mk((4, 64, 30, 30), dtype, cuda, 61)
+    x0 = _mk((4, 64, 30, 29), dtype, cuda, 61)  # odd pooled extents: partial 2x2 output blocks
     g1 = _mk((4, 64, 15, 15), dtype, cuda, 62)
     g2 = _mk((4, 64, 15, 15), dtype, cuda, 63)
     bn0 = layers.FusedBatchNorm2d(64).to(cuda)
