@@ -57,11 +57,27 @@ def parse(argv=None):
     ap.add_argument("--no-native-conv", action="store_true", help="A/B: MIOpen convolutions")
     ap.add_argument("--no-weight-shadow", action="store_true",
                     help="A/B: autocast casts fp32 weights every forward (no optimizer-kept bf16 copy)")
-    ap.add_argument("--profile-steps", type=int, default=6,
-                    help="extra steps AFTER the timed window with the hipEvent sync timeline "
-                         "(BASELINE's second metric: %% of step in all-reduce); 0 = off")
+    ap.add_argument("--profile-steps", type=int, default=8,
+                    help="a SECOND timed window of this many steps, after the headline window, with "
+                         "per-bucket hipEvents on the comm stream (one event slot per step, read after "
+                         "the window: no host sync inside it) -> BASELINE's second metric, %% of step "
+                         "in all-reduce, plus exposed comm; 0 = off")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                    help="native reducer collective (host = gloo staging, debug only)")
+    ap.add_argument("--rccl-channels", type=int, default=0,
+                    help="NCCL_MIN/MAX_NCHANNELS for the framework's RCCL communicator (0 = RCCL default)")
+    ap.add_argument("--fake-pg", action="store_true",
+                    help="testing: run as rank 0 of a --gpus-rank job on torch's fake process group (CPU)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
+
+
+def _rccl_version():
+    try:
+        from distributed_pytorch_training_amd import ops
+        return ops.native().rccl_version() if ops.native_available() else None
+    except Exception:
+        return None
 
 
 def train_args(a):
@@ -71,7 +87,8 @@ def train_args(a):
             "--image-size", str(a.image_size), "--num-classes", str(a.num_classes),
             "--impl", a.impl, "--amp-dtype", a.amp_dtype, "--optimizer", a.optimizer,
             "--bucket-cap-mb", str(a.bucket_cap_mb), "--first-bucket-mb", str(a.first_bucket_mb),
-            "--grad-dtype", a.grad_dtype, "--lr", "0.1", "--momentum", "0.9", "--weight-decay", "5e-4"]
+            "--grad-dtype", a.grad_dtype, "--lr", "0.1", "--momentum", "0.9", "--weight-decay", "5e-4",
+            "--comm", a.comm, "--rccl-channels", str(a.rccl_channels)]
     if not a.no_amp:
         argv.append("--amp")
     argv.append("--no-channels-last" if a.no_channels_last else "--channels-last")
@@ -96,7 +113,14 @@ def main(argv=None) -> int:
 
     setup_miopen_env()
     args = train_args(a)
-    info = init_distributed("auto")
+    if a.fake_pg:
+        from torch.testing._internal.distributed.fake_pg import FakeStore
+
+        from distributed_pytorch_training_amd.utils.dist import DistInfo
+        dist.init_process_group("fake", store=FakeStore(), rank=0, world_size=a.gpus)
+        info = DistInfo(0, a.gpus, 0, "fake", torch.device("cpu"))
+    else:
+        info = init_distributed("auto")
     gemm_db = setup_tunableop() if (a.impl == "native" and info.device.type == "cuda") else False
     rank, ws, device = info.rank, info.world_size, info.device
     if ws != a.gpus and rank == 0:
@@ -137,14 +161,29 @@ def main(argv=None) -> int:
     ms = 1e3 * dt / max(a.steps, 1)
     value = a.batch_size * ws * a.steps / dt
 
-    prof = {}
-    if a.profile_steps > 0 and a.impl == "native" and device.type == "cuda" and trainer.graphed is None:
-        # after the timed window: per-bucket RCCL events on (every rank runs the same steps)
+    prof, prof_window = {}, None
+    collective = ws > 1 and a.impl == "native" and trainer.ddp is not None and trainer.ddp.comm is not None
+    if a.profile_steps > 0 and collective and device.type == "cuda" and trainer.graphed is None:
+        # second timed window, per-bucket comm events on: one event slot per step, everything
+        # read after the window (every rank runs the same steps)
         trainer.timeline.enabled = True
-        trainer.ddp.set_profile(True)
+        trainer.timeline.max_pending = a.profile_steps + 1
+        trainer.ddp.set_profile(True, slots=a.profile_steps + 2)
+        run(2)                      # events/slots live; not timed
+        fence()
+        trainer.timeline.records.clear()
+        trainer.timeline._pending.clear()
+        t1 = time.time()
         run(a.profile_steps)
         fence()
-        prof = trainer.timeline.summary(skip=1)
+        pdt = time.time() - t1
+        if ws > 1:
+            t = torch.tensor([pdt], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            pdt = float(t.item())
+        prof = trainer.timeline.summary(skip=0)
+        prof_window = {"steps": a.profile_steps, "ms_per_step": round(1e3 * pdt / a.profile_steps, 3),
+                       "value": round(a.batch_size * ws * a.profile_steps / pdt, 2)}
 
     base = STOCK_TORCH_1GPU.get(a.batch_size) if (args.model == "resnet50" and args.amp and
                                                   args.amp_dtype == "bf16" and args.image_size == 224) else None
@@ -172,11 +211,22 @@ def main(argv=None) -> int:
         "baseline": {"stock_torch_1gpu_img_s": base, "source": "BASELINE.md (MI355X, --impl torch)"},
         "warmup_seconds": round(warm_s, 1),
     }
-    # BASELINE's second headline number; one GPU has no all-reduce (the reducer runs local)
-    rec["pct_step_allreduce"] = (round(prof["pct_step_allreduce"], 2) if "pct_step_allreduce" in prof
-                                 else (0.0 if ws == 1 else None))
+    # BASELINE's second headline number, measured in the second (profiled) window; null when
+    # there is no collective (one GPU: the reducer runs local) or it was not measured
+    rec["pct_step_allreduce"] = round(prof["pct_step_allreduce"], 2) if "pct_step_allreduce" in prof else None
+    rec["pct_step_exposed_comm"] = (round(prof["pct_step_exposed_comm"], 2)
+                                    if "pct_step_exposed_comm" in prof else None)
+    rec["sync_profile_window"] = prof_window
     if prof:
-        rec["sync_profile"] ={k: round(v, 4) if isinstance(v, float) else v for k, v in prof.items()}
+        rec["sync_profile"] = {k: round(v, 4) if isinstance(v, float) else v for k, v in prof.items()}
+    ddp = trainer.ddp
+    rec["comm"] = {"kind": (ddp.comm.kind if ddp is not None and ddp.comm is not None else
+                            ("gloo" if ws > 1 and a.impl == "native" else
+                             ("torch-ddp" if ws > 1 else "none"))),
+                   "buckets_mib": [round(v, 3) for v in ddp.bucket_sizes_mib()] if ddp is not None else None,
+                   "bucket_cap_mb": a.bucket_cap_mb, "first_bucket_mb": a.first_bucket_mb,
+                   "grad_dtype": a.grad_dtype, "rccl_channels": a.rccl_channels or None,
+                   "rccl_version": _rccl_version()}
     if rank == 0:
         line = json.dumps(rec)
         print(line, flush=True)

@@ -6,7 +6,9 @@
 #include <torch/extension.h>
 
 #include "kernels/kernels.h"
+#include "host_comm.h"
 #include "rccl_comm.h"
+#include "watchdog.h"
 #include "reducer.h"
 
 namespace py = pybind11;
@@ -16,6 +18,17 @@ namespace {
 
 hipStream_t cur_stream(const Tensor& t) {
   return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+dpt::WireType wire_of(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return dpt::WireType::kF32;
+    case at::kBFloat16: return dpt::WireType::kBF16;
+    case at::kHalf: return dpt::WireType::kF16;
+    case at::kLong: return dpt::WireType::kI64;
+    default: TORCH_CHECK(false, "unsupported collective dtype ", t.scalar_type());
+  }
+  return dpt::WireType::kF32;
 }
 
 void check_flat_f32(const Tensor& t, const char* name, int64_t align = 4) {
@@ -1047,46 +1060,60 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad_flip", &conv_dgrad_flip, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
 
-  py::class_<dpt::RcclComm, std::shared_ptr<dpt::RcclComm>>(m, "RcclComm")
+  // Collective seam (comm.h): RcclComm (production) and HostBridgeComm (ranks sharing a GPU)
+  py::class_<dpt::Collective, std::shared_ptr<dpt::Collective>>(m, "Collective")
+      .def("all_reduce", [](dpt::Collective& c, Tensor t, bool on_current_stream) {
+             TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "all_reduce needs a contiguous GPU tensor");
+             c10::hip::HIPGuard guard(t.device().index());
+             hipStream_t s = cur_stream(t);
+             c.all_reduce(t.data_ptr(), (size_t)t.numel(), wire_of(t), on_current_stream ? s : c.stream());
+           }, py::arg("tensor"), py::arg("on_current_stream") = true)
+      .def("broadcast", [](dpt::Collective& c, Tensor t, int root) {
+             TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "broadcast needs a contiguous GPU tensor");
+             c10::hip::HIPGuard guard(t.device().index());
+             c.broadcast(t.data_ptr(), (size_t)t.numel(), wire_of(t), root, cur_stream(t));
+           }, py::arg("tensor"), py::arg("root") = 0)
+      .def("abort", &dpt::Collective::abort)
+      .def("destroy", &dpt::Collective::destroy)
+      .def("check", &dpt::Collective::check)
+      .def_property_readonly("kind", &dpt::Collective::kind)
+      .def_property_readonly("ops", &dpt::Collective::ops)
+      .def_property_readonly("sequence_hash", &dpt::Collective::sequence_hash)
+      .def_property_readonly("rank", &dpt::Collective::rank)
+      .def_property_readonly("world_size", &dpt::Collective::world_size)
+      .def_property_readonly("device", &dpt::Collective::device);
+
+  py::class_<dpt::RcclComm, dpt::Collective, std::shared_ptr<dpt::RcclComm>>(m, "RcclComm")
       .def(py::init<const std::string&, int, int, int>(), py::arg("unique_id"), py::arg("rank"),
            py::arg("world_size"), py::arg("device"))
       .def_static("new_unique_id", []() { return py::bytes(dpt::RcclComm::new_unique_id()); })
-      .def("all_reduce", [](dpt::RcclComm& c, Tensor t, bool on_current_stream) {
-             TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "all_reduce needs a contiguous GPU tensor");
-             dpt::WireType w;
-             switch (t.scalar_type()) {
-               case at::kFloat: w = dpt::WireType::kF32; break;
-               case at::kBFloat16: w = dpt::WireType::kBF16; break;
-               case at::kHalf: w = dpt::WireType::kF16; break;
-               case at::kLong: w = dpt::WireType::kI64; break;
-               default: TORCH_CHECK(false, "unsupported all_reduce dtype");
-             }
-             c10::hip::HIPGuard guard(t.device().index());
-             hipStream_t s = cur_stream(t);
-             c.all_reduce(t.data_ptr(), (size_t)t.numel(), w, on_current_stream ? s : c.stream());
-           }, py::arg("tensor"), py::arg("on_current_stream") = true)
-      .def("broadcast", [](dpt::RcclComm& c, Tensor t, int root) {
-             TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "broadcast needs a contiguous GPU tensor");
-             dpt::WireType w;
-             switch (t.scalar_type()) {
-               case at::kFloat: w = dpt::WireType::kF32; break;
-               case at::kBFloat16: w = dpt::WireType::kBF16; break;
-               case at::kHalf: w = dpt::WireType::kF16; break;
-               case at::kLong: w = dpt::WireType::kI64; break;
-               default: TORCH_CHECK(false, "unsupported broadcast dtype");
-             }
-             c10::hip::HIPGuard guard(t.device().index());
-             c.broadcast(t.data_ptr(), (size_t)t.numel(), w, root, cur_stream(t));
-           }, py::arg("tensor"), py::arg("root") = 0)
-      .def("abort", &dpt::RcclComm::abort)
-      .def("destroy", &dpt::RcclComm::destroy)
-      .def_property_readonly("rank", &dpt::RcclComm::rank)
-      .def_property_readonly("world_size", &dpt::RcclComm::world_size)
-      .def_property_readonly("device", &dpt::RcclComm::device);
+      .def("enable_watchdog", &dpt::RcclComm::enable_watchdog, py::arg("timeout_s"), py::arg("poll_s") = 0.5,
+           py::arg("exit_grace_s") = 30.0)
+      .def_property_readonly("watchdog_tripped", &dpt::RcclComm::watchdog_tripped)
+      .def_property_readonly("watchdog_outstanding", &dpt::RcclComm::watchdog_outstanding)
+      .def("async_error", &dpt::RcclComm::async_error);
+
+  py::class_<dpt::HostBridgeComm, dpt::Collective, std::shared_ptr<dpt::HostBridgeComm>>(m, "HostBridgeComm")
+      .def(py::init<py::object, py::object, int, int, int>(), py::arg("all_reduce_fn"), py::arg("broadcast_fn"),
+           py::arg("rank"), py::arg("world_size"), py::arg("device"));
+
+  // Watchdog decision logic with an explicit clock (unit-tested with a fake clock)
+  py::class_<dpt::WatchdogCore>(m, "WatchdogCore")
+      .def(py::init<double>(), py::arg("timeout_s"))
+      .def("enqueue", &dpt::WatchdogCore::enqueue, py::arg("seq"), py::arg("now"))
+      .def("poll", [](dpt::WatchdogCore& w, double now, py::function done, const std::string& aerr) {
+             std::vector<uint64_t> completed;
+             std::string trip = w.poll(now, [&](uint64_t s) { return done(s).cast<bool>(); }, aerr, &completed);
+             return py::make_tuple(trip, completed);
+           }, py::arg("now"), py::arg("done"), py::arg("async_error") = std::string())
+      .def_property_readonly("tripped", &dpt::WatchdogCore::tripped)
+      .def_property_readonly("reason", &dpt::WatchdogCore::reason)
+      .def_property_readonly("outstanding", &dpt::WatchdogCore::outstanding)
+      .def("oldest_age", &dpt::WatchdogCore::oldest_age, py::arg("now"));
 
   py::class_<dpt::Reducer, std::shared_ptr<dpt::Reducer>>(m, "Reducer")
       .def(py::init<std::vector<Tensor>, std::vector<Tensor>, Tensor, std::vector<int64_t>, std::vector<int64_t>,
-                    std::vector<int64_t>, std::shared_ptr<dpt::RcclComm>, py::object, int, Tensor, Tensor, Tensor,
+                    std::vector<int64_t>, std::shared_ptr<dpt::Collective>, py::object, int, Tensor, Tensor, Tensor,
                     double, bool, bool, bool>(),
            py::arg("params"), py::arg("grad_views"), py::arg("flat_grad"), py::arg("bucket_offsets"),
            py::arg("bucket_numels"), py::arg("param_bucket"), py::arg("comm"), py::arg("py_allreduce"),
@@ -1098,11 +1125,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_require_sync", &dpt::Reducer::set_require_sync)
       .def("set_check_inf", &dpt::Reducer::set_check_inf)
       .def("set_accumulate", &dpt::Reducer::set_accumulate)
+      .def("set_debug", &dpt::Reducer::set_debug)
       .def_property_readonly("require_sync", &dpt::Reducer::require_sync)
       .def("ready_order", &dpt::Reducer::ready_order)
       .def_property_readonly("num_buckets", &dpt::Reducer::num_buckets)
       .def_property_readonly("backward_count", &dpt::Reducer::backward_count)
-      .def("bucket_times_ms", &dpt::Reducer::bucket_times_ms)
-      .def("step_times_ms", &dpt::Reducer::step_times_ms)
+      .def("bucket_times_ms", &dpt::Reducer::bucket_times_ms, py::arg("slot") = -1)
+      .def("step_times_ms", &dpt::Reducer::step_times_ms, py::arg("slot") = -1)
+      .def("set_profile_slots", &dpt::Reducer::set_profile_slots, py::arg("n"))
+      .def_property_readonly("profile_slots", &dpt::Reducer::profile_slots)
+      .def_property_readonly("last_slot", &dpt::Reducer::last_slot)
       .def("remove_hooks", &dpt::Reducer::remove_hooks);
 }

@@ -54,33 +54,60 @@ RcclComm::RcclComm(const std::string& unique_id, int rank, int world_size, int d
 
 RcclComm::~RcclComm() { destroy(); }
 
+void RcclComm::enable_watchdog(double timeout_s, double poll_s, double exit_grace_s) {
+  if (watchdog_) return;
+  watchdog_ = std::make_unique<StreamWatchdog>(
+      "rccl rank " + std::to_string(rank_), timeout_s, poll_s, exit_grace_s, [this] { this->abort(); },
+      [this] { return this->async_error(); });
+}
+
+std::string RcclComm::async_error() const {
+  if (comm_ == nullptr || aborted_.load()) return "";
+  ncclResult_t r = ncclSuccess;
+  if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return "";
+  if (r == ncclSuccess || r == ncclInProgress) return "";
+  return ncclGetErrorString(r);
+}
+
+void RcclComm::check() const {
+  if (watchdog_ && watchdog_->tripped())
+    throw std::runtime_error("RcclComm (rank " + std::to_string(rank_) + "): " + watchdog_->reason());
+  if (aborted_.load()) throw std::runtime_error("RcclComm: communicator was aborted");
+}
+
 void RcclComm::destroy() {
-  if (comm_ != nullptr && !aborted_) {
+  if (watchdog_) watchdog_->stop();
+  if (comm_ != nullptr && !aborted_.load()) {
     hipStreamSynchronize(stream_);
     ncclCommDestroy(comm_);
   }
   comm_ = nullptr;
+  watchdog_.reset();
   if (stream_ != nullptr) hipStreamDestroy(stream_);
   stream_ = nullptr;
 }
 
 void RcclComm::all_reduce(void* ptr, size_t count, WireType t, hipStream_t stream) {
-  if (aborted_ || comm_ == nullptr) throw std::runtime_error("RcclComm: communicator was aborted or destroyed");
+  if (aborted_.load() || comm_ == nullptr) throw std::runtime_error("RcclComm: communicator was aborted or destroyed");
   if (count == 0) return;
-  DPT_RCCL_CHECK(ncclAllReduce(ptr, ptr, count, to_nccl(t), ncclSum, comm_, stream ? stream : stream_));
+  hipStream_t s = stream ? stream : stream_;
+  note_op(0, count, t, 0);
+  DPT_RCCL_CHECK(ncclAllReduce(ptr, ptr, count, to_nccl(t), ncclSum, comm_, s));
+  if (watchdog_) watchdog_->track(s);
 }
 
 void RcclComm::broadcast(void* ptr, size_t count, WireType t, int root, hipStream_t stream) {
-  if (aborted_ || comm_ == nullptr) throw std::runtime_error("RcclComm: communicator was aborted or destroyed");
+  if (aborted_.load() || comm_ == nullptr) throw std::runtime_error("RcclComm: communicator was aborted or destroyed");
   if (count == 0) return;
-  DPT_RCCL_CHECK(ncclBroadcast(ptr, ptr, count, to_nccl(t), root, comm_, stream ? stream : stream_));
+  hipStream_t s = stream ? stream : stream_;
+  note_op(1, count, t, root);
+  DPT_RCCL_CHECK(ncclBroadcast(ptr, ptr, count, to_nccl(t), root, comm_, s));
+  if (watchdog_) watchdog_->track(s);
 }
 
 void RcclComm::abort() {
-  if (comm_ != nullptr && !aborted_) {
-    ncclCommAbort(comm_);
-    aborted_ = true;
-  }
+  bool expected = false;
+  if (comm_ != nullptr && aborted_.compare_exchange_strong(expected, true)) ncclCommAbort(comm_);
 }
 
 const char* rccl_version_string() {

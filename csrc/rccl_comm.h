@@ -7,7 +7,8 @@
 //     TCPStore-backed process group (control plane only), every rank ncclCommInitRank;
 //   * a dedicated high-priority HIP stream carries every bucket all-reduce so RCCL's
 //     kernels run beside the backward kernels on the compute stream, ordered by hipEvents;
-//   * buffers are persistent flat arenas (no caching-allocator recordStream bookkeeping).
+//   * buffers are persistent flat arenas (no caching-allocator recordStream bookkeeping);
+//   * a StreamWatchdog (watchdog.h) enforces the timeout and polls ncclCommGetAsyncError.
 // Links against torch's bundled librccl.so so one RCCL copy lives in the process (SURVEY.md
 // §7.5 hard part 1).
 #pragma once
@@ -15,40 +16,49 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <memory>
 #include <string>
+
+#include "comm.h"
+#include "watchdog.h"
 
 namespace dpt {
 
-enum class WireType { kF32 = 0, kBF16 = 1, kF16 = 2, kI64 = 3 };
-
-class RcclComm {
+class RcclComm : public Collective {
  public:
   RcclComm(const std::string& unique_id, int rank, int world_size, int device);
-  ~RcclComm();
+  ~RcclComm() override;
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
 
   static std::string new_unique_id();
 
-  // In-place SUM all-reduce of `count` elements at `ptr`, enqueued on `stream`.
-  void all_reduce(void* ptr, size_t count, WireType t, hipStream_t stream);
-  void broadcast(void* ptr, size_t count, WireType t, int root, hipStream_t stream);
+  void all_reduce(void* ptr, size_t count, WireType t, hipStream_t stream) override;
+  void broadcast(void* ptr, size_t count, WireType t, int root, hipStream_t stream) override;
 
-  hipStream_t stream() const { return stream_; }
-  int rank() const { return rank_; }
-  int world_size() const { return world_size_; }
-  int device() const { return device_; }
-  // Abort outstanding operations (failure path); the object is unusable after.
-  void abort();
-  // Orderly teardown (idempotent): destroy the communicator and its stream now, not at
-  // interpreter exit when the HIP runtime may already be gone.
-  void destroy();
+  hipStream_t stream() const override { return stream_; }
+  int rank() const override { return rank_; }
+  int world_size() const override { return world_size_; }
+  int device() const override { return device_; }
+  void abort() override;
+  void destroy() override;
+  void check() const override;
+  std::string kind() const override { return "rccl"; }
+
+  // Start the watchdog: a collective older than `timeout_s` (or an RCCL async error) aborts
+  // the communicator; `exit_grace_s` < 0 disables the last-resort process exit.
+  void enable_watchdog(double timeout_s, double poll_s, double exit_grace_s);
+  bool watchdog_tripped() const { return watchdog_ && watchdog_->tripped(); }
+  size_t watchdog_outstanding() const { return watchdog_ ? watchdog_->outstanding() : 0; }
+  std::string async_error() const;
 
  private:
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   int rank_, world_size_, device_;
-  bool aborted_ = false;
+  std::atomic<bool> aborted_{false};
+  std::unique_ptr<StreamWatchdog> watchdog_;
 };
 
 const char* rccl_version_string();

@@ -25,7 +25,7 @@ namespace dpt {
 Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_views,
                  at::Tensor flat_grad, std::vector<int64_t> bucket_offsets,
                  std::vector<int64_t> bucket_numels, std::vector<int64_t> param_bucket,
-                 std::shared_ptr<RcclComm> comm, py::object py_allreduce, int wire,
+                 std::shared_ptr<Collective> comm, py::object py_allreduce, int wire,
                  at::Tensor wire_buf, at::Tensor found_inf, at::Tensor scale, double host_factor,
                  bool check_inf, bool profile, bool steal_grads)
     : params_(std::move(params)),
@@ -75,18 +75,10 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
     throw std::invalid_argument("Reducer: steal mode needs a float32 arena");
 
   if (gpu_) {
-    const unsigned flags = profile_ ? hipEventDefault : hipEventDisableTiming;
     ev_ready_.resize(B);
     for (auto& e : ev_ready_) DPT_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (profile_) {
-      ev_start_.resize(B);
-      ev_end_.resize(B);
-      for (auto& e : ev_start_) DPT_HIP_OK(hipEventCreateWithFlags(&e, flags));
-      for (auto& e : ev_end_) DPT_HIP_OK(hipEventCreateWithFlags(&e, flags));
-    }
-    DPT_HIP_OK(hipEventCreateWithFlags(&ev_bwd_end_, flags));
-    DPT_HIP_OK(hipEventCreateWithFlags(&ev_done_, flags));
-    DPT_HIP_OK(hipEventCreateWithFlags(&ev_first_, flags));
+    DPT_HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    if (profile_) create_profile_events();
   }
 
   // One post-hook per parameter on its AccumulateGrad node: fires after the gradient has
@@ -112,15 +104,45 @@ void Reducer::remove_hooks() {
   hook_keys_.clear();
 }
 
+void Reducer::create_profile_events() {
+  const size_t B = bucket_offsets_.size(), S = (size_t)slots_;
+  auto make = [](std::vector<hipEvent_t>& v, size_t n) {
+    v.resize(n);
+    for (auto& e : v) DPT_HIP_OK(hipEventCreateWithFlags(&e, hipEventDefault));
+  };
+  make(ev_start_, S * B);
+  make(ev_end_, S * B);
+  make(ev_bwd_end_, S);
+  make(ev_done_, S);
+  make(ev_first_, S);
+}
+
+void Reducer::destroy_profile_events() {
+  for (auto* v : {&ev_start_, &ev_end_, &ev_bwd_end_, &ev_done_, &ev_first_}) {
+    for (auto e : *v) hipEventDestroy(e);
+    v->clear();
+  }
+}
+
+void Reducer::set_profile_slots(int64_t n) {
+  if (n < 1) throw std::invalid_argument("Reducer: profile_slots must be >= 1");
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!gpu_ || !profile_) {
+    slots_ = n;
+    return;
+  }
+  DPT_HIP_OK(hipDeviceSynchronize());  // no event of the old set may still be pending
+  destroy_profile_events();
+  slots_ = n;
+  create_profile_events();
+}
+
 Reducer::~Reducer() {
   remove_hooks();
   if (gpu_) {
     for (auto e : ev_ready_) hipEventDestroy(e);
-    for (auto e : ev_start_) hipEventDestroy(e);
-    for (auto e : ev_end_) hipEventDestroy(e);
-    if (ev_bwd_end_) hipEventDestroy(ev_bwd_end_);
-    if (ev_done_) hipEventDestroy(ev_done_);
-    if (ev_first_) hipEventDestroy(ev_first_);
+    if (ev_join_) hipEventDestroy(ev_join_);
+    destroy_profile_events();
   }
   if (!py_allreduce_.is_none()) {
     py::gil_scoped_acquire g;
@@ -135,6 +157,7 @@ void Reducer::prepare_for_backward() {
   std::fill(marked_.begin(), marked_.end(), 0);
   next_launch_ = 0;
   callback_queued_ = false;
+  slot_ = backward_count_ % slots_;
   if (record_order_) ready_order_.clear();
   if (gpu_) caller_stream_ = c10::hip::getCurrentHIPStream(flat_grad_.device().index()).stream();
   if (steal_) {
@@ -156,12 +179,18 @@ void Reducer::prepare_for_backward() {
 void Reducer::mark_ready(int64_t index) {
   if (!require_sync_) return;
   std::lock_guard<std::mutex> lk(mu_);
-  if (marked_[index]) return;  // second accumulation in one backward: already counted
+  if (marked_[index]) {  // second accumulation in one backward: already counted
+    if (debug_)
+      throw std::runtime_error("Reducer(debug): parameter " + std::to_string(index) +
+                               " marked ready twice in one backward (reentrant backward or a "
+                               "second backward without a forward?)");
+    return;
+  }
   marked_[index] = 1;
   if (record_order_) ready_order_.push_back(index);
   if (!callback_queued_) {
     callback_queued_ = true;
-    if (gpu_ && profile_) DPT_HIP_OK(hipEventRecord(ev_first_, caller_stream_));
+    if (gpu_ && profile_) DPT_HIP_OK(hipEventRecord(ev_first_[slot_], caller_stream_));
     torch::autograd::Engine::get_default_engine().queue_callback([this] { this->finalize(); });
   }
   if (steal_) stolen_[index] = params_[index].grad();
@@ -219,6 +248,8 @@ void Reducer::gather_bucket(int64_t b, hipStream_t s) {
 }
 
 void Reducer::launch_bucket(int64_t b) {
+  if (debug_ && launched_[b] == 2)
+    throw std::runtime_error("Reducer(debug): bucket " + std::to_string(b) + " launched twice in one backward");
   const int64_t off = bucket_offsets_[b], n = bucket_numels_[b];
   if (!gpu_) {
     py::gil_scoped_acquire g;
@@ -234,7 +265,8 @@ void Reducer::launch_bucket(int64_t b) {
   }
   hipStream_t cs = comm_->stream();
   DPT_HIP_OK(hipStreamWaitEvent(cs, ev_ready_[b], 0));
-  if (profile_) DPT_HIP_OK(hipEventRecord(ev_start_[b], cs));
+  const size_t pe = (size_t)slot_ * bucket_offsets_.size() + (size_t)b;
+  if (profile_) DPT_HIP_OK(hipEventRecord(ev_start_[pe], cs));
   float* g = flat_grad_.data_ptr<float>() + off;
   const float* scale = (scale_.defined() && scale_.numel() > 0) ? scale_.data_ptr<float>() : nullptr;
   float* finf = check_inf_ ? found_inf_.data_ptr<float>() : nullptr;
@@ -257,7 +289,7 @@ void Reducer::launch_bucket(int64_t b) {
   } else if (finf) {
     launch_grad_check(g, n, scale, host_factor_, finf, cs);
   }
-  if (profile_) DPT_HIP_OK(hipEventRecord(ev_end_[b], cs));
+  if (profile_) DPT_HIP_OK(hipEventRecord(ev_end_[pe], cs));
 }
 
 void Reducer::finalize() {
@@ -272,7 +304,7 @@ void Reducer::finalize() {
         DPT_HIP_OK(hipEventRecord(ev_ready_[b], producer));
       }
     }
-    if (profile_) DPT_HIP_OK(hipEventRecord(ev_bwd_end_, caller_stream_));
+    if (profile_) DPT_HIP_OK(hipEventRecord(ev_bwd_end_[slot_], caller_stream_));
   }
   for (size_t b = 0; b < launched_.size(); ++b) {
     if (launched_[b] != 2) {
@@ -282,10 +314,11 @@ void Reducer::finalize() {
   }
   next_launch_ = (int64_t)launched_.size();
   if (gpu_ && comm_) {
-    DPT_HIP_OK(hipEventRecord(ev_done_, comm_->stream()));
-    DPT_HIP_OK(hipStreamWaitEvent(caller_stream_, ev_done_, 0));
+    if (profile_) DPT_HIP_OK(hipEventRecord(ev_done_[slot_], comm_->stream()));
+    DPT_HIP_OK(hipEventRecord(ev_join_, comm_->stream()));
+    DPT_HIP_OK(hipStreamWaitEvent(caller_stream_, ev_join_, 0));
   } else if (gpu_ && profile_) {
-    DPT_HIP_OK(hipEventRecord(ev_done_, caller_stream_));
+    DPT_HIP_OK(hipEventRecord(ev_done_[slot_], caller_stream_));
   }
   if (steal_) {
     // Hand the arena views back as .grad and drop the stolen tensors (their memory returns to
@@ -302,26 +335,31 @@ void Reducer::finalize() {
   ++backward_count_;
 }
 
-std::vector<double> Reducer::bucket_times_ms() {
+std::vector<double> Reducer::bucket_times_ms(int64_t slot) {
   std::vector<double> out;
-  if (!gpu_ || !profile_ || !comm_) return out;
-  for (size_t b = 0; b < ev_start_.size(); ++b) {
+  if (!gpu_ || !profile_ || !comm_ || backward_count_ == 0) return out;
+  if (slot < 0) slot = last_slot();
+  const size_t B = bucket_offsets_.size();
+  for (size_t b = 0; b < B; ++b) {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, ev_start_[b], ev_end_[b]) != hipSuccess) ms = -1.f;
+    const size_t pe = (size_t)(slot % slots_) * B + b;
+    if (hipEventElapsedTime(&ms, ev_start_[pe], ev_end_[pe]) != hipSuccess) ms = -1.f;
     out.push_back(ms);
   }
   return out;
 }
 
-std::vector<double> Reducer::step_times_ms() {
+std::vector<double> Reducer::step_times_ms(int64_t slot) {
   // {first-grad-ready -> backward end, backward end -> comm done (exposed), first bucket
   //  start -> comm done (comm span)}
   std::vector<double> out;
-  if (!gpu_ || !profile_ || ev_start_.empty() || !comm_) return out;
+  if (!gpu_ || !profile_ || ev_start_.empty() || !comm_ || backward_count_ == 0) return out;
+  if (slot < 0) slot = last_slot();
+  const size_t s = (size_t)(slot % slots_), B = bucket_offsets_.size();
   float a = 0.f, b = 0.f, c = 0.f;
-  hipEventElapsedTime(&a, ev_first_, ev_bwd_end_);
-  hipEventElapsedTime(&b, ev_bwd_end_, ev_done_);
-  hipEventElapsedTime(&c, ev_start_[0], ev_done_);
+  hipEventElapsedTime(&a, ev_first_[s], ev_bwd_end_[s]);
+  hipEventElapsedTime(&b, ev_bwd_end_[s], ev_done_[s]);
+  hipEventElapsedTime(&c, ev_start_[s * B], ev_done_[s]);
   out = {a, b, c};
   return out;
 }

@@ -33,7 +33,7 @@
 #include <mutex>
 #include <vector>
 
-#include "rccl_comm.h"
+#include "comm.h"
 
 namespace dpt {
 
@@ -41,7 +41,7 @@ class Reducer {
  public:
   Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_views, at::Tensor flat_grad,
           std::vector<int64_t> bucket_offsets, std::vector<int64_t> bucket_numels,
-          std::vector<int64_t> param_bucket, std::shared_ptr<RcclComm> comm,
+          std::vector<int64_t> param_bucket, std::shared_ptr<Collective> comm,
           pybind11::object py_allreduce, int wire, at::Tensor wire_buf, at::Tensor found_inf,
           at::Tensor scale, double host_factor, bool check_inf, bool profile, bool steal_grads);
   ~Reducer();
@@ -54,12 +54,23 @@ class Reducer {
   void set_check_inf(bool v) { check_inf_ = v; }
   // Next synced backward adds into the arena (it holds no_sync micro-batch gradients).
   void set_accumulate(bool v) { accumulate_ = v; }
+  // Debug mode: a parameter marked ready twice in one backward, or a bucket
+  // launched twice, raises instead of being tolerated.
+  void set_debug(bool v) { debug_ = v; }
+  bool debug() const { return debug_; }
   std::vector<int64_t> ready_order() const { return ready_order_; }
   int64_t num_buckets() const { return (int64_t)bucket_offsets_.size(); }
   int64_t backward_count() const { return backward_count_; }
-  // Profiling: per bucket {launch->done ms}, plus {bwd_end->comm_done ms (exposed), comm span}.
-  std::vector<double> bucket_times_ms();
-  std::vector<double> step_times_ms();
+  // Profiling (profile=true): every backward records its events into slot
+  // (backward_count % profile_slots), so a window of up to `profile_slots` steps can run without
+  // host synchronisation and be read afterwards.  slot < 0: the last finished backward.
+  // Per bucket {comm start->done ms}, plus {first grad ready->bwd end, bwd_end->comm_done ms
+  // (exposed), first bucket start->comm done (comm span)}.
+  void set_profile_slots(int64_t n);
+  int64_t profile_slots() const { return slots_; }
+  int64_t last_slot() const { return backward_count_ > 0 ? (backward_count_ - 1) % slots_ : -1; }
+  std::vector<double> bucket_times_ms(int64_t slot = -1);
+  std::vector<double> step_times_ms(int64_t slot = -1);
   void remove_hooks();
 
  private:
@@ -75,11 +86,11 @@ class Reducer {
   std::vector<int64_t> ready_order_;
   std::vector<std::shared_ptr<torch::autograd::Node>> accumulators_;
   std::vector<uintptr_t> hook_keys_;
-  std::shared_ptr<RcclComm> comm_;
+  std::shared_ptr<Collective> comm_;
   pybind11::object py_allreduce_;
   int wire_;
   float host_factor_;
-  bool check_inf_, profile_, gpu_, steal_ = false, accumulate_ = false;
+  bool check_inf_, profile_, gpu_, steal_ = false, accumulate_ = false, debug_ = false;
   std::vector<at::Tensor> stolen_;        // gradients autograd handed over (steal mode)
   std::vector<std::vector<int64_t>> members_;
   bool require_sync_ = true;
@@ -88,8 +99,13 @@ class Reducer {
   int64_t next_launch_ = 0;  // buckets launch strictly in index order (RCCL needs one global order)
   int64_t backward_count_ = 0;
   hipStream_t caller_stream_ = nullptr;
-  std::vector<hipEvent_t> ev_ready_, ev_start_, ev_end_;
-  hipEvent_t ev_bwd_end_ = nullptr, ev_done_ = nullptr, ev_first_ = nullptr;
+  void create_profile_events();
+  void destroy_profile_events();
+  std::vector<hipEvent_t> ev_ready_;
+  // profiling events: [slot * B + b] per bucket, [slot] per backward
+  std::vector<hipEvent_t> ev_start_, ev_end_, ev_bwd_end_, ev_done_, ev_first_;
+  hipEvent_t ev_join_ = nullptr;   // comm-stream completion the caller's stream waits on
+  int64_t slots_ = 1, slot_ = 0;
   std::mutex mu_;
 };
 

@@ -91,7 +91,8 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--max-steps", default=0, type=int,
                    help="stop each epoch after this many steps (0 = full epoch)")
     g.add_argument("--warmup-steps", default=0, type=int,
-                   help="untimed steps excluded from the throughput window at the first epoch")
+                   help="the first N steps of the first epoch run but are excluded from the throughput "
+                        "windows (step lines and metrics_perf_rank0.csv)")
     g.add_argument("--profile-sync", action="store_true",
                    help="hipEvent timeline: per-step forward/backward/all-reduce/optimizer times")
     g.add_argument("--profile-out", default=None, type=str,
@@ -106,7 +107,25 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--dist-timeout", default=1800, type=int,
                    help="process-group timeout in seconds")
     g.add_argument("--check-consistency", default=0, type=int,
-                   help="debug: every N steps verify parameters are identical across ranks")
+                   help="debug: every N optimizer steps (and at every epoch end) verify that parameters "
+                        "are identical across ranks")
+    g.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                   help="device collective of the native reducer: rccl (RCCL over xGMI) or host (gloo "
+                        "through pinned host staging - lets several ranks share one GPU; debug only)")
+    g.add_argument("--rccl-channels", default=0, type=int,
+                   help="export NCCL_MIN/MAX_NCHANNELS before the RCCL communicator is created "
+                        "(0 = RCCL's topology default; >= 7 spans all xGMI links of an MI355X)")
+    g.add_argument("--ddp-debug", action="store_true",
+                   help="debug: reducer assertions (double ready-mark, double bucket launch) and a "
+                        "cross-rank collective-sequence check at every consistency check")
+    g.add_argument("--amp-val", action="store_true",
+                   help="run validation under autocast too (the reference validates in fp32)")
+    g.add_argument("--ref-throughput", action="store_true",
+                   help="native impl: time each step from after the loader yields to after a host sync "
+                        "(the reference's step-line definition, train_ddp.py:196,224) instead of the "
+                        "default sync-to-sync window, which has no per-step host sync")
+    g.add_argument("--fault-inject", default=None, type=str, metavar="RANK:STEP",
+                   help="testing: rank RANK exits abruptly (os._exit(17)) before global step STEP")
     g.add_argument("--cuda-graph", action="store_true",
                    help="capture the training step in a hipGraph (static shapes, native impl)")
     return p

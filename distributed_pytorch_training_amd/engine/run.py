@@ -32,24 +32,6 @@ def csv_row(epoch: int, tl: float, ta: float, vl: float, va: float, et: float) -
     return f"{epoch},{tl:.4f},{ta:.2f},{vl:.4f},{va:.2f},{et:.4f}\n"
 
 
-def _check_consistency(trainer, world_size: int) -> None:
-    """Debug: parameters must be bit-identical across ranks."""
-    import torch.distributed as dist
-
-    if world_size <= 1:
-        return
-    if trainer.ddp is not None:
-        flat = trainer.ddp.arena.param_flat
-    else:
-        flat = torch.cat([p.detach().reshape(-1) for p in trainer.module.parameters()])
-    s = flat.double().sum().reshape(1)
-    lo, hi = s.clone(), s.clone()
-    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-    if float(hi - lo) != 0.0:
-        raise RuntimeError(f"parameters diverged across ranks: checksum range {float(lo)}..{float(hi)}")
-
-
 def main(argv: Optional[Sequence[str]] = None) -> int:
     args = parse_args(argv)
     Path(args.output_dir).mkdir(parents=True, exist_ok=True)
@@ -87,9 +69,20 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     try:
         _epochs(args, trainer, train_loader, val_loader, train_sampler, start_epoch, rank, world_size,
                 metrics_path, perf_path)
-    except BaseException:
-        trainer.abort()  # unblock peers stuck in RCCL collectives, then re-raise
-        raise
+    except BaseException as e:
+        if world_size <= 1:
+            raise
+        # abort the device communicator (peers stuck in a collective error out
+        # instead of hanging), then leave non-zero without waiting on collectives a dead peer
+        # will never join (destroy_process_group / atexit handlers could block).
+        trainer.abort()
+        import traceback
+        traceback.print_exc()
+        print(f"rank {rank}: training failed ({type(e).__name__}: {e}); exiting", flush=True)
+        import sys
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(1)
     trainer.close()
     cleanup_distributed()
     return 0
@@ -105,7 +98,7 @@ def _epochs(args, trainer, train_loader, val_loader, train_sampler, start_epoch,
         else:
             vl, va = float("nan"), float("nan")
         if args.check_consistency:
-            _check_consistency(trainer, world_size)
+            trainer.check_consistency()
         if rank == 0:
             print(format_epoch_line(epoch, args.epochs, st.loss, st.acc, vl, va, st.epoch_time), flush=True)
             with metrics_path.open("a") as f:

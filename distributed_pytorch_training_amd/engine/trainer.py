@@ -31,6 +31,7 @@ from .. import ops
 from ..amp import DeviceGradScaler, autocast
 from ..ops import conv as native_conv
 from ..profiling.timeline import StepTimeline, roctx_range
+from ..utils.dist import all_reduce_
 
 
 def format_step_line(epoch: int, i: int, n: int, avg_loss: float, avg_acc: float, thr: float) -> str:
@@ -87,20 +88,24 @@ class Trainer:
 
     # ------------------------------------------------------------------ construction
     def _init_native(self, model: nn.Module, comm) -> None:
+        from ..models.layers import fuse_native_layers, set_conv_routing
         from ..optim import build_optimizer
         from ..parallel.ddp import NativeDDP
 
         args = self.args
-        if (getattr(args, "fused_bn", True) and self.device.type == "cuda"
-                and getattr(args, "channels_last", False)):
-            from ..models.layers import fuse_native_layers
-            fuse_native_layers(model)
-            native_conv.ENABLED = bool(getattr(args, "native_conv", True))
-            if getattr(args, "cuda_graph", False) and "DPT_CONV_MIN_PIXELS" not in os.environ:
-                # launches hidden by the graph: tiny convs are faster on MIOpen (ops/conv.py)
-                native_conv.MIN_PIXELS = 3072
+        gpu_cl = self.device.type == "cuda" and bool(getattr(args, "channels_last", False))
+        # MFMA convs need channels_last bf16/fp16 activations; routing is per model
+        use_native_conv = gpu_cl and bool(getattr(args, "native_conv", True)) and native_conv.ENABLED
+        min_px = None
+        if getattr(args, "cuda_graph", False) and "DPT_CONV_MIN_PIXELS" not in os.environ:
+            # launches hidden by the graph: tiny convs are faster on MIOpen (ops/conv.py)
+            min_px = 3072
+        if getattr(args, "fused_bn", True) and gpu_cl:
+            fuse_native_layers(model, native_conv=use_native_conv, min_pixels=min_px)
+        else:
+            set_conv_routing(model, use_native_conv, min_px)
         # per-step flip cache of the stride-1 backward-data weights (ops/conv.py)
-        self._native_conv_cache = self.device.type == "cuda" and native_conv.ENABLED
+        self._native_conv_cache = use_native_conv
         params_in_order = [p for p in model.parameters() if p.requires_grad]
         self.scaler = DeviceGradScaler(self.device, enabled=self.amp)
         shadow = None
@@ -112,7 +117,10 @@ class Trainer:
                              broadcast_buffers=args.broadcast_buffers, grad_dtype=args.grad_dtype,
                              found_inf=self.scaler.found_inf, scale=self.scaler.scale_tensor,
                              check_inf=self.amp, profile=self.timeline.enabled, comm=comm,
-                             weight_shadow=shadow)
+                             weight_shadow=shadow, comm_kind=getattr(args, "comm", "rccl"),
+                             timeout_s=getattr(args, "dist_timeout", None),
+                             rccl_channels=getattr(args, "rccl_channels", 0),
+                             debug=bool(getattr(args, "ddp_debug", False)))
         self.model = self.ddp
         self.module = model
         self.optimizer = build_optimizer(args.optimizer, self.ddp.arena, args, params_in_order)
@@ -165,6 +173,8 @@ class Trainer:
         tl.mark("start")
         if self._native_conv_cache:
             native_conv.begin_step()  # weights changed since the last step: new flip cache
+        else:
+            native_conv.reset_side_channels()
         ctx = self.ddp.no_sync() if not sync else contextlib.nullcontext()
         rx = self.roctx
         with ctx:
@@ -176,6 +186,9 @@ class Trainer:
             with roctx_range("backward+allreduce", rx):
                 try:
                     (self.scaler.scale(scaled) if self.amp else scaled).backward()
+                except BaseException:
+                    native_conv.reset_side_channels()  # no stale BN-backward partials survive
+                    raise
                 finally:
                     if self._native_conv_cache:
                         native_conv.end_caching()
@@ -188,10 +201,11 @@ class Trainer:
             self.log(f"rebuilt buckets: {self.ddp.bucket_sizes_mib()}")
         with roctx_range("optimizer", rx):
             self.optimizer.step(self.scaler if self.amp else None, host_factor=self.ddp.grad_factor,
-                                grads_checked=self.ddp.grads_checked, shadow=self.ddp.shadow_flat)
+                                grads_checked=self.ddp.grads_checked, shadow=self.ddp.shadow_flat,
+                                zero_grad=not self.ddp.grads_overwritten)
         tl.mark("opt")
         ops.accumulate_metrics(outputs, targets, loss, self.metrics)
-        tl.end_step(self.ddp.comm_profile if tl.enabled else None)
+        tl.end_step(self.ddp.comm_profile_ref() if tl.enabled else None)
         self.global_step += 1
         return outputs, loss
 
@@ -218,7 +232,46 @@ class Trainer:
         return outputs, loss
 
     # ------------------------------------------------------------------ epochs
+    def _fault_step(self) -> Optional[int]:
+        spec = getattr(self.args, "fault_inject", None)
+        if not spec:
+            return None
+        r, st = (int(v) for v in str(spec).split(":"))
+        return st if r == self.rank else None
+
+    def check_consistency(self) -> None:
+        """Debug: parameters must be bit-identical across ranks; with
+        ``--ddp-debug`` the device collective sequences must match too."""
+        if self.world_size <= 1:
+            return
+        if self.ddp is not None:
+            self.ddp.check_comm()
+            flat = self.ddp.arena.param_flat
+        else:
+            flat = torch.cat([p.detach().reshape(-1) for p in self.module.parameters()])
+        s = flat.double().sum().reshape(1)
+        lo, hi = s.clone(), s.clone()
+        all_reduce_(lo, op=dist.ReduceOp.MIN)
+        all_reduce_(hi, op=dist.ReduceOp.MAX)
+        if float(hi - lo) != 0.0:
+            raise RuntimeError(f"parameters diverged across ranks: checksum range {float(lo)}..{float(hi)}")
+        if self.ddp is not None and getattr(self.args, "ddp_debug", False):
+            self.ddp.verify_sequence()
+
+    def _host_touch(self) -> None:
+        """Host touch point: surface a tripped communicator watchdog as an exception."""
+        if self.ddp is not None:
+            self.ddp.check_comm()
+
     def train_one_epoch(self, epoch: int, loader, train_sampler=None) -> EpochStats:
+        """One epoch with the reference's stdout contract (train_ddp.py:170-263).
+
+        Throughput windows: native default = sync-to-sync wall time over the window (no
+        per-step host sync exists to time individual steps); ``--ref-throughput`` (and the torch
+        engine always) = the reference's definition, the sum of per-step times measured from
+        after the loader yields to after the step's host sync (train_ddp.py:196,224).
+        ``--warmup-steps N``: the first N steps of the first epoch this trainer runs are left
+        out of every window."""
         args, rank, ws = self.args, self.rank, self.world_size
         self.model.train()
         if train_sampler is not None:
@@ -227,6 +280,13 @@ class Trainer:
             loader.set_epoch(epoch)
         n = len(loader)
         native = self.impl == "native"
+        ref_thr = (not native) or bool(getattr(args, "ref_throughput", False))
+        warm = 0
+        if not getattr(self, "_warmed", False):
+            warm = max(0, int(getattr(args, "warmup_steps", 0) or 0))
+            self._warmed = True
+        check_every = int(getattr(args, "check_consistency", 0) or 0)
+        fault_at = self._fault_step()
         if native:
             self.metrics.zero_()
         epoch_loss, epoch_correct, epoch_total = 0.0, 0, 0
@@ -237,43 +297,46 @@ class Trainer:
         win_start = time.time()
         steps = 0
         for i, (images, targets) in enumerate(loader):
+            if fault_at is not None and self.global_step >= fault_at:
+                os._exit(17)   # --fault-inject: die abruptly, peers must not hang
             sync = (i + 1) % self.grad_accum == 0 or i + 1 == n
+            batch_start = time.time()
+            outputs, loss = self.train_step(images, targets, sync)
+            bs = images.size(0)
             if native:
-                self.train_step(images, targets, sync)
-                bs = images.size(0)
-                accum_samples += bs * ws
-                steps += 1
-                if rank == 0 and (i + 1) % args.print_freq == 0:
+                if ref_thr:
                     _sync(self.device)
-                    now = time.time()
-                    accum_time = now - win_start
-                    m = self.metrics.tolist()
-                    avg_loss = m[0] / m[2]
-                    avg_acc = 100.0 * m[1] / m[2]
-                    thr = accum_samples / accum_time if accum_time > 0 else 0.0
-                    self.log(format_step_line(epoch, i, n, avg_loss, avg_acc, thr))
-                    windows.append({"step": i + 1, "seconds": accum_time, "samples": accum_samples,
-                                    "throughput": thr})
-                    accum_samples = 0
-                    win_start = time.time()
             else:
-                batch_start = time.time()
-                outputs, loss = self.train_step(images, targets, sync)
-                bs = images.size(0)
                 epoch_loss += loss.item() * bs
                 _, preds = outputs.max(1)
                 epoch_correct += preds.eq(targets).sum().item()
                 epoch_total += bs
-                accum_time += time.time() - batch_start
-                accum_samples += bs * ws
-                steps += 1
-                if rank == 0 and (i + 1) % args.print_freq == 0:
-                    thr = accum_samples / accum_time if accum_time > 0 else 0.0
-                    self.log(format_step_line(epoch, i, n, epoch_loss / epoch_total,
-                                              100.0 * epoch_correct / epoch_total, thr))
-                    windows.append({"step": i + 1, "seconds": accum_time, "samples": accum_samples,
-                                    "throughput": thr})
-                    accum_time, accum_samples = 0.0, 0
+            steps += 1
+            if i < warm:
+                if i + 1 == warm:          # warmup over: the windows start now
+                    _sync(self.device)
+                    win_start, accum_time, accum_samples = time.time(), 0.0, 0
+                continue
+            accum_time += time.time() - batch_start
+            accum_samples += bs * ws
+            if sync and check_every and self.global_step % check_every == 0:
+                self.check_consistency()
+            if rank == 0 and (i + 1) % args.print_freq == 0:
+                if native:
+                    _sync(self.device)
+                    self._host_touch()
+                    if not ref_thr:
+                        accum_time = time.time() - win_start
+                    m = self.metrics.tolist()
+                    avg_loss, avg_acc = m[0] / m[2], 100.0 * m[1] / m[2]
+                else:
+                    avg_loss, avg_acc = epoch_loss / epoch_total, 100.0 * epoch_correct / epoch_total
+                thr = accum_samples / accum_time if accum_time > 0 else 0.0
+                self.log(format_step_line(epoch, i, n, avg_loss, avg_acc, thr))
+                windows.append({"step": i + 1, "seconds": accum_time, "samples": accum_samples,
+                                "throughput": thr})
+                accum_time, accum_samples = 0.0, 0
+                win_start = time.time()
         # ---- epoch reduction (one float64[3] all-reduce instead of three scalars)
         if native:
             tot = self.metrics.clone()
@@ -281,8 +344,9 @@ class Trainer:
             tot = torch.tensor([epoch_loss, float(epoch_correct), float(epoch_total)],
                                dtype=torch.float64, device=self.device)
         if ws > 1:
-            dist.all_reduce(tot)
+            all_reduce_(tot)
         _sync(self.device)
+        self._host_touch()
         epoch_time = time.time() - start_epoch
         t = tot.tolist()
         samples = int(t[2])
@@ -292,11 +356,14 @@ class Trainer:
 
     @torch.no_grad()
     def validate(self, loader) -> EpochStats:
+        """Full unsharded pass on every rank (reference train_ddp.py:266-300).  fp32 like the
+        reference - no autocast even under ``--amp`` - unless ``--amp-val`` opts in."""
         self.model.eval()
         acc = torch.zeros(3, dtype=torch.float64, device=self.device)
         t0 = time.time()
+        amp_val = self.amp and bool(getattr(self.args, "amp_val", False))
         for images, targets in loader:
-            with autocast(self.device, self.amp, self.amp_dtype):
+            with autocast(self.device, amp_val, self.amp_dtype):
                 outputs = self.model(images)
                 loss = self.criterion(outputs, targets)
             if self.impl == "native":
@@ -308,7 +375,7 @@ class Trainer:
                 acc[1] += preds.eq(targets).sum().item()
                 acc[2] += bs
         if self.world_size > 1:
-            dist.all_reduce(acc)
+            all_reduce_(acc)
         t = acc.tolist()
         if self.rank == 0 and t[2] > 0:
             return EpochStats(t[0] / t[2], 100.0 * t[1] / t[2], time.time() - t0)

@@ -172,10 +172,24 @@ class GemmConv1x1(nn.Conv2d):
         return y.permute(0, 3, 1, 2)
 
 
-def fuse_native_layers(model: nn.Module, gemm_1x1: bool = False) -> int:
+def set_conv_routing(model: nn.Module, native_conv: bool = True, min_pixels=None) -> None:
+    """Per-model conv routing: MFMA kernels (ops/conv.py) or MIOpen, stored on each conv."""
+    for m in model.modules():
+        if isinstance(m, nn.Conv2d):
+            m.dpt_native_conv = bool(native_conv)
+            m.dpt_min_pixels = min_pixels
+
+
+def fuse_native_layers(model: nn.Module, gemm_1x1: bool = False, native_conv: bool = True,
+                       min_pixels=None) -> int:
     """Install the gfx950 fused layers: BatchNorm2d -> FusedBatchNorm2d (fused with ReLU /
     residual add by the model's ``bn_act`` calls) and MaxPool2d -> FusedMaxPool2d.  Modules
-    keep their parameters/buffers, so state dicts and checkpoints are unchanged."""
+    keep their parameters/buffers, so state dicts and checkpoints are unchanged.
+
+    ``native_conv`` / ``min_pixels``: this model's conv routing (MFMA kernels or MIOpen; convs
+    with fewer output pixels than ``min_pixels`` stay on MIOpen), stored on each conv module so
+    two models in one process never share it."""
+    set_conv_routing(model, native_conv, min_pixels)
     n = fuse_batchnorm(model)
     for parent in model.modules():
         for name, child in list(parent.named_children()):

@@ -25,13 +25,19 @@ from . import native, native_available
 _CL = torch.channels_last
 # element types of the MFMA kernels (bf16 and fp16 operands, fp32 accumulation)
 _DT16 = (torch.bfloat16, torch.float16)
+# process-wide kill switch (environment); per-model routing lives on the conv modules
 ENABLED = os.environ.get("DPT_NATIVE_CONV", "1") != "0"
 # Backward-data of a conv fed by a fused BN+ReLU also sums that BN's backward statistics in its
 # epilogue (the BN backward then skips its statistics pass).
 BN_BWD_FUSE = os.environ.get("DPT_BN_BWD_FUSE", "1") != "0"
-# dx.data_ptr() -> (p1, p2, shape, dres_ptr, p3): handed from a conv's backward to the BN backward
-# that receives dx as its output gradient (ops/bn.py), consumed once
+# dx.data_ptr() -> (generation, dx._version, p1, p2, shape, dres_ptr, p3): handed from a conv's
+# backward to the BN backward that receives dx as its output gradient (ops/bn.py), consumed once.
+# An entry is only honoured in the step generation that made it and while dx is unmodified (its
+# version counter unchanged: autograd accumulating a second gradient into dx in place would
+# invalidate the statistics); begin_step()/reset_side_channels() drop everything left over (an
+# aborted backward), so a reused allocation can never pick up stale statistics.
 _BNB_PARTIALS = {}
+_GEN = [0]
 # Stride-2 backward-data on the MFMA kernels (four parity-class convs); 0 = MIOpen
 S2_DGRAD = os.environ.get("DPT_S2_DGRAD", "1") != "0"
 # The im2col stem path is correct but measured slower than MIOpen on ResNet-50's 7x7/2 stem at
@@ -39,7 +45,8 @@ S2_DGRAD = os.environ.get("DPT_S2_DGRAD", "1") != "0"
 STEM_ENABLED = os.environ.get("DPT_NATIVE_STEM", "0") == "1"
 
 
-# Convs with fewer output pixels than this go to MIOpen (default: none).  A 128-row tile grid
+# Convs with fewer output pixels than this go to MIOpen (default: none; a model can override it
+# per conv through models.layers.fuse_native_layers(min_pixels=...)).  A 128-row tile grid
 # that small cannot fill 256 CUs - ResNet-18 on 32x32 inputs has 128-2048 output pixels in
 # layer2-4 at batch 128 - and with the launches hidden by a hipGraph MIOpen's small-shape
 # kernels win (3072: 46.5k -> 60.7k img/s), but eagerly the native path is faster (41.6k vs
@@ -47,7 +54,7 @@ STEM_ENABLED = os.environ.get("DPT_NATIVE_STEM", "0") == "1"
 MIN_PIXELS = int(os.environ.get("DPT_CONV_MIN_PIXELS", "0"))
 
 
-def supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups) -> bool:
+def supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups, min_pixels=None) -> bool:
     if not (ENABLED and x.is_cuda and native_available() and x.dtype in _DT16
             and w.dtype == x.dtype and x.dim() == 4 and groups == 1):
         return False
@@ -57,7 +64,8 @@ def supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, group
     ho = (x.shape[2] + 2 * padding[0] - r) // stride[0] + 1
     wo = (x.shape[3] + 2 * padding[1] - s) // stride[1] + 1
     return (cin % 64 == 0 and cout % 64 == 0 and r == s and x.shape[1] == cin
-            and x.shape[0] * ho * wo >= MIN_PIXELS and x.is_contiguous(memory_format=_CL))
+            and x.shape[0] * ho * wo >= (MIN_PIXELS if min_pixels is None else min_pixels)
+            and x.is_contiguous(memory_format=_CL))
 
 
 def _cl(t: torch.Tensor) -> torch.Tensor:
@@ -76,7 +84,7 @@ def _backward(ctx, dy):
         if src is not None and not isinstance(src[2], dict):  # BN+ReLU: (x, mean, coef)
             bn_x, bn_mean, bn_coef = src
             dx, p1, p2, _ = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, bn_coef, w_flipped=wt)
-            _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), None, None)
+            _put_bnb(dx, p1, p2, None, None)
         elif src is not None and _dres_ok(dres := src[2].pop("dres", None), x):  # (x, mean, slot)
             # block-tail BN+add+ReLU (ops/bn.py pair outputs): the next block's tail already
             # produced the identity-path gradient dres; dx becomes the tail's masked total
@@ -86,7 +94,7 @@ def _backward(ctx, dy):
             # folded into it (ops/bn.py _BN2AddReLUPair) - also sum that BN's statistic
             x2, mean2 = (src[3], src[4]) if len(src) > 3 else (None, None)
             dx, p1, p2, p3 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, None, x, dres, wt, x2, mean2)
-            _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), dres.data_ptr(), p3 if x2 is not None else None)
+            _put_bnb(dx, p1, p2, dres.data_ptr(), p3 if x2 is not None else None)
         elif s == 1:
             dx = native().conv_dgrad_flip(dy, w, p)[0] if wt is None else native().conv_dgrad_preflipped(dy, wt, p)
         elif s == 2 and S2_DGRAD and x.dim() == 4:
@@ -94,7 +102,7 @@ def _backward(ctx, dy):
             if src is not None and not isinstance(src[2], dict) and w.shape[2] > 1:
                 # BN+ReLU input: its backward statistics from the parity-class epilogues too
                 dx, p1, p2 = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3], src[0], src[1], src[2])
-                _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), None, None)
+                _put_bnb(dx, p1, p2, None, None)
             else:
                 dx = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3])[0]
         else:
@@ -116,7 +124,18 @@ def _backward(ctx, dy):
 _FLIP = {"on": False, "pending": {}, "done": {}}
 
 
+def reset_side_channels() -> None:
+    """New step generation: forget every BN-backward hand-over not consumed so far."""
+    _GEN[0] += 1
+    _BNB_PARTIALS.clear()
+
+
+def _put_bnb(dx, p1, p2, dres_ptr, p3) -> None:
+    _BNB_PARTIALS[dx.data_ptr()] = (_GEN[0], dx._version, p1, p2, tuple(dx.shape), dres_ptr, p3)
+
+
 def begin_step() -> None:
+    reset_side_channels()
     _FLIP["on"] = True
     _FLIP["pending"].clear()
     _FLIP["done"].clear()
@@ -199,7 +218,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bo
 def register_bnb_partials(dx: torch.Tensor, p1: torch.Tensor, p2: torch.Tensor) -> None:
     """Hand BN+ReLU backward-statistics partials summed by dx's producer to the BN backward
     that receives dx as its output gradient (other producers than convs: the stem pool)."""
-    _BNB_PARTIALS[dx.data_ptr()] = (p1, p2, tuple(dx.shape), None, None)
+    _put_bnb(dx, p1, p2, None, None)
 
 
 def take_bnb_partials(dy: torch.Tensor):
@@ -210,9 +229,12 @@ def take_bnb_partials(dy: torch.Tensor):
     if not _BNB_PARTIALS:
         return None
     ent = _BNB_PARTIALS.pop(dy.data_ptr(), None)
-    if ent is None or ent[2] != tuple(dy.shape):
+    if ent is None:
         return None
-    return ent[0], ent[1], ent[3], ent[4]
+    gen, ver, p1, p2, shape, dres_ptr, p3 = ent
+    if gen != _GEN[0] or ver != dy._version or shape != tuple(dy.shape):
+        return None
+    return p1, p2, dres_ptr, p3
 
 
 def take_bn_partials(x: torch.Tensor):

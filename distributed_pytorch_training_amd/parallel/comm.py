@@ -1,15 +1,30 @@
-"""Communicator bootstrap: the framework-owned RCCL communicator for the gradient hot path.
+"""Communicator bootstrap: the framework-owned collective for the gradient hot path.
 
 Control plane: torch's process group (``env://`` TCPStore rendezvous, reference
 train_ddp.py:65) carries the 128-byte RCCL unique id from rank 0 to every rank.  Data
-plane: the C++ ``RcclComm`` (csrc/rccl_comm.cpp) owns the communicator and a
-high-priority HIP stream that the C++ reducer enqueues bucket all-reduces on.
+plane: a C++ ``Collective`` (csrc/comm.h) that the C++ reducer enqueues bucket all-reduces
+on, one of
 
-On CPU (gloo) there is no RCCL; ``make_comm`` returns ``None`` and the reducer drives
-``torch.distributed`` through a Python callback instead.
+* ``"rccl"`` - ``RcclComm`` (csrc/rccl_comm.cpp): RCCL over xGMI on a dedicated
+  high-priority HIP stream, guarded by a watchdog thread (csrc/watchdog.cpp) that enforces
+  ``--dist-timeout`` and polls ``ncclCommGetAsyncError``;
+* ``"host"`` - ``HostBridgeComm`` (csrc/host_comm.cpp): the same device-pointer contract
+  served by ``torch.distributed`` over gloo through pinned host staging.  Several ranks can
+  then share one GPU and still run the whole multi-rank GPU data path (tests/
+  test_multirank_gpu.py); it is a verification / debug transport, not a fast one.
+
+On CPU (gloo) there is no device collective; ``make_comm`` returns ``None`` and the reducer
+drives ``torch.distributed`` through a Python callback instead.
+
+RCCL channel count: ``rccl_channels`` > 0 exports ``NCCL_MIN_NCHANNELS`` /
+``NCCL_MAX_NCHANNELS`` before ``ncclCommInitRank`` (read once at communicator creation).  On
+an 8x MI355X node every GPU has 7 point-to-point xGMI links; a ring uses one outgoing link
+per channel, so a bucket only reaches the aggregate link bandwidth with >= 7 channels
+(SURVEY.md §5.8).  0 keeps RCCL's own topology-derived choice.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -17,12 +32,49 @@ import torch.distributed as dist
 
 from .. import ops
 
+COMM_KINDS = ("rccl", "host")
+_HOST_GROUP = None
 
-def make_comm(device: torch.device, rank: int, world_size: int):
-    """Create an RcclComm on ``device`` (GPU) or return None (CPU/gloo path)."""
+
+def _host_group():
+    """A gloo group for the host bridge (the default group when it already is gloo)."""
+    global _HOST_GROUP
+    if _HOST_GROUP is None:
+        _HOST_GROUP = dist.group.WORLD if dist.get_backend() == "gloo" else dist.new_group(backend="gloo")
+    return _HOST_GROUP
+
+
+def _host_all_reduce(t: torch.Tensor) -> None:
+    dist.all_reduce(t, group=_host_group())
+
+
+def _host_broadcast(t: torch.Tensor, root: int) -> None:
+    dist.broadcast(t, root, group=_host_group())
+
+
+def apply_rccl_channels(n: int) -> None:
+    if n and n > 0:
+        os.environ.setdefault("NCCL_MIN_NCHANNELS", str(int(n)))
+        os.environ.setdefault("NCCL_MAX_NCHANNELS", str(int(n)))
+
+
+def make_comm(device: torch.device, rank: int, world_size: int, kind: str = "rccl",
+              timeout_s: Optional[float] = None, rccl_channels: int = 0,
+              exit_grace_s: float = 30.0):
+    """Create the device collective on ``device`` (GPU) or return None (CPU/gloo path)."""
     if device.type != "cuda":
         return None
+    if kind not in COMM_KINDS:
+        raise ValueError(f"unknown communicator kind {kind!r}; expected one of {COMM_KINDS}")
     C = ops.native()
+    dev = device.index if device.index is not None else 0
+    if kind == "host":
+        if world_size > 1 and not dist.is_initialized():
+            raise RuntimeError("the host-bridge communicator needs an initialised process group")
+        if world_size > 1:
+            _host_group()   # collective group creation: every rank, same point
+        return C.HostBridgeComm(_host_all_reduce, _host_broadcast, rank, world_size, dev)
+    apply_rccl_channels(rccl_channels)
     if world_size > 1:
         if not dist.is_initialized():
             raise RuntimeError("make_comm needs an initialised torch.distributed process group")
@@ -31,11 +83,14 @@ def make_comm(device: torch.device, rank: int, world_size: int):
         uid = box[0]
     else:
         uid = C.RcclComm.new_unique_id()
-    return C.RcclComm(uid, rank, world_size, device.index if device.index is not None else 0)
+    comm = C.RcclComm(uid, rank, world_size, dev)
+    if timeout_s and timeout_s > 0 and world_size > 1:
+        comm.enable_watchdog(float(timeout_s), 0.5, float(exit_grace_s))
+    return comm
 
 
 def broadcast_(tensor: torch.Tensor, comm, src: int = 0) -> None:
-    """Broadcast on the current stream through the RCCL comm (GPU) or torch.distributed."""
+    """Broadcast on the current stream through the device comm (GPU) or torch.distributed."""
     if comm is not None:
         comm.broadcast(tensor, src)
     elif dist.is_initialized() and dist.get_world_size() > 1:
@@ -47,3 +102,9 @@ def all_reduce_(tensor: torch.Tensor, comm=None) -> None:
         comm.all_reduce(tensor, True)
     elif dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(tensor)
+
+
+def check(comm) -> None:
+    """Host touch point: raise if the communicator's watchdog tripped (no-op without one)."""
+    if comm is not None:
+        comm.check()

@@ -44,7 +44,9 @@ class NativeDDP(nn.Module):
                  grad_dtype: str = "fp32", found_inf: Optional[torch.Tensor] = None,
                  scale: Optional[torch.Tensor] = None, check_inf: bool = False,
                  profile: bool = False, rebuild_buckets: bool = True, comm=None,
-                 weight_shadow: Optional[torch.dtype] = None) -> None:
+                 weight_shadow: Optional[torch.dtype] = None, comm_kind: str = "rccl",
+                 timeout_s: Optional[float] = None, rccl_channels: int = 0,
+                 debug: bool = False) -> None:
         super().__init__()
         self.module = module
         self.rank, self.world_size = rank, world_size
@@ -53,6 +55,7 @@ class NativeDDP(nn.Module):
         self.broadcast_buffers = broadcast_buffers
         self.grad_dtype = grad_dtype
         self.profile = profile
+        self._profile_slots = 1
         self.rebuild_buckets = rebuild_buckets and world_size > 1
         self.require_backward_grad_sync = True
         self._sync_buffers_next = True
@@ -61,6 +64,7 @@ class NativeDDP(nn.Module):
         self.found_inf = found_inf if found_inf is not None else torch.zeros(1, device=self.device)
         self.scale = scale
         self.check_inf = check_inf
+        self.debug = debug
 
         named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
         if world_size > 1:
@@ -69,8 +73,9 @@ class NativeDDP(nn.Module):
         named = list(reversed(named))
         self.arena = FlatArena([p for _, p in named], names=[n for n, _ in named])
         self.buffers_arena = BufferArena(module)
-        self.comm = comm if comm is not None else (make_comm(self.device, rank, world_size)
-                                                   if world_size > 1 else None)
+        self.comm = comm if comm is not None else (
+            make_comm(self.device, rank, world_size, kind=comm_kind, timeout_s=timeout_s,
+                      rccl_channels=rccl_channels) if world_size > 1 else None)
         if world_size > 1:
             broadcast_(self.arena.param_flat, self.comm, 0)
             for t in self.buffers_arena.tensors():
@@ -131,6 +136,48 @@ class NativeDDP(nn.Module):
             self.plan.offsets, self.plan.numels, self.plan.param_bucket, self.comm, py_cb, wire,
             wire_buf, self.found_inf, self.scale if self.scale is not None else torch.empty(0),
             1.0 / self.world_size, bool(self.check_inf), bool(self.profile), gpu)
+        if self.debug:
+            self.reducer.set_debug(True)
+        if self._profile_slots > 1:
+            self.reducer.set_profile_slots(self._profile_slots)
+        self._verify_plan()
+
+    def plan_signature(self) -> str:
+        """Hash of the collective sequence one backward issues: bucket count, element counts
+        and wire dtype, in launch order."""
+        desc = f"{self.grad_dtype};" + ",".join(str(n) for n in self.plan.numels)
+        return hashlib.sha1(desc.encode()).hexdigest()
+
+    def _verify_plan(self) -> None:
+        """Every rank must issue the same bucket all-reduces in the same order, or the
+        collectives pair up wrongly and hang (RCCL) / mis-sum (gloo).  Compared once per
+        (re)build over the control plane; a mismatch raises on every rank instead of
+        deadlocking in the first backward."""
+        if self.world_size <= 1 or not dist.is_initialized():
+            return
+        mine = (self.plan_signature(), len(self.plan.numels))
+        gathered = [None] * self.world_size
+        dist.all_gather_object(gathered, mine)
+        if any(g != gathered[0] for g in gathered):
+            raise RuntimeError("NativeDDP: gradient bucket plans differ across ranks "
+                               f"(signature, buckets) per rank = {gathered}; every rank must use the "
+                               "same model, --bucket-cap-mb / --first-bucket-mb and --grad-dtype")
+
+    def check_comm(self) -> None:
+        """Host touch point: raise if the communicator's watchdog tripped."""
+        if self.comm is not None:
+            self.comm.check()
+
+    def verify_sequence(self) -> None:
+        """Debug: the device collectives issued so far must be the same sequence on every rank
+        (count and a running hash of kind / element count / dtype / root)."""
+        if self.world_size <= 1 or self.comm is None or not dist.is_initialized():
+            return
+        mine = (int(self.comm.ops), int(self.comm.sequence_hash))
+        gathered = [None] * self.world_size
+        dist.all_gather_object(gathered, mine)
+        if any(g != gathered[0] for g in gathered):
+            raise RuntimeError(f"NativeDDP: collective sequences diverged across ranks: {gathered}")
 
     def _cpu_allreduce(self, b: int, off: int, n: int) -> None:
         """gloo path: called by the C++ reducer when bucket ``b`` is complete."""
@@ -149,6 +196,13 @@ class NativeDDP(nn.Module):
     def grad_factor(self) -> float:
         """Host-side factor the optimizer applies to the arena gradients (1/world_size)."""
         return 1.0 / self.world_size
+
+    @property
+    def grads_overwritten(self) -> bool:
+        """True when the next synced backward rewrites every arena gradient (the GPU
+        steal-mode reducer gathers each bucket and zero-fills unused parameters), so the
+        optimizer need not zero the arena (``no_sync`` zeroes it itself on entry)."""
+        return self.reducer is not None and self.device.type == "cuda"
 
     @property
     def grads_checked(self) -> bool:
@@ -176,6 +230,9 @@ class NativeDDP(nn.Module):
             raise RuntimeError("no_sync/gradient accumulation is not supported with 16-bit weight "
                                "shadows; construct NativeDDP with weight_shadow=None")
         old = self.require_backward_grad_sync
+        if not self._pending_accum and self.grads_overwritten:
+            # first micro-batch: the optimizer left the last step's gradients in the arena
+            self.arena.grad_flat.zero_()
         self.require_backward_grad_sync = False
         self._pending_accum = True
         if self.reducer is not None:
@@ -239,21 +296,33 @@ class NativeDDP(nn.Module):
     def bucket_sizes_mib(self) -> List[float]:
         return self.plan.sizes_mib(self.arena.param_flat.element_size()) if self.plan else []
 
-    def set_profile(self, enabled: bool) -> None:
+    def set_profile(self, enabled: bool, slots: int = 1) -> None:
         """Turn the reducer's per-bucket hipEvent timing on/off after construction (the events
         are created with the reducer, so it is rebuilt over the same arena - layout, buckets and
-        communicator unchanged).  Call between steps, never inside a captured hipGraph."""
-        if bool(enabled) == bool(self.profile):
+        communicator unchanged).  ``slots``: how many backwards keep their own events, i.e. how
+        many steps may run before their times must be read (no host sync inside a window of
+        that many steps).  Call between steps, never inside a captured hipGraph."""
+        slots = max(1, int(slots))
+        if bool(enabled) == bool(self.profile) and slots == self._profile_slots:
             return
         self.profile = bool(enabled)
+        self._profile_slots = slots
         if self.reducer is not None:
             self._build_reducer()
 
-    def comm_profile(self):
+    def comm_profile(self, slot: int = -1):
+        """Per-bucket and per-step comm times of backward ``slot`` (-1: the last one), or None."""
         if self.reducer is None or self.comm is None:
             return None
-        return {"bucket_ms": list(self.reducer.bucket_times_ms()),
-                "step_ms": list(self.reducer.step_times_ms())}
+        return {"bucket_ms": list(self.reducer.bucket_times_ms(slot)),
+                "step_ms": list(self.reducer.step_times_ms(slot))}
+
+    def comm_profile_ref(self):
+        """A deferred reader of the backward that just finished (valid for ``slots`` steps)."""
+        if self.reducer is None or self.comm is None:
+            return None
+        slot = int(self.reducer.last_slot)
+        return lambda: self.comm_profile(slot)
 
     def state_dict(self, *a, **kw):  # unwrapped keys, torchvision-compatible
         return self.module.state_dict(*a, **kw)

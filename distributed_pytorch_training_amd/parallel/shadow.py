@@ -40,13 +40,19 @@ class ShadowConv2d(nn.Conv2d):
     # set by fuse_native_layers on convs that feed a fused BatchNorm: the native conv's
     # epilogue then also emits the BN statistics partials
     dpt_bn_stats = False
+    # per-model conv routing, set by models.layers.fuse_native_layers (None: ops/conv.py defaults)
+    dpt_native_conv = True
+    dpt_min_pixels = None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         sh = active_shadow(self, x)
         if sh is None:
             return super().forward(x)
         w, b = sh["weight"], sh.get("bias", self.bias)
-        if b is None and native_conv.supported(x, w, self.stride, self.padding, self.dilation, self.groups):
+        if not self.dpt_native_conv:
+            return self._conv_forward(x, w, b)
+        if b is None and native_conv.supported(x, w, self.stride, self.padding, self.dilation, self.groups,
+                                               self.dpt_min_pixels):
             return native_conv.conv2d(x, w, self.stride[0], self.padding[0], self.dpt_bn_stats)
         if b is None and native_conv.s2d_stem_supported(x, w, self.stride, self.padding, self.dilation, self.groups):
             return native_conv.s2d_stem_conv2d(x, w, self.dpt_bn_stats)

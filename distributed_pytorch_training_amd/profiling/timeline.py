@@ -12,17 +12,19 @@ nothing beyond wall clock.  This module measures it:
 * derived: forward / backward / optimizer ms, all-reduce busy ms, exposed ms, and
   "% of step in all-reduce" (busy / step) and "% of step exposed" (exposed / step).
 
-Event reads are deferred: a step's events are resolved one step later (they are complete
-by then without a host sync), so profiling does not serialise the pipeline.
+Event reads are deferred: a step's events are resolved ``max_pending`` steps later (they are
+complete by then), and the reducer keeps one event set per step of the window (event slots),
+so profiling does not serialise the pipeline.
 ``roctx_range`` emits markers for ``rocprofv3 --marker-trace`` when roctx is loadable.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import ctypes
 import json
 import statistics
-from typing import Dict, List, Optional
+from typing import Deque, Dict, List, Optional
 
 import torch
 
@@ -32,7 +34,9 @@ class StepTimeline:
         self.enabled = enabled and torch.device(device).type == "cuda"
         self.device = device
         self._marks: Dict[str, torch.cuda.Event] = {}
-        self._pending: Optional[tuple] = None
+        self._pending: Deque[tuple] = collections.deque()
+        # steps whose events may stay unread; must stay below the reducer's profile slots
+        self.max_pending = 1
         self.records: List[Dict[str, float]] = []
 
     def mark(self, name: str) -> None:
@@ -48,27 +52,23 @@ class StepTimeline:
 
     def end_step(self, comm_profile=None) -> None:
         """``comm_profile``: None, a dict, or a zero-argument callable returning the reducer's
-        per-bucket times.  The reducer re-records its events every backward, so its times must
-        be read before the next step: with a callable, this step's "opt" event is waited on and
-        the times are read now (one host sync per profiled step); the compute-stream marks
-        alone stay deferred by one step."""
+        per-bucket times for THIS step (``NativeDDP.comm_profile_ref()``: bound to the step's
+        event slot).  Nothing is read now: up to ``max_pending`` steps stay unresolved, so a
+        profiled window has no per-step host synchronisation when the reducer keeps at least
+        ``max_pending + 1`` event slots; older steps are resolved (their events are long
+        complete) as new ones arrive."""
         if not self.enabled:
             return
-        self._resolve_pending()
-        marks = dict(self._marks)
+        self._pending.append((dict(self._marks), comm_profile))
         self._marks = {}
-        if callable(comm_profile):
-            if "opt" in marks:
-                marks["opt"].synchronize()
-            comm_profile = comm_profile()
-        self._pending = (marks, comm_profile)
+        while len(self._pending) > self.max_pending:
+            self._resolve_one()
 
-    def _resolve_pending(self) -> None:
-        if self._pending is None:
-            return
-        marks, comm = self._pending
-        self._pending = None
+    def _resolve_one(self) -> None:
+        marks, comm = self._pending.popleft()
         marks["opt"].synchronize()
+        if callable(comm):
+            comm = comm()
         rec = {"fwd_ms": marks["start"].elapsed_time(marks["fwd"]),
                "bwd_ms": marks["fwd"].elapsed_time(marks["bwd"]),
                "opt_ms": marks["bwd"].elapsed_time(marks["opt"]),
@@ -81,6 +81,10 @@ class StepTimeline:
                 rec["exposed_comm_ms"] = comm["step_ms"][1]
                 rec["comm_span_ms"] = comm["step_ms"][2]
         self.records.append(rec)
+
+    def _resolve_pending(self) -> None:
+        while self._pending:
+            self._resolve_one()
 
     def flush(self) -> None:
         if self.enabled:

@@ -113,6 +113,21 @@ def reduce_tensor(tensor: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
     return tensor
 
 
+def all_reduce_(tensor: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+    """In-place all-reduce that never hands a GPU tensor to gloo: with a gloo process group
+    (CPU runs, or ranks sharing one GPU) a device tensor is reduced through a host copy -
+    gloo's own CUDA path is not relied on (it returned wrong sums in this environment)."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return tensor
+    if tensor.is_cuda and dist.get_backend() == "gloo":
+        host = tensor.detach().cpu()
+        dist.all_reduce(host, op=op)
+        tensor.copy_(host)
+    else:
+        dist.all_reduce(tensor, op=op)
+    return tensor
+
+
 def barrier() -> None:
     if is_distributed() and dist.is_initialized():
         dist.barrier()

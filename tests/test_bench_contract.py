@@ -35,8 +35,27 @@ def test_bench_single_process_cpu(tmp_path):
     lines = _json_lines(r.stdout)
     assert len(lines) == 1
     _check(lines[0], 1)
-    assert lines[0]["pct_step_allreduce"] == 0.0
+    # one rank: no collective, so the sync share is not a number (null), not a fake 0.0
+    assert lines[0]["pct_step_allreduce"] is None
+    assert lines[0]["comm"]["kind"] == "none"
 
+
+def test_bench_fake_pg_eight_ranks(tmp_path):
+    """The N=8 line shape (the driver's scaling run) on torch's fake process group: rank 0 of an
+    8-rank job, every collective a no-op; the sync-profiling fields are present."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--fake-pg", *TINY],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    rec = lines[0]
+    _check(rec, 8)
+    for k in ("pct_step_allreduce", "pct_step_exposed_comm", "sync_profile_window", "comm"):
+        assert k in rec, k
+    comm = rec["comm"]
+    assert comm["kind"] == "gloo" and comm["bucket_cap_mb"] == 25.0 and comm["first_bucket_mb"] == 1.0
+    assert len(comm["buckets_mib"]) >= 2 and sum(comm["buckets_mib"]) > 40     # ResNet-18: 42.65 MiB
+    assert "rccl_version" in comm
 
 def test_bench_torchrun_gloo_two_ranks(tmp_path):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")

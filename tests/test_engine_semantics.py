@@ -1,0 +1,60 @@
+"""Engine semantics that must match the reference (train_ddp.py):
+
+* validation runs in fp32 even under ``--amp`` (train_ddp.py:266-283 has no autocast), with an
+  opt-in ``--amp-val``;
+* ``--warmup-steps`` keeps the first steps out of the throughput windows;
+* ``--ref-throughput`` times each step after the loader yields (train_ddp.py:196,224).
+"""
+import torch
+
+from distributed_pytorch_training_amd.config import parse_args
+from distributed_pytorch_training_amd.data import SyntheticLoader
+from distributed_pytorch_training_amd.engine.trainer import Trainer
+from distributed_pytorch_training_amd.models import build_model
+
+BASE = ["--dataset", "synthetic", "--image-size", "32", "--num-classes", "10", "--batch-size", "16",
+        "--model", "resnet18", "--amp-dtype", "bf16"]
+
+
+def _trainer(extra, impl="native"):
+    torch.manual_seed(0)
+    args = parse_args(BASE + ["--impl", impl] + extra)
+    model = build_model("resnet18", 10)
+    return Trainer(model, args, 0, 1, torch.device("cpu"), log=lambda s: None)
+
+
+def _val_loader():
+    return SyntheticLoader(64, 16, 32, 10, torch.device("cpu"), seed=3)
+
+
+def test_validation_is_fp32_under_amp():
+    for impl in ("native", "torch"):
+        plain = _trainer([], impl).validate(_val_loader())
+        amp = _trainer(["--amp"], impl).validate(_val_loader())
+        assert (plain.loss, plain.acc) == (amp.loss, amp.acc), impl
+
+
+def test_amp_val_opt_in_changes_the_quantity():
+    plain = _trainer([]).validate(_val_loader())
+    ampv = _trainer(["--amp", "--amp-val"]).validate(_val_loader())
+    assert plain.loss != ampv.loss       # bf16 autocast forward: a (slightly) different number
+
+
+def test_warmup_steps_leave_the_windows():
+    tr = _trainer(["--warmup-steps", "3", "--print-freq", "2"])
+    st = tr.train_one_epoch(0, SyntheticLoader(16 * 8, 16, 32, 10, torch.device("cpu"), seed=1))
+    # steps 1-3 excluded: windows close at steps 4 (1 step), 6, 8 (2 steps each)
+    assert [w["step"] for w in st.windows] == [4, 6, 8]
+    assert [w["samples"] for w in st.windows] == [16, 32, 32]
+    assert st.steps == 8
+    # only the first epoch warms up
+    st2 = tr.train_one_epoch(1, SyntheticLoader(16 * 4, 16, 32, 10, torch.device("cpu"), seed=1))
+    assert [w["samples"] for w in st2.windows] == [32, 32]
+
+
+def test_ref_throughput_window_is_sum_of_step_times():
+    tr = _trainer(["--ref-throughput", "--print-freq", "2"])
+    st = tr.train_one_epoch(0, SyntheticLoader(16 * 4, 16, 32, 10, torch.device("cpu"), seed=1))
+    assert len(st.windows) == 2
+    for w in st.windows:
+        assert w["seconds"] > 0 and abs(w["throughput"] - w["samples"] / w["seconds"]) < 1e-6
