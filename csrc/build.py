@@ -9,7 +9,13 @@ built object travels with the repository snapshot to the GPU box.
 Linking uses torch's bundled ``libamdhip64.so.7`` / ``librccl.so.1`` (same sonames as
 /opt/rocm's), so one HIP runtime and one RCCL live in the process.
 
-Usage: ``python csrc/build.py [--jobs N] [--force] [--debug]``
+Usage: ``python csrc/build.py [--jobs N] [--force] [--debug] [--asan]``
+
+``--asan``: the HOST C++ (reducer, communicators, watchdog, bindings) is
+compiled with AddressSanitizer into ``build/asan/_C*.so`` - never over the in-tree extension;
+the GPU kernels are not instrumented (no GPU sanitizer on this pool).  Run with
+``LD_PRELOAD=$(gcc -print-file-name=libasan.so) ASAN_OPTIONS=detect_leaks=0
+DPT_NATIVE_LIB=build/asan/_C*.so python -m pytest tests/test_ddp_gloo.py`` (tests/test_asan.py).
 """
 from __future__ import annotations
 
@@ -43,8 +49,9 @@ def _torch_paths():
     return tdir, incs, bool(torch._C._GLIBCXX_USE_CXX11_ABI)
 
 
-def output_path() -> Path:
-    return PKG / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+def output_path(asan: bool = False) -> Path:
+    name = "_C" + sysconfig.get_config_var("EXT_SUFFIX")
+    return (ROOT / "build" / "asan" / name) if asan else (PKG / name)
 
 
 def _run(cmd):
@@ -63,16 +70,20 @@ def _stamp(src: Path, flags) -> str:
     return h.hexdigest()[:16]
 
 
-def build(jobs: int = 4, force: bool = False, debug: bool = False, verbose: bool = False) -> Path:
+def build(jobs: int = 4, force: bool = False, debug: bool = False, verbose: bool = False,
+          asan: bool = False) -> Path:
     tdir, tincs, cxx11 = _torch_paths()
     BUILD.mkdir(parents=True, exist_ok=True)
+    host_build = BUILD.parent / "native-asan" if asan else BUILD
+    host_build.mkdir(parents=True, exist_ok=True)
     py_inc = sysconfig.get_paths()["include"]
     opt = ["-O0", "-g"] if debug else ["-O3"]
+    host_opt = ["-O1", "-g", "-fsanitize=address", "-fno-omit-frame-pointer"] if asan else opt
     common_defs = ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DHIPBLAS_V2",
                    f"-D_GLIBCXX_USE_CXX11_ABI={int(cxx11)}"]
     hip_flags = [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-std=c++17", "-fPIC",
                  *opt, "-Wall", "-Wno-unused-result", *common_defs, f"-I{CSRC}", f"-I{CSRC / 'kernels'}"]
-    cpp_flags = ["g++", "-std=c++17", "-fPIC", "-fvisibility=hidden", *opt, "-Wall", "-Wno-unused-variable", "-Wno-sign-compare",
+    cpp_flags = ["g++", "-std=c++17", "-fPIC", "-fvisibility=hidden", *host_opt, "-Wall", "-Wno-unused-variable", "-Wno-sign-compare",
                  *common_defs, "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C",
                  f"-I{CSRC}", *[f"-I{p}" for p in tincs], f"-I{ROCM / 'include'}", f"-I{py_inc}"]
 
@@ -84,7 +95,7 @@ def build(jobs: int = 4, force: bool = False, debug: bool = False, verbose: bool
 
     def compile_one(item):
         src, flags = item
-        obj = BUILD / (src.stem + (".hip.o" if src.suffix == ".hip" else ".o"))
+        obj = (BUILD if src.suffix == ".hip" else host_build) / (src.stem + (".hip.o" if src.suffix == ".hip" else ".o"))
         stamp = BUILD / (obj.name + ".stamp")
         key = _stamp(src, flags)
         if not force and obj.exists() and stamp.exists() and stamp.read_text() == key:
@@ -99,7 +110,8 @@ def build(jobs: int = 4, force: bool = False, debug: bool = False, verbose: bool
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         results = list(ex.map(compile_one, jobs_list))
     objs = [o for o, _ in results]
-    out = output_path()
+    out = output_path(asan)
+    out.parent.mkdir(parents=True, exist_ok=True)
     rebuilt = any(changed for _, changed in results)
     if rebuilt or force or not out.exists():
         tlib = tdir / "lib"
@@ -132,9 +144,10 @@ def main(argv=None) -> int:
     ap.add_argument("--jobs", type=int, default=int(os.environ.get("MAX_JOBS", "4")))
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="host code with AddressSanitizer -> build/asan/")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args(argv)
-    out = build(jobs=min(a.jobs, 16), force=a.force, debug=a.debug, verbose=a.verbose)
+    out = build(jobs=min(a.jobs, 16), force=a.force, debug=a.debug, verbose=a.verbose, asan=a.asan)
     print(f"built {out}")
     return 0
 

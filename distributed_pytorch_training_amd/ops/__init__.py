@@ -13,8 +13,25 @@ import torch
 
 from . import reference
 
-try:  # the in-tree extension, built by csrc/build.py
-    from .. import _C  # type: ignore[attr-defined]
+def _load():
+    """The in-tree extension built by csrc/build.py, or the file named by ``DPT_NATIVE_LIB``
+    (the AddressSanitizer build under build/asan/, CPU debug runs only)."""
+    import os
+    path = os.environ.get("DPT_NATIVE_LIB")
+    if not path:
+        from .. import _C as mod  # type: ignore[attr-defined]
+        return mod
+    import importlib.util
+    import sys
+    spec = importlib.util.spec_from_file_location("distributed_pytorch_training_amd._C", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    sys.modules["distributed_pytorch_training_amd._C"] = mod
+    return mod
+
+
+try:
+    _C = _load()
     _IMPORT_ERROR: Optional[BaseException] = None
 except Exception as e:  # pragma: no cover - depends on the build
     _C = None

@@ -165,7 +165,7 @@ def test_pair_outputs_sum_gradients(cuda, use):
     torch.testing.assert_close(bn.bias.grad, b.grad, rtol=2e-2, atol=0.5)
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("shape,k,s,p", [((8, 64, 112, 112), 3, 2, 1), ((2, 16, 9, 7), 3, 2, 1),
                                          ((2, 16, 10, 11), 3, 2, 1), ((3, 8, 5, 6), 3, 2, 1), ((1, 8, 1, 2), 3, 2, 1),
                                          ((2, 8, 8, 8), 2, 2, 0), ((3, 24, 10, 10), 3, 1, 1)])
@@ -184,6 +184,39 @@ def test_maxpool_matches_torch(cuda, dtype, shape, k, s, p):
     yb.backward(g)
     rt, at = TOL[dtype]
     torch.testing.assert_close(xa.grad.float(), xb.grad.float(), rtol=rt, atol=at)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("k,s,p", [(3, 2, 1), (3, 1, 1)])
+def test_maxpool_nan_and_neg_inf(cuda, dtype, k, s, p):
+    """NaN propagates (torch's max_pool2d returns NaN for a window holding one, and routes the
+    gradient to it); -inf only wins an all--inf window.  Planted at the first tap of padded
+    windows (row/col 0), mid-image, and in a window whose other taps are -inf.  Reference: torch's
+    NCHW kernel (the reference's layout): an all--inf window routes its gradient to the first
+    in-image tap there (torch's NHWC kernel sends it to flat index 0 of the image instead)."""
+    from distributed_pytorch_training_amd.ops.pool import max_pool2d_nhwc
+
+    x = _mk((2, 16, 11, 10), dtype, cuda, 51)
+    x[0, 0, 0, 0] = float("nan")            # first tap of the top-left (padded) window
+    x[0, 3, 5, 4] = float("nan")            # interior
+    x[1, 2, 0, 3] = float("nan")            # top border
+    x[1, 5, 4:7, 4:7] = float("-inf")       # a whole 3x3 block of -inf ...
+    x[1, 6, 4:7, 4:7] = float("-inf")
+    x[1, 6, 5, 5] = float("nan")            # ... with a NaN in the middle
+    x[0, 7, :, :] = float("-inf")           # an all--inf channel
+    x = x.contiguous(memory_format=torch.channels_last)
+    xa = x.detach().clone().requires_grad_()
+    xb = x.detach().contiguous().requires_grad_()          # NCHW
+    ya = max_pool2d_nhwc(xa, k, s, p)
+    yb = torch.nn.functional.max_pool2d(xb, k, s, p)
+    assert torch.equal(torch.isnan(ya), torch.isnan(yb))
+    m = ~torch.isnan(yb)
+    assert torch.equal(ya[m], yb[m])
+    g = _mk(tuple(ya.shape), dtype, cuda, 52)
+    ya.backward(g)
+    yb.backward(g)
+    rt, at = TOL[dtype]
+    torch.testing.assert_close(xa.grad.float(), xb.grad.float(), rtol=rt, atol=at, equal_nan=True)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])

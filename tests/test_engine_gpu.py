@@ -268,3 +268,25 @@ def test_weight_shadow_matches_autocast_casts(cuda, model_name, opt):
             p.add_(1.0)
     sh.sync_weights()
     assert torch.equal(sh.ddp.shadow_flat, sh.ddp.arena.param_flat.to(torch.bfloat16))
+
+
+def test_validation_lines_identical_across_engines_under_amp(cuda):
+    """Validation is fp32 in the reference even with --amp (train_ddp.py:266-283): the native
+    engine (fused layers, weight shadows) and the stock torch engine print the same Val
+    loss/acc for the same weights, and the native number does not change with --amp."""
+    from distributed_pytorch_training_amd.data import SyntheticLoader
+    from distributed_pytorch_training_amd.engine.trainer import format_epoch_line
+
+    torch.manual_seed(0)
+    base = build_model("resnet50", 100, cuda, image_size=64, channels_last=True)
+    loader = SyntheticLoader(256, 64, 64, 100, cuda, channels_last=True, seed=9)
+    common = ["--model", "resnet50", "--dataset", "synthetic", "--image-size", "64", "--num-classes", "100",
+              "--channels-last"]
+    lines = {}
+    for name, extra in [("native_amp", ["--amp", "--amp-dtype", "bf16"]),
+                        ("torch_amp", ["--amp", "--amp-dtype", "bf16", "--impl", "torch"]),
+                        ("native_fp32", [])]:
+        tr = Trainer(copy.deepcopy(base), parse_args(common + extra), 0, 1, cuda, log=lambda s: None)
+        vs = tr.validate(loader)
+        lines[name] = format_epoch_line(0, 1, 0.0, 0.0, vs.loss, vs.acc, 0.0).split("|")[1]
+    assert lines["native_amp"] == lines["torch_amp"] == lines["native_fp32"], lines
