@@ -234,6 +234,17 @@ void check_cl_bf16(const Tensor& t, const char* name) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
 }
 bool is_f16(const Tensor& t) { return t.scalar_type() == at::kHalf; }
+
+// split-K scratch for a conv with a small tile grid (undefined when it runs unsplit)
+Tensor splitk_ws(const Tensor& like, int64_t M, int Cout, int64_t K) {
+  const int splits = dpt::conv_fwd_splits(M, Cout, K, nullptr, cur_stream(like));
+  if (splits <= 1) return Tensor();
+  return at::empty({(int64_t)splits * M * Cout}, like.options().dtype(at::kFloat));
+}
+// columns of a conv's BN partials: one per 128-row tile, or per 16-row slab when split-K runs
+int64_t partial_cols(const Tensor& ws, int64_t M) {
+  return ws.defined() ? dpt::conv_split_cols(M) : dpt::conv_m_tiles(M);
+}
 void same_16(const Tensor& a, const Tensor& b, const char* op) {
   TORCH_CHECK(a.scalar_type() == b.scalar_type(), op, ": operands must share one 16-bit dtype (bf16 or fp16)");
 }
@@ -256,17 +267,18 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bo
   const int Ho = out_h > 0 ? out_h : Hs, Wo = out_w > 0 ? out_w : Ws;
   TORCH_CHECK(Ho > 0 && Wo > 0 && Ho <= Hs && Wo <= Ws, "conv_fwd: bad output size");
   auto y = at::empty({N, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(x.device().index());
+  Tensor ws = splitk_ws(x, (int64_t)N * Ho * Wo, Cout, (int64_t)R * S * C);
   Tensor ps, pq;
   if (want_stats) {
-    const int mt = dpt::conv_m_tiles((int64_t)N * Ho * Wo);
+    const int64_t mt = partial_cols(ws, (int64_t)N * Ho * Wo);
     ps = at::empty({Cout, mt}, x.options().dtype(at::kFloat));
     pq = at::empty({Cout, mt}, x.options().dtype(at::kFloat));
   }
-  c10::hip::HIPGuard guard(x.device().index());
   dpt::launch_conv_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()), N, H, W, C, Cout, R, S, (int)stride, (int)pad,
                        want_stats ? ps.data_ptr<float>() : nullptr, want_stats ? pq.data_ptr<float>() : nullptr,
-                       cur_stream(x), Ho, Wo, is_f16(x));
+                       cur_stream(x), Ho, Wo, is_f16(x), ws.defined() ? ws.data_ptr<float>() : nullptr);
   return {y, ps, pq};
 }
 
@@ -333,7 +345,9 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
   }
   auto wt = pre ? *w_flipped : at::empty({C, Cout, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int mt = dpt::conv_m_tiles((int64_t)N * H * W);
+  c10::hip::HIPGuard guard(dy.device().index());
+  Tensor ws = splitk_ws(dy, (int64_t)N * H * W, C, (int64_t)R * S * Cout);
+  const int64_t mt = partial_cols(ws, (int64_t)N * H * W);
   auto p1 = at::empty({C, mt}, dy.options().dtype(at::kFloat));
   auto p2 = at::empty({C, mt}, dy.options().dtype(at::kFloat));
   const bool two = bn_x2.has_value() && bn_x2->defined();
@@ -344,7 +358,6 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
     TORCH_CHECK(bn_x2->sizes() == bn_x.sizes(), "conv_dgrad_bnstats: bn_x2 must match bn_x");
   }
   auto p3 = at::empty({two ? C : 0, two ? mt : 0}, dy.options().dtype(at::kFloat));
-  c10::hip::HIPGuard guard(dy.device().index());
   auto st = cur_stream(dy);
   if (!pre)
     dpt::launch_conv_wt_flip(reinterpret_cast<const uint16_t*>(w.data_ptr()), reinterpret_cast<uint16_t*>(wt.data_ptr()),
@@ -358,7 +371,8 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
                                  res ? reinterpret_cast<const uint16_t*>(bn_res->data_ptr()) : nullptr,
                                  two ? reinterpret_cast<const uint16_t*>(bn_x2->data_ptr()) : nullptr,
                                  two ? f32_param(bn_mean2, C, "bn_mean2") : nullptr,
-                                 two ? p3.data_ptr<float>() : nullptr, is_f16(dy));
+                                 two ? p3.data_ptr<float>() : nullptr, is_f16(dy),
+                                 ws.defined() ? ws.data_ptr<float>() : nullptr);
   return {dx, p1, p2, p3};
 }
 
@@ -436,9 +450,10 @@ Tensor conv_dgrad_preflipped(Tensor dy, Tensor wt, int64_t pad) {
   auto dx = at::empty({N, C, Ho + R - 1 - 2 * (int)pad, Wo + S - 1 - 2 * (int)pad},
                       dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   c10::hip::HIPGuard guard(dy.device().index());
+  Tensor ws = splitk_ws(dy, dx.size(0) * dx.size(2) * dx.size(3), C, (int64_t)R * S * Cout);
   dpt::launch_conv_fwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                        reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, 1, (int)(R - 1 - pad),
-                       nullptr, nullptr, cur_stream(dy), 0, 0, is_f16(dy));
+                       nullptr, nullptr, cur_stream(dy), 0, 0, is_f16(dy), ws.defined() ? ws.data_ptr<float>() : nullptr);
   return dx;
 }
 
@@ -458,10 +473,12 @@ std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad) {
   dpt::launch_conv_wt_flip(reinterpret_cast<const uint16_t*>(w.data_ptr()), reinterpret_cast<uint16_t*>(wt.data_ptr()),
                            Cout, R, S, C, st);
   const int N = dy.size(0), Ho = dy.size(2), Wo = dy.size(3);
-  auto dx = at::empty({N, C, Ho, Wo}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto dx = at::empty({N, C, Ho + R - 1 - 2 * (int)pad, Wo + S - 1 - 2 * (int)pad},
+                      dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor ws = splitk_ws(dy, dx.size(0) * dx.size(2) * dx.size(3), C, (int64_t)R * S * Cout);
   dpt::launch_conv_fwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                        reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, 1, (int)(R - 1 - pad),
-                       nullptr, nullptr, st, 0, 0, is_f16(dy));
+                       nullptr, nullptr, st, 0, 0, is_f16(dy), ws.defined() ? ws.data_ptr<float>() : nullptr);
   return {dx, wt};
 }
 
@@ -1045,6 +1062,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("grad_output"), py::arg("lse"),
         py::arg("heads"), py::arg("scale"));
   m.def("conv_set_variant", &dpt::conv_set_variant, py::arg("variant"));
+  m.def("conv_fwd_splits", [](int64_t M, int Cout, int64_t K, bool graph) {
+          return dpt::conv_fwd_splits_for(M, Cout, K, graph);
+        }, py::arg("M"), py::arg("Cout"), py::arg("K"), py::arg("graph") = false);
+  m.def("conv_set_splitk", &dpt::conv_set_splitk, py::arg("on"));
   m.def("conv_dgrad", &conv_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("conv_dgrad_bnstats", &conv_dgrad_bnstats, py::arg("grad_output"), py::arg("w"), py::arg("pad"),
         py::arg("bn_x"), py::arg("bn_mean"), py::arg("bn_coef"), py::arg("bn_y") = py::none(),

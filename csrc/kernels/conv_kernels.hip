@@ -114,6 +114,11 @@ struct ConvFwdArgs {
   // parity classes write consecutive column ranges of one array)
   int bp_ld, bp_off;
   int f16;  // fp16 element type (bf16 otherwise)
+  // split-K (small grids): block (tile, split) reduces K-steps [split*kps, +kps) into an fp32
+  // partial tile of part [splits][M][Cout]; conv_split_epilogue_kernel sums the splits and runs
+  // the epilogue (16-bit rounding, BN statistics, BNB/BNR) the unsplit kernel would have run
+  float* part;
+  int splits, kps;
 };
 
 // K-major operands (rows of the LDS image = k) use the transposing reads and the swizzle of
@@ -149,17 +154,24 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 // cell (1x1 / stride-2 backward-data, whose other classes receive no gradient).
 // BNR2 (with BNR): the downsample-branch statistic s3 too (p.bnx2 / bn_mean2 / bp3).
 // F16: fp16 operands and outputs (bf16 otherwise).
+// NT: threads per block - 256 (4 waves, 2 blocks per CU) or 512 (8 waves, 2 per SIMD, one
+// 256-row block per CU: twice the MFMA work per staged byte, the large-tile regime of
+// cdna_hip_programming.md §5 where the 2-stage glds pipeline is MFMA-bound rather than
+// L2-bound).
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
-          bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, bool F16 = false>
-__global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs p) {
+          bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, bool F16 = false,
+          int NT = conv::kThreads, bool SPLIT = false>
+__global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
   constexpr int BM = BMT;
+  constexpr int NW = NT / 64;         // waves
   constexpr int WN = BN / 64;         // waves along N (each wave owns 64 output channels)
-  constexpr int WM = 4 / WN;          // waves along M
+  constexpr int WM = NW / WN;         // waves along M
   constexpr int MI = BM / (WM * 32);  // 32-row MFMA tiles per wave
   constexpr int NI = 2;               // 32-col MFMA tiles per wave
-  constexpr int A_PER_T = BM * 8 / kThreads;  // glds instructions per wave per K-step (A)
-  constexpr int B_PER_T = BN * 8 / kThreads;  // (B)
+  static_assert(WM * WN == NW && MI >= 1 && MI * WM * 32 == BM, "conv_fwd_kernel: bad wave tiling");
+  constexpr int A_PER_T = BM * 8 / NT;  // glds instructions per wave per K-step (A)
+  constexpr int B_PER_T = BN * 8 / NT;  // (B)
   constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int C_STRIDE = BN * 2 + 16;  // epilogue image row stride (bytes), padded
@@ -171,8 +183,12 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int nwg = (BM == 256 ? p.mt256 : p.m_tiles) * p.n_tiles;
-  const int bid = conv::xcd_remap(blockIdx.x, nwg);
+  const int tiles = (BM == 256 ? p.mt256 : p.m_tiles) * p.n_tiles;
+  const int nsplit = SPLIT ? p.splits : 1;
+  const int bid0 = conv::xcd_remap(blockIdx.x, tiles * nsplit);
+  // split-K: the splits of one tile are consecutive ids (one XCD, shared A/B rows in its L2)
+  const int sp = SPLIT ? bid0 % nsplit : 0;
+  const int bid = SPLIT ? bid0 / nsplit : bid0;
   const int mt = bid / p.n_tiles, nt = bid % p.n_tiles;
   const int64_t m0 = (int64_t)mt * BM;
   const int n0 = nt * BN;
@@ -226,7 +242,9 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
 
   const int cblocks = p.C >= BK ? p.C / BK : 1;
   const int tps = p.C >= BK ? 1 : BK / p.C;  // taps per K-step (narrow inputs)
-  const int nk = (int)(Kg / BK);
+  const int nk_all = (int)(Kg / BK);
+  const int ks0 = SPLIT ? sp * p.kps : 0;
+  const int ks1 = SPLIT ? min(nk_all, ks0 + p.kps) : nk_all;
 
   // global -> LDS directly (no staging registers); wave-uniform LDS base per 1 KiB.
   auto stage = [&](int ks, int buf) {
@@ -292,24 +310,41 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
   };
 
   if (STAGES == 2) {
-    stage(0, 0);
+    stage(ks0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int ks = 0; ks < nk; ++ks) {
-      const int cur = ks & 1;
-      if (ks + 1 < nk) stage(ks + 1, cur ^ 1);
+    for (int ks = ks0; ks < ks1; ++ks) {
+      const int cur = (ks - ks0) & 1;
+      if (ks + 1 < ks1) stage(ks + 1, cur ^ 1);
       mma(cur);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
   } else {
-    for (int ks = 0; ks < nk; ++ks) {
+    for (int ks = ks0; ks < ks1; ++ks) {
       stage(ks, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       mma(0);
       __syncthreads();
     }
+  }
+  if constexpr (SPLIT) {
+    // fp32 partial tile straight from the accumulators: 32 lanes = 32 consecutive channels
+    const int lr2 = lane & 31, lh2 = lane >> 5;
+    float* out = p.part + (int64_t)sp * p.M * p.Cout;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = n0 + wn * 64 + j * 32 + lr2;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int64_t m = m0 + wm * (MI * 32) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh2;
+          if (m < p.M) out[m * p.Cout + col] = acc[i][j][e];
+        }
+      }
+    return;
   }
 
   // ---- epilogue: 16-bit rounding, BN partial sums, stores ----
@@ -379,7 +414,7 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
   }
   if (LDSEPI) {
     constexpr int CPR = BN / 8;          // 16-byte chunks per output row
-    constexpr int RPP = kThreads / CPR;  // rows per pass
+    constexpr int RPP = NT / CPR;  // rows per pass
     constexpr int NPASS = BM / RPP;
     // global operands of the BN epilogues are loaded a group of passes at a time, before any
     // store of the group (the output may alias nothing, but the compiler cannot know that)
@@ -491,7 +526,7 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
     }
     if (BNB) {
       // threads sharing a channel group: orow = tid / CPR -> lanes l, l+CPR, ... of a wave, then
-      // the 4 waves through LDS (the epilogue image is no longer read: reuse its space)
+      // the NW waves through LDS (the epilogue image is no longer read: reuse its space)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
 #pragma unroll
@@ -503,7 +538,7 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
       }
       __syncthreads();
       constexpr int NS3 = two ? 3 : 2;
-      float* bred = reinterpret_cast<float*>(lds);  // [4 waves][NS3][BN]
+      float* bred = reinterpret_cast<float*>(lds);  // [NW waves][NS3][BN]
       if (lane < CPR) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -516,7 +551,7 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
       if (tid < BN) {
         float a = 0.f, b = 0.f, c3 = 0.f;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
+        for (int w = 0; w < NW; ++w) {
           a += bred[(w * NS3) * BN + tid];
           b += bred[(w * NS3 + 1) * BN + tid];
           if (two) c3 += bred[(w * NS3 + 2) * BN + tid];
@@ -526,6 +561,130 @@ __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_kernel(ConvFwdArgs
         p.bp2[pc] = b;
         if (two) p.bp3[pc] = c3;
       }
+    }
+  }
+}
+
+// ---- split-K epilogue: sum the fp32 partial tiles, then the conv epilogue --------------------
+// One block per (16-row slab, 64-channel group), 256 threads = 8 channel groups x 16 rows x 2
+// split halves (each half sums every other split; LDS joins them) - small-grid convs have few
+// rows, so the slab is kept short to spread the split sums over many blocks.  Identical
+// per-element math to conv_fwd_kernel's LDS epilogue (16-bit rounding of the sum, BN
+// statistics from the rounded values; BNB: s1 = sum dz, s2 = sum dz*(x - mean) with the BN+ReLU
+// mask; BNR: dz = (g + res) * (y > 0) is what is stored; BNR2: s3 = sum dz*(x2 - mean2)).
+// Statistics partials: one column per 16-row slab, [C][ceil(M/16)] (conv_split_cols).
+constexpr int kSplitRows = 16;
+template <bool STATS, bool BNB, bool BNR, bool BNR2, bool F16>
+__global__ __launch_bounds__(256) void conv_split_epilogue_kernel(ConvFwdArgs p) {
+  const int rb = blockIdx.x, cgb = blockIdx.y, cols = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int oc = tid & 7, orow = (tid >> 3) & 15, half = tid >> 7;
+  const int c0 = cgb * 64 + oc * 8;
+  const int64_t MC = p.M * p.Cout;
+  const int64_t m = (int64_t)rb * kSplitRows + orow;
+  const bool live = m < p.M;
+  const int64_t off = (live ? m : 0) * p.Cout + c0;
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = 0.f;
+  if (live) {
+    for (int sp = half; sp < p.splits; sp += 2) {
+      const float4* q = reinterpret_cast<const float4*>(p.part + sp * MC + off);
+      const float4 a = q[0], b = q[1];
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+  }
+  __shared__ float join[128][9];
+  __shared__ float red[2][3][64];
+  if (half == 1) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) join[tid & 127][k] = v[k];
+  }
+  __syncthreads();
+  constexpr bool two = BNR && BNR2;
+  float q0[8], q1[8], q2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) q0[k] = q1[k] = q2[k] = 0.f;
+  if (half == 0 && live) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += join[tid][k];
+    uint32_t u[4];
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) u[k2] = cpack<F16>(f32x2_t{v[2 * k2], v[2 * k2 + 1]});
+    if (BNB) {
+      const uint4 xv = *reinterpret_cast<const uint4*>(p.bnx + off);
+      uint4 yv = make_uint4(0u, 0u, 0u, 0u), rv = yv, x2v = yv;
+      if (BNR) {
+        yv = *reinterpret_cast<const uint4*>(p.bny + off);
+        rv = *reinterpret_cast<const uint4*>(p.bnres + off);
+        if (two) x2v = *reinterpret_cast<const uint4*>(p.bnx2 + off);
+      }
+      const uint32_t xu[4] = {xv.x, xv.y, xv.z, xv.w}, yu[4] = {yv.x, yv.y, yv.z, yv.w};
+      const uint32_t ru[4] = {rv.x, rv.y, rv.z, rv.w}, x2u[4] = {x2v.x, x2v.y, x2v.z, x2v.w};
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) {
+        float dzp[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int k = 2 * k2 + h, c = c0 + k;
+          const float g = cunpack<F16>(u[k2], h);
+          const float x = cunpack<F16>(xu[k2], h);
+          float dz;
+          if (BNR) {
+            dz = cunpack<F16>(yu[k2], h) > 0.0f ? g + cunpack<F16>(ru[k2], h) : 0.0f;
+          } else {
+            dz = __builtin_fmaf(x, p.bn_coef[c], p.bn_coef[p.Cout + c]) > 0.0f ? g : 0.0f;
+          }
+          dzp[h] = dz;
+          q0[k] = dz;
+          q1[k] = dz * (x - p.bn_mean[c]);
+          if (two) q2[k] = dz * (cunpack<F16>(x2u[k2], h) - p.bn_mean2[c]);
+        }
+        if (BNR) u[k2] = cpack<F16>(f32x2_t{dzp[0], dzp[1]});
+      }
+    }
+    if (STATS) {
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float f = cunpack<F16>(u[k2], h);
+          q0[2 * k2 + h] = f;
+          q1[2 * k2 + h] = f * f;
+        }
+    }
+    *reinterpret_cast<uint4*>(p.y + off) = make_uint4(u[0], u[1], u[2], u[3]);
+  }
+  if (!STATS && !BNB) return;
+  // the 16 rows of a channel group: lanes l, l+8, ..., l+56 of waves 0 and 1
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+      q0[k] += __shfl_xor(q0[k], o, 64);
+      q1[k] += __shfl_xor(q1[k], o, 64);
+      if (two) q2[k] += __shfl_xor(q2[k], o, 64);
+    }
+  }
+  if (wid < 2 && lane < 8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[wid][0][oc * 8 + k] = q0[k];
+      red[wid][1][oc * 8 + k] = q1[k];
+      if (two) red[wid][2][oc * 8 + k] = q2[k];
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const float a = red[0][0][tid] + red[1][0][tid], b = red[0][1][tid] + red[1][1][tid];
+    const int64_t pc = ((int64_t)cgb * 64 + tid) * cols + rb;
+    if (STATS) {
+      p.psum[pc] = a;
+      p.psq[pc] = b;
+    } else {
+      p.bp1[pc] = a;
+      p.bp2[pc] = b;
+      if (two) p.bp3[pc] = red[0][2][tid] + red[1][2][tid];
     }
   }
 }
@@ -1125,6 +1284,7 @@ bool conv_supported_narrow(int C, int Cout, int S) {
 }
 
 int conv_m_tiles(int64_t M) { return (int)((M + conv::BM - 1) / conv::BM); }
+int conv_split_cols(int64_t M) { return (int)((M + 15) / 16); }
 
 // Kernel variant: 0 = default (1-stage + LDS epilogue), 5/6 = 256-row blocks (register / LDS
 // epilogue), 1 = 2-stage + LDS epilogue, 2 = 2-stage +
@@ -1145,9 +1305,10 @@ void conv_set_variant(int v) { g_conv_variant = v; }
 // Launch one conv_fwd_kernel instantiation in the element type of a.f16 (fp16 is instantiated
 // for the production 128-row, 1-stage, LDS-epilogue variants only).
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
-          bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false>
-static void fwd_launch(dim3 grid, dim3 block, hipStream_t s, const ConvFwdArgs& a) {
-  if constexpr (BMT == 128 && STAGES == 1 && LDSEPI) {
+          bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, int NT = conv::kThreads>
+static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdArgs& a) {
+  const dim3 block(NT);
+  if constexpr (BMT == 128 && STAGES == 1 && LDSEPI && NT == conv::kThreads) {
     if (a.f16) {
       hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, STAGES, LDSEPI, BKN, STATS, BNB, BNR, REMAP, ZSIB, BNR2, true>),
                          grid, block, 0, s, a);
@@ -1156,8 +1317,89 @@ static void fwd_launch(dim3 grid, dim3 block, hipStream_t s, const ConvFwdArgs& 
   } else {
     if (a.f16) throw std::runtime_error("conv: fp16 runs the default kernel variant only");
   }
-  hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, STAGES, LDSEPI, BKN, STATS, BNB, BNR, REMAP, ZSIB, BNR2, false>), grid,
-                     block, 0, s, a);
+  hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, STAGES, LDSEPI, BKN, STATS, BNB, BNR, REMAP, ZSIB, BNR2, false, NT>),
+                     grid, block, 0, s, a);
+}
+
+// ---- split-K for small grids ------------------------------------------------------------------
+// A conv whose 128 x BN tile grid is far below one block per CU (ResNet-18 on 32x32 images:
+// layer4 is 4 tiles at batch 128, each a 72-step K loop) is latency-bound on the K loop: split
+// the K-steps over blocks (fp32 partials, summed by conv_split_epilogue_kernel).  Target ~2
+// blocks per CU, at least 2 K-steps per split.  DPT_CONV_SPLITK=0 disables it (A/B).
+static int g_splitk = -1;
+static bool splitk_enabled() {
+  if (g_splitk < 0) {
+    const char* e = std::getenv("DPT_CONV_SPLITK");
+    g_splitk = (e == nullptr || std::atoi(e) != 0) ? 1 : 0;
+  }
+  return g_splitk == 1;
+}
+void conv_set_splitk(bool on) { g_splitk = on ? 1 : 0; }
+
+int conv_fwd_splits(int64_t M, int Cout, int64_t K, int* kps_out, hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  const bool capturing = s != nullptr && hipStreamIsCapturing(s, &cs) == hipSuccess &&
+                         cs == hipStreamCaptureStatusActive;
+  return conv_fwd_splits_for(M, Cout, K, capturing, kps_out);
+}
+
+int conv_fwd_splits_for(int64_t M, int Cout, int64_t K, bool graph, int* kps_out) {
+  const int n_tiles = Cout % 128 == 0 ? Cout / 128 : Cout / 64;
+  const int64_t tiles = (int64_t)conv_m_tiles(M) * n_tiles;
+  const int nk = (int)(K / conv::BK);
+  if (kps_out) *kps_out = nk;
+  if (!splitk_enabled() || tiles >= 160 || nk < 4) return 1;
+  // Eager launches are host-bound at these sizes: the extra epilogue launch only pays where the
+  // single-block K loop is long (tens of microseconds); inside a hipGraph capture it always does.
+  if (!graph && (tiles > 32 || nk < 24)) return 1;
+  const int want = (int)((512 + tiles - 1) / tiles);
+  const int kps = std::max(2, (nk + want - 1) / want);
+  const int splits = (nk + kps - 1) / kps;
+  if (splits <= 1) return 1;
+  if (kps_out) *kps_out = kps;
+  return splits;
+}
+
+template <int BN, bool STATS, bool BNB, bool BNR, bool BNR2>
+static void split_launch(const ConvFwdArgs& a, hipStream_t s) {
+  const dim3 grid((unsigned)(a.m_tiles * a.n_tiles * a.splits)), block(conv::kThreads);
+  // the main loop's epilogue flags do not matter (SPLIT returns before it): one instantiation
+  if (a.f16)
+    hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, false, false, false, false, false, false, false, true,
+                                        conv::kThreads, true>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, false, false, false, false, false, false, false, false,
+                                        conv::kThreads, true>), grid, block, 0, s, a);
+  const dim3 egrid((unsigned)((a.M + kSplitRows - 1) / kSplitRows), (unsigned)(a.Cout / 64));
+  if (a.f16)
+    hipLaunchKernelGGL((conv_split_epilogue_kernel<STATS, BNB, BNR, BNR2, true>), egrid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_split_epilogue_kernel<STATS, BNB, BNR, BNR2, false>), egrid, dim3(256), 0, s, a);
+}
+
+// Launch the split-K path when the plan asks for it and a workspace was provided.
+static bool maybe_split(ConvFwdArgs& a, float* ws, bool stats, bool bnb, bool bnr, bool bnr2, hipStream_t s) {
+  if (ws == nullptr) return false;
+  int kps = 0;
+  const int splits = conv_fwd_splits(a.M, a.Cout, (int64_t)a.R * a.S * a.C, &kps, s);
+  if (splits <= 1) return false;
+  a.part = ws;
+  a.splits = splits;
+  a.kps = kps;
+  a.n_tiles = a.Cout % 128 == 0 ? a.Cout / 128 : a.Cout / 64;
+  const bool wide = a.Cout % 128 == 0;
+#define DPT_SPLIT(S_, B_, R_, R2_)                                                   \
+  do {                                                                              \
+    if (wide) split_launch<128, S_, B_, R_, R2_>(a, s);                             \
+    else split_launch<64, S_, B_, R_, R2_>(a, s);                                   \
+  } while (0)
+  if (stats) DPT_SPLIT(true, false, false, false);
+  else if (bnb && bnr && bnr2) DPT_SPLIT(false, true, true, true);
+  else if (bnb && bnr) DPT_SPLIT(false, true, true, false);
+  else if (bnb) DPT_SPLIT(false, true, false, false);
+  else DPT_SPLIT(false, false, false, false);
+#undef DPT_SPLIT
+  return true;
 }
 
 template <int BMW, int BNW, int STAGES>
@@ -1215,10 +1457,34 @@ static void conv_fwd_dispatch(int variant, bool bkn, ConvFwdArgs a, hipStream_t 
   }
 }
 
+// 8-wave (512-thread), 2-stage variants: 9 = 256x256 tile, 10 = 256x128, 11 = 128x256.
+// Returns false when the shape does not fit the variant's N tile.
+static bool conv_fwd_big(int v, ConvFwdArgs& a, hipStream_t s) {
+  const int bn = v == 10 ? 128 : 256, bm = v == 11 ? 128 : 256;
+  if (a.Cout % bn) return false;
+  a.n_tiles = a.Cout / bn;
+  a.mt256 = (int)((a.M + 255) / 256);
+  const int mt = bm == 256 ? a.mt256 : a.m_tiles;
+  const dim3 grid((unsigned)(mt * a.n_tiles)), block(512);
+  const bool st = a.psum != nullptr;
+  if (v == 9) {
+    if (st) fwd_launch<256, 256, 2, true, false, true, false, false, false, false, false, 512>(grid, block, s, a);
+    else fwd_launch<256, 256, 2, true, false, false, false, false, false, false, false, 512>(grid, block, s, a);
+  } else if (v == 10) {
+    if (st) fwd_launch<256, 128, 2, true, false, true, false, false, false, false, false, 512>(grid, block, s, a);
+    else fwd_launch<256, 128, 2, true, false, false, false, false, false, false, false, 512>(grid, block, s, a);
+  } else {
+    if (st) fwd_launch<128, 256, 2, true, false, true, false, false, false, false, false, 512>(grid, block, s, a);
+    else fwd_launch<128, 256, 2, true, false, false, false, false, false, false, false, 512>(grid, block, s, a);
+  }
+  return true;
+}
+
 static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
                           int R, int S, int stride, int pad, float* psum, float* psq, bool bkn, hipStream_t s,
-                          int Ho = 0, int Wo = 0, bool f16 = false) {
+                          int Ho = 0, int Wo = 0, bool f16 = false, float* ws = nullptr) {
   ConvFwdArgs a;
+  a.part = nullptr; a.splits = 1; a.kps = 0;
   a.f16 = f16 ? 1 : 0;
   a.x = x; a.w = w; a.y = y; a.psum = psum; a.psq = psq;
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S; a.stride = stride; a.pad = pad;
@@ -1231,8 +1497,11 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
   const bool wide = Cout % 128 == 0;
   a.n_tiles = Cout / (wide ? 128 : 64);
   a.mt256 = 0;
-  if (wide) conv_fwd_dispatch<128>(conv_variant(), bkn, a, s);
-  else conv_fwd_dispatch<64>(conv_variant(), bkn, a, s);
+  const int v = conv_variant();
+  if (!bkn && maybe_split(a, ws, psum != nullptr, false, false, false, s)) return;
+  if (!bkn && !a.f16 && v >= 9 && v <= 11 && conv_fwd_big(v, a, s)) return;
+  if (wide) conv_fwd_dispatch<128>(v, bkn, a, s);
+  else conv_fwd_dispatch<64>(v, bkn, a, s);
 }
 
 // Stride-1 backward-data through a flipped/transposed weight wt [C][R][S][Cout] (the forward
@@ -1242,8 +1511,9 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
                                int C, int R, int S, int pad, const uint16_t* bnx, const float* bn_mean,
                                const float* bn_coef, float* bp1, float* bp2, hipStream_t s,
                                const uint16_t* bny, const uint16_t* bnres, const uint16_t* bnx2,
-                               const float* bn_mean2, float* bp3, bool f16) {
+                               const float* bn_mean2, float* bp3, bool f16, float* ws) {
   ConvFwdArgs a;
+  a.part = nullptr; a.splits = 1; a.kps = 0;
   a.f16 = f16 ? 1 : 0;
   a.x = dy; a.w = wt; a.y = dx; a.psum = nullptr; a.psq = nullptr;
   a.N = N; a.H = Ho; a.W = Wo; a.C = Cout; a.Cout = C; a.R = R; a.S = S; a.stride = 1; a.pad = R - 1 - pad;
@@ -1258,6 +1528,7 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
   a.bp_ld = a.m_tiles; a.bp_off = 0;
   const bool res = bny != nullptr;
   const dim3 block(conv::kThreads);
+  if (maybe_split(a, ws, false, true, res, res && bnx2 != nullptr, s)) return;
   a.n_tiles = C % 128 == 0 ? C / 128 : C / 64;
   const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
   const bool two = res && bnx2 != nullptr;
@@ -1274,8 +1545,8 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
 
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
                      int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s, int Ho, int Wo,
-                     bool f16) {
-  conv_fwd_impl(x, w, y, N, H, W, C, Cout, R, S, stride, pad, psum, psq, false, s, Ho, Wo, f16);
+                     bool f16, float* ws) {
+  conv_fwd_impl(x, w, y, N, H, W, C, Cout, R, S, stride, pad, psum, psq, false, s, Ho, Wo, f16, ws);
 }
 
 // Stride-1 backward-data: dx[N,H,W,C] = conv(dy, flip(w)^T, pad' = R-1-pad) with the flip and
@@ -1324,6 +1595,7 @@ void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, i
       const int Ha = (H - ph + 1) / 2, Wa = (W - pw + 1) / 2;
       if (Ha <= 0 || Wa <= 0 || J[ph] == 0 || Js[pw] == 0) continue;
       ConvFwdArgs a;
+      a.part = nullptr; a.splits = 1; a.kps = 0;
       a.f16 = f16 ? 1 : 0;
       a.x = dy; a.w = w; a.y = dx; a.psum = nullptr; a.psq = nullptr;
       a.N = N; a.H = Ho; a.W = Wo; a.C = Cout; a.Cout = C; a.R = J[ph]; a.S = Js[pw]; a.stride = 1;

@@ -141,9 +141,17 @@ bool conv_supported_narrow(int C, int Cout, int S);  // C = 16/32 with S % (64/C
 int conv_m_tiles(int64_t M);
 void conv_set_variant(int v);
 // Ho/Wo > 0: explicit output size (padding applied on top/left only beyond what it needs)
+// ws: split-K workspace of conv_fwd_splits(M, Cout, R*S*C) * M * Cout floats when that is > 1
+// (nullptr: never split).  Small tile grids split the K loop over blocks (fp32 partials).
+// (s: the launch stream - inside a hipGraph capture small grids always split, eagerly only
+// the very latency-bound ones); split-K writes BN partials with conv_split_cols(M) columns
+int conv_fwd_splits(int64_t M, int Cout, int64_t K, int* kps = nullptr, hipStream_t s = nullptr);
+int conv_fwd_splits_for(int64_t M, int Cout, int64_t K, bool graph, int* kps = nullptr);
+int conv_split_cols(int64_t M);
+void conv_set_splitk(bool on);  // run-time switch (A/B tests); default on unless DPT_CONV_SPLITK=0
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
                      int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s, int Ho = 0,
-                     int Wo = 0, bool f16 = false);
+                     int Wo = 0, bool f16 = false, float* ws = nullptr);
 // f16: fp16 operands/outputs throughout (bf16 otherwise) - every conv launcher below takes it.
 // backward-weight: dw [Cout,R,S,C] (kind 0 f32 / 1 bf16 / 2 f16) = sum over pixels of dy x x-shifted;
 // part: plan.part_floats floats of split-K scratch.  C % 64 == 0, Cout % 64 == 0.
@@ -163,7 +171,7 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
                                const float* bn_coef, float* bp1, float* bp2, hipStream_t s,
                                const uint16_t* bny = nullptr, const uint16_t* bnres = nullptr,
                                const uint16_t* bnx2 = nullptr, const float* bn_mean2 = nullptr,
-                               float* bp3 = nullptr, bool f16 = false);
+                               float* bp3 = nullptr, bool f16 = false, float* ws = nullptr);
 // many weights flipped/transposed (wt[ci][R-1-r][S-1-s][co] = w[co][r][s][ci]) in one launch
 constexpr int kWtFlipMax = 64;
 struct WtFlipBatch {

@@ -513,3 +513,82 @@ def test_resnet50_fp16_native_step(cuda):
     e_nat = ((upd("nat") - u32).norm() / u32.norm()).item()
     e_mio = ((upd("mio") - u32).norm() / u32.norm()).item()
     assert e_nat <= 1.5 * e_mio + 0.02, (e_nat, e_mio)
+
+
+SPLIT_SHAPES = [
+    # N, C, H, W, Cout, k, pad: ResNet-18 / 32x32 layer3-4 shapes (4-16 tiles) and a partial tile
+    (128, 512, 1, 1, 512, 3, 1),
+    (128, 256, 2, 2, 256, 3, 1),
+    (3, 128, 5, 7, 192, 3, 1),
+    (128, 256, 2, 2, 512, 1, 0),
+]
+
+
+@pytest.mark.parametrize("shape", SPLIT_SHAPES)
+def test_splitk_conv_matches_unsplit(cuda, shape):
+    """Split-K (conv_fwd_splits > 1: small tile grids) vs the single-block K loop: forward with BN
+    statistics, stride-1 backward-data through a pre-flipped weight, and the BN+ReLU statistics
+    (BNB) / block-tail (BNR) backward-data epilogues run from the fp32 partial sums."""
+    N, C, H, W, Cout, k, p = shape
+    C_ = ops.native()
+    M = N * H * W
+    # eagerly only the long-K tiny grids split; under hipGraph capture every small grid does
+    assert C_.conv_fwd_splits(M, Cout, k * k * C, True) > 1
+    if C_.conv_fwd_splits(M, Cout, k * k * C) <= 1:
+        pytest.skip("this shape splits under hipGraph capture only (test_splitk_under_graph)")
+    x, w = _operands(cuda, N, C, H, W, Cout, k, seed=7)
+    gy = torch.randn(N, Cout, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    wt = C_.conv_wt_flip_multi([w])[0]
+    g = torch.Generator(device=cuda).manual_seed(8)
+    bnx = torch.randn(N, C, H, W, device=cuda, generator=g).to(torch.bfloat16).contiguous(memory_format=CL)
+    bny = torch.relu(torch.randn(N, C, H, W, device=cuda, generator=g)).to(torch.bfloat16).contiguous(memory_format=CL)
+    bnres = torch.randn(N, C, H, W, device=cuda, generator=g).to(torch.bfloat16).contiguous(memory_format=CL)
+    mean = torch.randn(C, device=cuda, generator=g) * 0.1
+    coef = torch.cat([torch.rand(C, device=cuda, generator=g) + 0.5, torch.randn(C, device=cuda, generator=g) * 0.1])
+    outs = []
+    for on in (True, False):
+        C_.conv_set_splitk(on)
+        y, ps, pq = C_.conv_fwd(x, w, 1, p, True)
+        dx = C_.conv_dgrad_preflipped(gy, wt, p)
+        d1, p1, p2, _ = C_.conv_dgrad_bnstats(gy, w, p, bnx, mean, coef, w_flipped=wt)
+        d2, q1, q2, _ = C_.conv_dgrad_bnstats(gy, w, p, bnx, mean, None, bny, bnres, wt)
+        outs.append([y, ps.sum(1), pq.sum(1), dx, d1, p1.sum(1), p2.sum(1), d2, q1.sum(1), q2.sum(1)])
+    C_.conv_set_splitk(True)
+    ref = F.conv2d(x.float(), w.float(), padding=p)
+    torch.testing.assert_close(outs[0][0].float(), ref, rtol=1e-2, atol=1e-2)
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * b.float().abs().max().item() + 1e-3)
+
+
+def test_splitk_under_graph_matches_eager(cuda):
+    """Inside a hipGraph capture every small grid splits (conv_fwd_splits(..., graph=True)): the
+    replayed forward + BN statistics + BNB backward-data equal the eager (unsplit) results."""
+    C_ = ops.native()
+    N, C, H, W, Cout, k, p = 128, 128, 4, 4, 128, 3, 1        # 16 tiles, 18 K-steps
+    assert C_.conv_fwd_splits(N * H * W, Cout, k * k * C) == 1
+    assert C_.conv_fwd_splits(N * H * W, Cout, k * k * C, True) > 1
+    x, w = _operands(cuda, N, C, H, W, Cout, k, seed=9)
+    gy = torch.randn(N, Cout, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    wt = C_.conv_wt_flip_multi([w])[0]
+    bnx = torch.randn(N, C, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    mean = torch.randn(C, device=cuda) * 0.1
+    coef = torch.cat([torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda) * 0.1])
+
+    def run():
+        y, ps, pq = C_.conv_fwd(x, w, 1, p, True)
+        d1, p1, p2, _ = C_.conv_dgrad_bnstats(gy, w, p, bnx, mean, coef, w_flipped=wt)
+        return [y, ps.sum(1), pq.sum(1), d1, p1.sum(1), p2.sum(1)]
+
+    eager = run()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        run()                                   # warm the allocator on the side stream
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = run()
+    g.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(out, eager):
+        torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * b.float().abs().max().item() + 1e-3)
