@@ -389,22 +389,25 @@ std::vector<Tensor> conv_dgrad_s2(Tensor dy, Tensor w, int64_t pad, int64_t H, i
   TORCH_CHECK((int64_t)N * H * W < (int64_t(1) << 31), "conv_dgrad_s2: too many pixels");
   auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   const bool bnb = bn_x.has_value() && bn_x->defined();
+  c10::hip::HIPGuard guard(dy.device().index());
+  const dpt::ConvS2Plan plan = dpt::conv_dgrad_s2_plan(N, (int)H, (int)W, C, Cout, R, S, (int)pad, cur_stream(dy));
+  Tensor ws;
+  if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, dy.options().dtype(at::kFloat));
   Tensor p1, p2;
   if (bnb) {
     check_cl_bf16(*bn_x, "bn_x");
     same_16(dy, *bn_x, "conv_dgrad_s2");
     TORCH_CHECK(bn_x->sizes() == dx.sizes(), "conv_dgrad_s2: bn_x must match the conv input");
-    const int chunks = dpt::conv_dgrad_s2_chunks(N, (int)H, (int)W, R, S, (int)pad);
-    p1 = at::empty({C, chunks}, dy.options().dtype(at::kFloat));
-    p2 = at::empty({C, chunks}, dy.options().dtype(at::kFloat));
+    p1 = at::empty({C, plan.chunks}, dy.options().dtype(at::kFloat));
+    p2 = at::empty({C, plan.chunks}, dy.options().dtype(at::kFloat));
   }
-  c10::hip::HIPGuard guard(dy.device().index());
   dpt::launch_conv_dgrad_s2(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
                             reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, (int)pad, (int)H, (int)W,
                             cur_stream(dy), bnb ? reinterpret_cast<const uint16_t*>(bn_x->data_ptr()) : nullptr,
                             bnb ? f32_param(bn_mean, C, "bn_mean") : nullptr,
                             bnb ? f32_param(bn_coef, 2 * C, "bn_coef") : nullptr,
-                            bnb ? p1.data_ptr<float>() : nullptr, bnb ? p2.data_ptr<float>() : nullptr, is_f16(dy));
+                            bnb ? p1.data_ptr<float>() : nullptr, bnb ? p2.data_ptr<float>() : nullptr, is_f16(dy),
+                            ws.defined() ? ws.data_ptr<float>() : nullptr);
   if (!bnb) return {dx};
   return {dx, p1, p2};
 }
@@ -1065,7 +1068,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd_splits", [](int64_t M, int Cout, int64_t K, bool graph) {
           return dpt::conv_fwd_splits_for(M, Cout, K, graph);
         }, py::arg("M"), py::arg("Cout"), py::arg("K"), py::arg("graph") = false);
-  m.def("conv_set_splitk", &dpt::conv_set_splitk, py::arg("on"));
+  m.def("conv_set_splitk", &dpt::conv_set_splitk, py::arg("mode"));
   m.def("conv_dgrad", &conv_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("conv_dgrad_bnstats", &conv_dgrad_bnstats, py::arg("grad_output"), py::arg("w"), py::arg("pad"),
         py::arg("bn_x"), py::arg("bn_mean"), py::arg("bn_coef"), py::arg("bn_y") = py::none(),

@@ -574,7 +574,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
 // mask; BNR: dz = (g + res) * (y > 0) is what is stored; BNR2: s3 = sum dz*(x2 - mean2)).
 // Statistics partials: one column per 16-row slab, [C][ceil(M/16)] (conv_split_cols).
 constexpr int kSplitRows = 16;
-template <bool STATS, bool BNB, bool BNR, bool BNR2, bool F16>
+template <bool STATS, bool BNB, bool BNR, bool BNR2, bool REMAP, bool ZSIB, bool F16>
 __global__ __launch_bounds__(256) void conv_split_epilogue_kernel(ConvFwdArgs p) {
   const int rb = blockIdx.x, cgb = blockIdx.y, cols = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -583,13 +583,24 @@ __global__ __launch_bounds__(256) void conv_split_epilogue_kernel(ConvFwdArgs p)
   const int64_t MC = p.M * p.Cout;
   const int64_t m = (int64_t)rb * kSplitRows + orow;
   const bool live = m < p.M;
-  const int64_t off = (live ? m : 0) * p.Cout + c0;
+  const int64_t poff = (live ? m : 0) * p.Cout + c0;  // partials: GEMM row
+  // destination row (REMAP: the GEMM row's pixel in one stride-2 parity class of dx)
+  int64_t grow = live ? m : 0;
+  int oy = 0, ox = 0;
+  if (REMAP) {
+    const int64_t hw = (int64_t)p.Ho * p.Wo, img = grow / hw, rem = grow - img * hw;
+    const int a = (int)(rem / p.Wo), b = (int)(rem - (int64_t)a * p.Wo);
+    oy = 2 * a + p.oph;
+    ox = 2 * b + p.opw;
+    grow = (img * p.oH + oy) * p.oW + ox;
+  }
+  const int64_t off = grow * p.Cout + c0;
   float v[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) v[k] = 0.f;
   if (live) {
     for (int sp = half; sp < p.splits; sp += 2) {
-      const float4* q = reinterpret_cast<const float4*>(p.part + sp * MC + off);
+      const float4* q = reinterpret_cast<const float4*>(p.part + sp * MC + poff);
       const float4 a = q[0], b = q[1];
       v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
     }
@@ -654,6 +665,15 @@ __global__ __launch_bounds__(256) void conv_split_epilogue_kernel(ConvFwdArgs p)
         }
     }
     *reinterpret_cast<uint4*>(p.y + off) = make_uint4(u[0], u[1], u[2], u[3]);
+    if (ZSIB) {  // the three other positions of the 2x2 cell get no gradient (1x1 / stride 2)
+      const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+      const int64_t rs = (int64_t)p.oW * p.Cout;
+      if (ox + 1 < p.oW) *reinterpret_cast<uint4*>(p.y + off + p.Cout) = z;
+      if (oy + 1 < p.oH) {
+        *reinterpret_cast<uint4*>(p.y + off + rs) = z;
+        if (ox + 1 < p.oW) *reinterpret_cast<uint4*>(p.y + off + rs + p.Cout) = z;
+      }
+    }
   }
   if (!STATS && !BNB) return;
   // the 16 rows of a channel group: lanes l, l+8, ..., l+56 of waves 0 and 1
@@ -677,11 +697,12 @@ __global__ __launch_bounds__(256) void conv_split_epilogue_kernel(ConvFwdArgs p)
   __syncthreads();
   if (tid < 64) {
     const float a = red[0][0][tid] + red[1][0][tid], b = red[0][1][tid] + red[1][1][tid];
-    const int64_t pc = ((int64_t)cgb * 64 + tid) * cols + rb;
+    const int64_t c = (int64_t)cgb * 64 + tid;
     if (STATS) {
-      p.psum[pc] = a;
-      p.psq[pc] = b;
+      p.psum[c * cols + rb] = a;
+      p.psq[c * cols + rb] = b;
     } else {
+      const int64_t pc = c * p.bp_ld + p.bp_off + rb;
       p.bp1[pc] = a;
       p.bp2[pc] = b;
       if (two) p.bp3[pc] = red[0][2][tid] + red[1][2][tid];
@@ -1326,15 +1347,17 @@ static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdAr
 // layer4 is 4 tiles at batch 128, each a 72-step K loop) is latency-bound on the K loop: split
 // the K-steps over blocks (fp32 partials, summed by conv_split_epilogue_kernel).  Target ~2
 // blocks per CU, at least 2 K-steps per split.  DPT_CONV_SPLITK=0 disables it (A/B).
+// 0 = never split, 1 = auto (the policy below), 2 = the in-graph policy everywhere (tests that
+// compare eager with replayed steps)
 static int g_splitk = -1;
-static bool splitk_enabled() {
+static int splitk_mode() {
   if (g_splitk < 0) {
     const char* e = std::getenv("DPT_CONV_SPLITK");
-    g_splitk = (e == nullptr || std::atoi(e) != 0) ? 1 : 0;
+    g_splitk = e == nullptr ? 1 : std::atoi(e);
   }
-  return g_splitk == 1;
+  return g_splitk;
 }
-void conv_set_splitk(bool on) { g_splitk = on ? 1 : 0; }
+void conv_set_splitk(int mode) { g_splitk = mode; }
 
 int conv_fwd_splits(int64_t M, int Cout, int64_t K, int* kps_out, hipStream_t s) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -1348,10 +1371,11 @@ int conv_fwd_splits_for(int64_t M, int Cout, int64_t K, bool graph, int* kps_out
   const int64_t tiles = (int64_t)conv_m_tiles(M) * n_tiles;
   const int nk = (int)(K / conv::BK);
   if (kps_out) *kps_out = nk;
-  if (!splitk_enabled() || tiles >= 160 || nk < 4) return 1;
+  const int mode = splitk_mode();
+  if (mode == 0 || tiles >= 160 || nk < 4) return 1;
   // Eager launches are host-bound at these sizes: the extra epilogue launch only pays where the
   // single-block K loop is long (tens of microseconds); inside a hipGraph capture it always does.
-  if (!graph && (tiles > 32 || nk < 24)) return 1;
+  if (!graph && mode == 1 && (tiles > 32 || nk < 24)) return 1;
   const int want = (int)((512 + tiles - 1) / tiles);
   const int kps = std::max(2, (nk + want - 1) / want);
   const int splits = (nk + kps - 1) / kps;
@@ -1360,25 +1384,29 @@ int conv_fwd_splits_for(int64_t M, int Cout, int64_t K, bool graph, int* kps_out
   return splits;
 }
 
-template <int BN, bool STATS, bool BNB, bool BNR, bool BNR2>
+template <int BN, bool STATS, bool BNB, bool BNR, bool BNR2, bool BKN = false, bool REMAP = false, bool ZSIB = false>
 static void split_launch(const ConvFwdArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)(a.m_tiles * a.n_tiles * a.splits)), block(conv::kThreads);
   // the main loop's epilogue flags do not matter (SPLIT returns before it): one instantiation
   if (a.f16)
-    hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, false, false, false, false, false, false, false, true,
+    hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, BKN, false, false, false, false, false, false, true,
                                         conv::kThreads, true>), grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, false, false, false, false, false, false, false, false,
+    hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, BKN, false, false, false, false, false, false, false,
                                         conv::kThreads, true>), grid, block, 0, s, a);
   const dim3 egrid((unsigned)((a.M + kSplitRows - 1) / kSplitRows), (unsigned)(a.Cout / 64));
   if (a.f16)
-    hipLaunchKernelGGL((conv_split_epilogue_kernel<STATS, BNB, BNR, BNR2, true>), egrid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_split_epilogue_kernel<STATS, BNB, BNR, BNR2, REMAP, ZSIB, true>), egrid, dim3(256), 0, s,
+                       a);
   else
-    hipLaunchKernelGGL((conv_split_epilogue_kernel<STATS, BNB, BNR, BNR2, false>), egrid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_split_epilogue_kernel<STATS, BNB, BNR, BNR2, REMAP, ZSIB, false>), egrid, dim3(256), 0, s,
+                       a);
 }
 
-// Launch the split-K path when the plan asks for it and a workspace was provided.
-static bool maybe_split(ConvFwdArgs& a, float* ws, bool stats, bool bnb, bool bnr, bool bnr2, hipStream_t s) {
+// Launch the split-K path when the plan asks for it and a workspace was provided.  BNB
+// statistics go to columns [bp_off, bp_off + ceil(M/16)) of the [C][bp_ld] partial arrays.
+static bool maybe_split(ConvFwdArgs& a, float* ws, bool stats, bool bnb, bool bnr, bool bnr2, hipStream_t s,
+                        bool bkn = false, bool remap = false, bool zsib = false) {
   if (ws == nullptr) return false;
   int kps = 0;
   const int splits = conv_fwd_splits(a.M, a.Cout, (int64_t)a.R * a.S * a.C, &kps, s);
@@ -1388,17 +1416,28 @@ static bool maybe_split(ConvFwdArgs& a, float* ws, bool stats, bool bnb, bool bn
   a.kps = kps;
   a.n_tiles = a.Cout % 128 == 0 ? a.Cout / 128 : a.Cout / 64;
   const bool wide = a.Cout % 128 == 0;
-#define DPT_SPLIT(S_, B_, R_, R2_)                                                   \
-  do {                                                                              \
-    if (wide) split_launch<128, S_, B_, R_, R2_>(a, s);                             \
-    else split_launch<64, S_, B_, R_, R2_>(a, s);                                   \
+#define DPT_SPLIT(...)                                      \
+  do {                                                      \
+    if (wide) split_launch<128, __VA_ARGS__>(a, s);         \
+    else split_launch<64, __VA_ARGS__>(a, s);               \
   } while (0)
-  if (stats) DPT_SPLIT(true, false, false, false);
-  else if (bnb && bnr && bnr2) DPT_SPLIT(false, true, true, true);
-  else if (bnb && bnr) DPT_SPLIT(false, true, true, false);
-  else if (bnb) DPT_SPLIT(false, true, false, false);
-  else DPT_SPLIT(false, false, false, false);
+  if (remap) {
+    if (bnb) DPT_SPLIT(false, true, false, false, true, true, false);
+    else if (zsib) DPT_SPLIT(false, false, false, false, true, true, true);
+    else DPT_SPLIT(false, false, false, false, true, true, false);
+  } else if (stats) {
+    DPT_SPLIT(true, false, false, false);
+  } else if (bnb && bnr && bnr2) {
+    DPT_SPLIT(false, true, true, true);
+  } else if (bnb && bnr) {
+    DPT_SPLIT(false, true, true, false);
+  } else if (bnb) {
+    DPT_SPLIT(false, true, false, false);
+  } else {
+    DPT_SPLIT(false, false, false, false);
+  }
 #undef DPT_SPLIT
+  (void)bkn;
   return true;
 }
 
@@ -1528,7 +1567,12 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
   a.bp_ld = a.m_tiles; a.bp_off = 0;
   const bool res = bny != nullptr;
   const dim3 block(conv::kThreads);
-  if (maybe_split(a, ws, false, true, res, res && bnx2 != nullptr, s)) return;
+  {
+    const int64_t keep_ld = a.bp_ld;
+    a.bp_ld = conv_split_cols(a.M);  // split: one partial column per 16-row slab
+    if (maybe_split(a, ws, false, true, res, res && bnx2 != nullptr, s)) return;
+    a.bp_ld = keep_ld;
+  }
   a.n_tiles = C % 128 == 0 ? C / 128 : C / 64;
   const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
   const bool two = res && bnx2 != nullptr;
@@ -1563,76 +1607,109 @@ void launch_conv_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int 
 // tap; its output rows land on (2a + ph, 2b + pw) (REMAP epilogue).  A class with no taps
 // (e.g. the odd classes of a 1x1 / stride-2 conv) gets zeros from the class-(0,0) launch (ZSIB)
 // - every dx element is written exactly once, no memset pass.
-int conv_dgrad_s2_chunks(int N, int H, int W, int R, int S, int pad) {
-  int chunks = 0;
-  for (int ph = 0; ph < 2; ++ph)
-    for (int pw = 0; pw < 2; ++pw) {
-      const int r0 = ((ph + pad) % 2 + 2) % 2, s0 = ((pw + pad) % 2 + 2) % 2;
-      const int Ha = (H - ph + 1) / 2, Wa = (W - pw + 1) / 2;
-      if (Ha > 0 && Wa > 0 && r0 < R && s0 < S) chunks += conv_m_tiles((int64_t)N * Ha * Wa);
-    }
-  return chunks;
-}
-
-void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout,
-                          int C, int R, int S, int pad, int H, int W, hipStream_t s, const uint16_t* bnx,
-                          const float* bn_mean, const float* bn_coef, float* bp1, float* bp2, bool f16) {
-  const bool bnb = bnx != nullptr;
-  const int bp_ld = bnb ? conv_dgrad_s2_chunks(N, H, W, R, S, pad) : 0;
-  int bp_off = 0;
-  int J[2], r0[2], Js[2], s0[2], D[2], Ds[2];
+// Parity-class geometry of the stride-2 backward-data (one stride-1 conv per non-empty class).
+struct S2Class {
+  int ph, pw, Rc, Sc, pad, Ha, Wa, tr0, ts0;
+  bool zsib;
+};
+static int s2_classes(int H, int W, int R, int S, int pad, S2Class* out) {
+  int J[2], r0[2], Js[2], s0[2], D[2];
   for (int ph = 0; ph < 2; ++ph) {
     r0[ph] = ((ph + pad) % 2 + 2) % 2;
     J[ph] = r0[ph] < R ? (R - 1 - r0[ph]) / 2 + 1 : 0;
     D[ph] = (ph + pad - r0[ph]) / 2;  // dy row of tap r0 for a = 0
     s0[ph] = r0[ph];
     Js[ph] = s0[ph] < S ? (S - 1 - s0[ph]) / 2 + 1 : 0;
-    Ds[ph] = D[ph];
   }
   const bool zsib = J[1] == 0 && Js[1] == 0 && J[0] > 0 && Js[0] > 0;
-  for (int ph = 0; ph < 2; ++ph) {
+  int n = 0;
+  for (int ph = 0; ph < 2; ++ph)
     for (int pw = 0; pw < 2; ++pw) {
       const int Ha = (H - ph + 1) / 2, Wa = (W - pw + 1) / 2;
       if (Ha <= 0 || Wa <= 0 || J[ph] == 0 || Js[pw] == 0) continue;
-      ConvFwdArgs a;
-      a.part = nullptr; a.splits = 1; a.kps = 0;
-      a.f16 = f16 ? 1 : 0;
-      a.x = dy; a.w = w; a.y = dx; a.psum = nullptr; a.psq = nullptr;
-      a.N = N; a.H = Ho; a.W = Wo; a.C = Cout; a.Cout = C; a.R = J[ph]; a.S = Js[pw]; a.stride = 1;
       // GEMM tap jj (0..J-1) reads dy row a + D - (J-1) + jj, weight tap r0 + 2*(J-1-jj)
-      a.pad = J[ph] - 1 - D[ph];
-      if (Js[pw] - 1 - Ds[pw] != a.pad) throw std::runtime_error("conv_dgrad_s2: unequal class paddings");
-      a.Ho = Ha; a.Wo = Wa;
-      a.M = (int64_t)N * Ha * Wa;
-      a.m_tiles = conv_m_tiles(a.M);
-      a.mt256 = 0;
-      a.Rw = R; a.Sw = S;
-      a.tr0 = r0[ph] + 2 * (J[ph] - 1); a.trs = -2;
-      a.ts0 = s0[pw] + 2 * (Js[pw] - 1); a.tss = -2;
-      a.oH = H; a.oW = W; a.oph = ph; a.opw = pw;
-      a.bnx = bnx; a.bny = nullptr; a.bnres = nullptr; a.bn_mean = bn_mean; a.bn_coef = bn_coef;
-      a.bnx2 = nullptr; a.bn_mean2 = nullptr; a.bp3 = nullptr;
-      a.bp1 = bp1; a.bp2 = bp2; a.bp_ld = bp_ld; a.bp_off = bp_off;
-      bp_off += a.m_tiles;
-      const bool z = zsib && ph == 0 && pw == 0;
-      const dim3 block(conv::kThreads);
-      a.n_tiles = C % 128 == 0 ? C / 128 : C / 64;
-      const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
-      if (bnb) {
-        // zero classes (ZSIB) only arise for 1x1 kernels, whose input is never a fused BN+ReLU
-        // output in the models here: BNB and ZSIB are not combined
-        if (z) throw std::runtime_error("conv_dgrad_s2: BN statistics with zero-filled classes unsupported");
-        if (C % 128 == 0) fwd_launch<128, 128, 1, true, true, false, true, false, true, false>(grid, block, s, a);
-        else fwd_launch<128, 64, 1, true, true, false, true, false, true, false>(grid, block, s, a);
-        continue;
-      }
-      if (C % 128 == 0) {
-        if (z) fwd_launch<128, 128, 1, true, true, false, false, false, true, true>(grid, block, s, a);
-        else fwd_launch<128, 128, 1, true, true, false, false, false, true, false>(grid, block, s, a);
-      } else {
-        if (z) fwd_launch<128, 64, 1, true, true, false, false, false, true, true>(grid, block, s, a);
-        else fwd_launch<128, 64, 1, true, true, false, false, false, true, false>(grid, block, s, a);
-      }
+      const int pad_c = J[ph] - 1 - D[ph];
+      if (Js[pw] - 1 - D[pw] != pad_c) throw std::runtime_error("conv_dgrad_s2: unequal class paddings");
+      out[n++] = S2Class{ph, pw, J[ph], Js[pw], pad_c, Ha, Wa, r0[ph] + 2 * (J[ph] - 1), s0[pw] + 2 * (Js[pw] - 1),
+                         zsib && ph == 0 && pw == 0};
+    }
+  return n;
+}
+
+ConvS2Plan conv_dgrad_s2_plan(int N, int H, int W, int C, int Cout, int R, int S, int pad, hipStream_t s) {
+  S2Class cl[4];
+  const int n = s2_classes(H, W, R, S, pad, cl);
+  ConvS2Plan pl{0, 0};
+  for (int i = 0; i < n; ++i) {
+    const int64_t M = (int64_t)N * cl[i].Ha * cl[i].Wa;
+    const int splits = conv_fwd_splits(M, C, (int64_t)cl[i].Rc * cl[i].Sc * Cout, nullptr, s);
+    pl.chunks += splits > 1 ? conv_split_cols(M) : conv_m_tiles(M);
+    if (splits > 1) pl.ws_floats = std::max(pl.ws_floats, (int64_t)splits * M * C);
+  }
+  return pl;
+}
+
+int conv_dgrad_s2_chunks(int N, int H, int W, int R, int S, int pad) {
+  S2Class cl[4];
+  const int n = s2_classes(H, W, R, S, pad, cl);
+  int chunks = 0;
+  for (int i = 0; i < n; ++i) chunks += conv_m_tiles((int64_t)N * cl[i].Ha * cl[i].Wa);
+  return chunks;
+}
+
+void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout,
+                          int C, int R, int S, int pad, int H, int W, hipStream_t s, const uint16_t* bnx,
+                          const float* bn_mean, const float* bn_coef, float* bp1, float* bp2, bool f16, float* ws) {
+  const bool bnb = bnx != nullptr;
+  // with a workspace the classes may split (the caller sized ws and bp_ld by conv_dgrad_s2_plan)
+  const int bp_ld = bnb ? (ws ? conv_dgrad_s2_plan(N, H, W, C, Cout, R, S, pad, s).chunks
+                              : conv_dgrad_s2_chunks(N, H, W, R, S, pad))
+                        : 0;
+  int bp_off = 0;
+  S2Class cl[4];
+  const int ncl = s2_classes(H, W, R, S, pad, cl);
+  for (int ci = 0; ci < ncl; ++ci) {
+    const S2Class& k = cl[ci];
+    ConvFwdArgs a;
+    a.part = nullptr; a.splits = 1; a.kps = 0;
+    a.f16 = f16 ? 1 : 0;
+    a.x = dy; a.w = w; a.y = dx; a.psum = nullptr; a.psq = nullptr;
+    a.N = N; a.H = Ho; a.W = Wo; a.C = Cout; a.Cout = C; a.R = k.Rc; a.S = k.Sc; a.stride = 1;
+    a.pad = k.pad;
+    a.Ho = k.Ha; a.Wo = k.Wa;
+    a.M = (int64_t)N * k.Ha * k.Wa;
+    a.m_tiles = conv_m_tiles(a.M);
+    a.mt256 = 0;
+    a.Rw = R; a.Sw = S;
+    a.tr0 = k.tr0; a.trs = -2;
+    a.ts0 = k.ts0; a.tss = -2;
+    a.oH = H; a.oW = W; a.oph = k.ph; a.opw = k.pw;
+    a.bnx = bnx; a.bny = nullptr; a.bnres = nullptr; a.bn_mean = bn_mean; a.bn_coef = bn_coef;
+    a.bnx2 = nullptr; a.bn_mean2 = nullptr; a.bp3 = nullptr;
+    a.bp1 = bp1; a.bp2 = bp2; a.bp_ld = bp_ld; a.bp_off = bp_off;
+    const bool z = k.zsib;
+    // zero classes (ZSIB) only arise for 1x1 kernels, whose input is never a fused BN+ReLU output
+    // in the models here: BNB and ZSIB are not combined
+    if (bnb && z) throw std::runtime_error("conv_dgrad_s2: BN statistics with zero-filled classes unsupported");
+    if (maybe_split(a, ws, false, bnb, false, false, s, true, true, z)) {
+      bp_off += conv_split_cols(a.M);
+      continue;
+    }
+    bp_off += a.m_tiles;
+    const dim3 block(conv::kThreads);
+    a.n_tiles = C % 128 == 0 ? C / 128 : C / 64;
+    const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
+    if (bnb) {
+      if (C % 128 == 0) fwd_launch<128, 128, 1, true, true, false, true, false, true, false>(grid, block, s, a);
+      else fwd_launch<128, 64, 1, true, true, false, true, false, true, false>(grid, block, s, a);
+      continue;
+    }
+    if (C % 128 == 0) {
+      if (z) fwd_launch<128, 128, 1, true, true, false, false, false, true, true>(grid, block, s, a);
+      else fwd_launch<128, 128, 1, true, true, false, false, false, true, false>(grid, block, s, a);
+    } else {
+      if (z) fwd_launch<128, 64, 1, true, true, false, false, false, true, true>(grid, block, s, a);
+      else fwd_launch<128, 64, 1, true, true, false, false, false, true, false>(grid, block, s, a);
     }
   }
 }
@@ -1662,9 +1739,11 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
   const int steps = (int)((M + 63) / 64);
   // ~768 blocks (3 per CU) and at least 32 K-steps per split: a split's fp32 partial tile
   // (BMW x BNW x 4 B, written once and read once by the reduce) then costs < 1/8 of the
-  // operand bytes it streams.
+  // operand bytes it streams.  Small problems that cannot fill the chip that way (ResNet-18 on
+  // 32x32 images: 2-128 K-steps) are K-loop-latency-bound instead: down to 2 K-steps per split.
   int splits = (768 + tiles - 1) / tiles;
-  splits = std::max(1, std::min(splits, steps / 32));
+  const int min_steps = (int64_t)tiles * (steps / 32) >= 512 ? 32 : 2;
+  splits = std::max(1, std::min(splits, steps / min_steps));
   pl.steps_per_split = (steps + splits - 1) / splits;
   pl.splits = (steps + pl.steps_per_split - 1) / pl.steps_per_split;
   pl.part_floats = pl.splits > 1 ? (int64_t)pl.splits * Cout * R * S * C : 0;

@@ -148,7 +148,7 @@ void conv_set_variant(int v);
 int conv_fwd_splits(int64_t M, int Cout, int64_t K, int* kps = nullptr, hipStream_t s = nullptr);
 int conv_fwd_splits_for(int64_t M, int Cout, int64_t K, bool graph, int* kps = nullptr);
 int conv_split_cols(int64_t M);
-void conv_set_splitk(bool on);  // run-time switch (A/B tests); default on unless DPT_CONV_SPLITK=0
+void conv_set_splitk(int mode);  // 0 off / 1 auto (default, DPT_CONV_SPLITK) / 2 in-graph policy always
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
                      int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s, int Ho = 0,
                      int Wo = 0, bool f16 = false, float* ws = nullptr);
@@ -183,10 +183,15 @@ struct WtFlipBatch {
 };
 void launch_conv_wt_flip_multi(WtFlipBatch b, hipStream_t s);
 // stride-2 backward-data straight from the KRSC weight w [Cout,R,S,C]: dy [N,Ho,Wo,Cout] -> dx [N,H,W,C]
+struct ConvS2Plan {
+  int chunks;          // BN-partial columns over all parity classes
+  int64_t ws_floats;   // split-K workspace (0: no class splits)
+};
+ConvS2Plan conv_dgrad_s2_plan(int N, int H, int W, int C, int Cout, int R, int S, int pad, hipStream_t s);
 void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int N, int Ho, int Wo, int Cout,
                           int C, int R, int S, int pad, int H, int W, hipStream_t s, const uint16_t* bnx = nullptr,
                           const float* bn_mean = nullptr, const float* bn_coef = nullptr, float* bp1 = nullptr,
-                          float* bp2 = nullptr, bool f16 = false);
+                          float* bp2 = nullptr, bool f16 = false, float* ws = nullptr);
 // [C][chunks] partial columns the BN-statistics variant of launch_conv_dgrad_s2 writes
 int conv_dgrad_s2_chunks(int N, int H, int W, int R, int S, int pad);
 // stride-1 backward-data straight from the KRSC weight w [Cout,R,S,C]: dy [N,Ho,Wo,Cout] -> dx [N,Ho,Wo,C]

@@ -96,10 +96,10 @@ class Trainer:
         gpu_cl = self.device.type == "cuda" and bool(getattr(args, "channels_last", False))
         # MFMA convs need channels_last bf16/fp16 activations; routing is per model
         use_native_conv = gpu_cl and bool(getattr(args, "native_conv", True)) and native_conv.ENABLED
+        # every supported conv runs native: small tile grids split their K loop (split-K,
+        # conv_kernels.hip), which made the MFMA path faster than MIOpen on ResNet-18 / 32x32
+        # under hipGraph too; DPT_CONV_MIN_PIXELS still routes tiny convs to MIOpen
         min_px = None
-        if getattr(args, "cuda_graph", False) and "DPT_CONV_MIN_PIXELS" not in os.environ:
-            # launches hidden by the graph: tiny convs are faster on MIOpen (ops/conv.py)
-            min_px = 3072
         if getattr(args, "fused_bn", True) and gpu_cl:
             fuse_native_layers(model, native_conv=use_native_conv, min_pixels=min_px)
         else:

@@ -46,11 +46,10 @@ STEM_ENABLED = os.environ.get("DPT_NATIVE_STEM", "0") == "1"
 
 
 # Convs with fewer output pixels than this go to MIOpen (default: none; a model can override it
-# per conv through models.layers.fuse_native_layers(min_pixels=...)).  A 128-row tile grid
-# that small cannot fill 256 CUs - ResNet-18 on 32x32 inputs has 128-2048 output pixels in
-# layer2-4 at batch 128 - and with the launches hidden by a hipGraph MIOpen's small-shape
-# kernels win (3072: 46.5k -> 60.7k img/s), but eagerly the native path is faster (41.6k vs
-# 28.6k img/s; BASELINE.md ResNet-18 table), so the default keeps every supported conv native.
+# per conv through models.layers.fuse_native_layers(min_pixels=...)).  Small tile grids used to
+# lose to MIOpen's small-shape kernels under hipGraph (ResNet-18 on 32x32: 128-2048 output
+# pixels in layer2-4 at batch 128); the kernels now split the K loop over blocks there
+# (conv_fwd_splits), which beats MIOpen at every size (BASELINE.md ResNet-18 table).
 MIN_PIXELS = int(os.environ.get("DPT_CONV_MIN_PIXELS", "0"))
 
 

@@ -546,14 +546,14 @@ def test_splitk_conv_matches_unsplit(cuda, shape):
     mean = torch.randn(C, device=cuda, generator=g) * 0.1
     coef = torch.cat([torch.rand(C, device=cuda, generator=g) + 0.5, torch.randn(C, device=cuda, generator=g) * 0.1])
     outs = []
-    for on in (True, False):
+    for on in (1, 0):
         C_.conv_set_splitk(on)
         y, ps, pq = C_.conv_fwd(x, w, 1, p, True)
         dx = C_.conv_dgrad_preflipped(gy, wt, p)
         d1, p1, p2, _ = C_.conv_dgrad_bnstats(gy, w, p, bnx, mean, coef, w_flipped=wt)
         d2, q1, q2, _ = C_.conv_dgrad_bnstats(gy, w, p, bnx, mean, None, bny, bnres, wt)
         outs.append([y, ps.sum(1), pq.sum(1), dx, d1, p1.sum(1), p2.sum(1), d2, q1.sum(1), q2.sum(1)])
-    C_.conv_set_splitk(True)
+    C_.conv_set_splitk(1)
     ref = F.conv2d(x.float(), w.float(), padding=p)
     torch.testing.assert_close(outs[0][0].float(), ref, rtol=1e-2, atol=1e-2)
     for a, b in zip(*outs):
@@ -591,4 +591,31 @@ def test_splitk_under_graph_matches_eager(cuda):
     g.replay()
     torch.cuda.synchronize()
     for a, b in zip(out, eager):
+        torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * b.float().abs().max().item() + 1e-3)
+
+
+@pytest.mark.parametrize("shape", [(64, 256, 4, 4, 512, 3, 1), (64, 128, 8, 8, 256, 1, 0), (3, 64, 9, 7, 128, 3, 1)])
+def test_splitk_stride2_dgrad_matches_unsplit(cuda, shape):
+    """Stride-2 backward-data with split-K parity classes (the graph policy, conv_set_splitk(2)):
+    REMAP epilogue, zero-filled classes of a 1x1/2 conv (ZSIB) and the BN+ReLU statistics."""
+    N, C, H, W, Cout, k, p = shape
+    C_ = ops.native()
+    x, w = _operands(cuda, N, C, H, W, Cout, k, seed=11)
+    Ho, Wo = (H + 2 * p - k) // 2 + 1, (W + 2 * p - k) // 2 + 1
+    gy = torch.randn(N, Cout, Ho, Wo, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    bnx = torch.randn(N, C, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    mean = torch.randn(C, device=cuda) * 0.1
+    coef = torch.cat([torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda) * 0.1])
+    outs = []
+    for mode in (2, 0):
+        C_.conv_set_splitk(mode)
+        r = [C_.conv_dgrad_s2(gy, w, p, H, W)[0]]
+        if k > 1:
+            d, p1, p2 = C_.conv_dgrad_s2(gy, w, p, H, W, bnx, mean, coef)
+            r += [d, p1.sum(1), p2.sum(1)]
+        outs.append(r)
+    C_.conv_set_splitk(1)
+    ref = torch.nn.grad.conv2d_input(x.shape, w.float(), gy.float(), stride=2, padding=p)
+    torch.testing.assert_close(outs[0][0].float(), ref, rtol=1e-2, atol=2e-2)
+    for a, b in zip(*outs):
         torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * b.float().abs().max().item() + 1e-3)
