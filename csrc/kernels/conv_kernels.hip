@@ -946,22 +946,27 @@ struct ConvWgradArgs {
   int f16;             // fp16 operands (bf16 otherwise)
 };
 
-template <int BMW, int BNW, int STAGES, bool F16 = false>
-__global__ __launch_bounds__(conv::kThreads, 2) void conv_wgrad_kernel(ConvWgradArgs p) {
+// NT = 256: 2 x 2 waves; NT = 512 (256 x 256 tiles): 2 x 4 waves of 128 x 64 - twice the MFMA
+// work per staged byte, one block per CU.
+template <int BMW, int BNW, int STAGES, bool F16 = false, int NT = conv::kThreads>
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(ConvWgradArgs p) {
   using namespace conv;
+  constexpr int NW = NT / 64;
+  constexpr int WNW = NT == 512 ? 4 : 2, WMW = NW / WNW;  // waves along N / M
   constexpr int BKP = 64;                   // pixels per K-step
   constexpr int RBA = BMW * 2, RBB = BNW * 2;  // LDS row bytes (dy image, x image)
   constexpr int A_BYTES = BKP * RBA, B_BYTES = BKP * RBB;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int A_INSTR = A_BYTES / 1024 / 4;  // glds instructions per wave per tile
-  constexpr int B_INSTR = B_BYTES / 1024 / 4;
+  constexpr int A_INSTR = A_BYTES / 1024 / NW;  // glds instructions per wave per tile
+  constexpr int B_INSTR = B_BYTES / 1024 / NW;
   constexpr int A_RPI = 1024 / RBA, B_RPI = 1024 / RBB;  // rows per glds instruction
-  constexpr int WTM = BMW / 2, WTN = BNW / 2;  // wave tile (2 x 2 waves)
+  constexpr int WTM = BMW / WMW, WTN = BNW / WNW;  // wave tile
   constexpr int MI = WTM / 32, NI = WTN / 32;
+  static_assert(MI >= 1 && NI >= 1 && A_INSTR >= 1 && B_INSTR >= 1, "conv_wgrad_kernel: bad tiling");
   __shared__ __attribute__((aligned(16))) unsigned char lds[STAGES * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WNW, wn = wid % WNW;
   const int tiles = p.co_tiles * p.n_tiles;
   const int bid = conv::xcd_remap(blockIdx.x, tiles * p.splits);
   const int sp = bid / tiles, tile = bid - sp * tiles;
@@ -1735,6 +1740,8 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
   const int64_t M = (int64_t)N * pl.Ho * pl.Wo;
   pl.bmw = Cout % 128 == 0 ? 128 : 64;
   pl.bnw = C % 128 == 0 ? 128 : 64;
+  // variant 12 (A/B): 8-wave 256 x 256 tiles where both channel counts allow them
+  if (conv_variant() == 12 && Cout % 256 == 0 && C % 256 == 0) pl.bmw = pl.bnw = 256;
   const int tiles = (Cout / pl.bmw) * (R * S * C / pl.bnw);
   const int steps = (int)((M + 63) / 64);
   // ~768 blocks (3 per CU) and at least 32 K-steps per split: a split's fp32 partial tile
@@ -1769,7 +1776,10 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
   a.direct = (R == 1 && S == 1 && stride == 1 && pad == 0) ? 1 : 0;
   const dim3 grid((unsigned)(a.co_tiles * a.n_tiles * a.splits)), block(conv::kThreads);
   const int v = a.f16 ? 0 : conv_variant();
-  if (v == 1 || v == 2) {
+  if (pl.bmw == 256) {  // conv_wgrad_plan chose the 8-wave 256 x 256 tile
+    if (a.f16) throw std::runtime_error("conv_wgrad: the 256 x 256 variant is bf16 only");
+    hipLaunchKernelGGL((conv_wgrad_kernel<256, 256, 2, false, 512>), grid, dim3(512), 0, st, a);
+  } else if (v == 1 || v == 2) {
     if (pl.bmw == 128 && pl.bnw == 128) wgrad_launch<128, 128, 2>(grid, block, st, a);
     else if (pl.bmw == 128) wgrad_launch<128, 64, 2>(grid, block, st, a);
     else if (pl.bnw == 128) wgrad_launch<64, 128, 2>(grid, block, st, a);

@@ -21,7 +21,7 @@ __device__ __forceinline__ f32x16_t mfma32(bf16x8_t a, bf16x8_t b, f32x16_t c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-// ---- LDS images with rows of RB bytes (RB = 128: 64 bf16, RB = 256: 128 bf16) -----------------
+// ---- LDS images with rows of RB bytes (RB = 128: 64 bf16, RB = 256: 128 bf16, RB = 512) -------
 // 16-byte chunk ch of row `row` is stored at slot wg_slot(row, ch).  The XOR makes both read
 // kinds conflict-free: ds_read_b128 of one chunk from 16 consecutive rows (A/B operands with
 // rows = M/N) and ds_read_b64_tr_b16 of 4 consecutive rows x 32 columns per 32-lane half
@@ -29,7 +29,9 @@ __device__ __forceinline__ f32x16_t mfma32(bf16x8_t a, bf16x8_t b, f32x16_t c) {
 // slot it writes, chunk wg_slot(row, slot).
 template <int RB>
 __device__ __forceinline__ int wg_slot(int row, int ch) {
-  if (RB == 256) return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
+  // RB = 512 (256 bf16): the same low-4-bit XOR - each row starts on bank 0, and the 4 rows one
+  // transposing read touches land on 4 distinct 64-byte bank groups
+  if (RB == 256 || RB == 512) return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
   return ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
 }
 
