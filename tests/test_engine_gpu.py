@@ -39,14 +39,19 @@ def test_native_matches_torch_fp32(cuda, opt):
     # between two conv algorithm runs, so its parity bound is a few lr steps.
     # Each parameter's 3-step update must agree with stock torch's to 1% of the update's norm
     # (conv1 sits at the end of backward, so it carries every upstream fp32 rounding difference
-    # of two different conv-algorithm choices), and elementwise within an absolute bound.
-    atol = 1e-3 if opt == "sgd" else 4e-3
+    # of two different conv-algorithm choices), and elementwise within 1e-3 or 5% of the largest
+    # element of the update (MIOpen's fp32 solver choice depends on what ran earlier in the
+    # process, and a deep 4x4-spatial layer's update tails then differ by more than 1e-3).
     for (n, p), (_, q), w0 in zip(nat.module.named_parameters(), ref.module.named_parameters(), p0):
+        du_ref = (q - w0).double()
         if opt == "sgd":
-            du_ref = (q - w0).double()
             rel = ((p - q).double().norm() / du_ref.norm().clamp_min(1e-12)).item()
             assert rel < 1e-2, f"{n}: |native-torch|/|torch update| = {rel:.3e}"
-        torch.testing.assert_close(p, q, rtol=2e-3, atol=atol, msg=n)
+            atol = max(1e-3, 0.05 * du_ref.abs().max().item())
+        else:
+            atol = 4e-3
+        torch.testing.assert_close(p, q, rtol=2e-3, atol=atol,
+                                   msg=lambda m, n=n: f"{n}: {m}")
 
 
 def test_native_amp_bf16_step_and_scaler(cuda):
