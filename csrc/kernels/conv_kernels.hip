@@ -943,6 +943,11 @@ struct ConvWgradArgs {
   int co_tiles, n_tiles, splits, steps_per_split;
   FastDiv div_wo, div_howo;
   int direct;          // 1x1, stride 1, pad 0: x row = dy row
+  // K-step advance of a lane's x row by BKP = 64 pixels, 64 = A*Ho*Wo + B*Wo + Cq (host-side):
+  // wi += dw_step (wrap: -wwrap, hi += stride), hi += dh_step (wrap: -hwrap); the element
+  // offset moves by dp_w / dp_wwrap / dp_h / dp_hwrap alongside (image carries folded in)
+  int dw_step, wwrap, dh_step, hwrap;
+  int dp_w, dp_wwrap, dp_h, dp_hwrap;
   int f16;             // fp16 operands (bf16 otherwise)
 };
 
@@ -995,37 +1000,71 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(ConvWgradArgs p) {
     bchk[i] = wg_slot<RBB>(brow[i], lane % (RBB / 16));
   }
 
-  auto stage = [&](int ks, int buf) {
+  // Per-lane row state, set up once and advanced by one K-step per stage() call (stage() runs
+  // for ks = k0, k0+1, ... in order): the K loop does no divisions and no multiplies - the
+  // 64-bit address multiplies of a per-step recompute were the largest VALU cost of this loop.
+  // 32-bit offsets (launch_conv_wgrad checks the tensor sizes).
+  int aoff[A_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) aoff[i] = (k0 * BKP + arow[i]) * p.Cout + co0 + achk[i] * 8;
+  int bm[B_INSTR], bh[B_INSTR], bw[B_INSTR], bsub[B_INSTR], boff[B_INSTR];
+#pragma unroll
+  for (int i = 0; i < B_INSTR; ++i) {
+    const int m = k0 * BKP + brow[i];
+    bm[i] = m;
+    bsub[i] = tps > 1 ? bchk[i] * 8 / p.C : 0;  // narrow inputs: this chunk's tap
+    if (p.direct) {
+      bh[i] = 0; bw[i] = 0;
+      boff[i] = m * p.C + ci0 + bchk[i] * 8;
+    } else {
+      const int n = m / (p.Ho * p.Wo), rem = m - n * (p.Ho * p.Wo);
+      const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+      bh[i] = ho * p.stride - p.pad + r;
+      bw[i] = wo * p.stride - p.pad + s;
+      boff[i] = ((n * p.H + bh[i]) * p.W + bw[i]) * p.C + ci0 + bchk[i] * 8;
+    }
+  }
+  const int wlim = p.Wo * p.stride - p.pad + s;  // wo >= Wo
+  const int hlim = p.Ho * p.stride - p.pad + r;  // ho >= Ho
+  const int adelta = BKP * p.Cout;
+  const int dp_step = p.dp_w + p.dp_h, hstep1 = p.dh_step + p.stride;
+
+  // Buffer loads into LDS: the descriptors' range check zero-fills rows past the end (dy:
+  // m >= M) and the zero-padding taps (x: offset kOOB), so no address selects are needed.
+  constexpr uint32_t kOOB = 0xFFFFFF00u;  // >= any num_records here, and offset + 16 does not wrap
+  const __amdgpu_buffer_rsrc_t rdy =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, 0, (int)((uint32_t)p.M * (uint32_t)p.Cout * 2u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.x, 0, (int)((uint32_t)p.N * (uint32_t)(p.H * p.W * p.C) * 2u), 0x00020000);
+
+  auto stage = [&](int /*ks*/, int buf) {
     unsigned char* a = lds + buf * STAGE;
     unsigned char* b = a + A_BYTES;
-    const int mb = ks * BKP;
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) {
-      const int m = mb + arow[i];
-      const void* src = m < p.M ? (const void*)(p.dy + (int64_t)m * p.Cout + co0 + achk[i] * 8)
-                                : (const void*)g_conv_zero16;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(a + (wid * A_INSTR + i) * 1024),
-                                       16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rdy, (__attribute__((address_space(3))) void*)(a + (wid * A_INSTR + i) * 1024),
+                                               16, (uint32_t)aoff[i] * 2u, 0, 0, 0);
+      aoff[i] += adelta;
     }
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i) {
-      const int m = mb + brow[i];
-      const void* src = (const void*)g_conv_zero16;
-      if (m < p.M) {
-        if (p.direct) {
-          src = p.x + (int64_t)m * p.C + ci0 + bchk[i] * 8;
-        } else {
-          const uint32_t n = fdiv((uint32_t)m, p.div_howo);
-          const uint32_t rem = (uint32_t)m - n * (uint32_t)(p.Ho * p.Wo);
-          const uint32_t ho = fdiv(rem, p.div_wo), wo = rem - ho * (uint32_t)p.Wo;
-          const int hi = (int)ho * p.stride - p.pad + r, wi = (int)wo * p.stride - p.pad + s;
-          const int sub = tps > 1 ? bchk[i] * 8 / p.C : 0;  // narrow inputs: this chunk's tap
-          if ((unsigned)hi < (unsigned)p.H && (unsigned)(wi + sub) < (unsigned)p.W)
-            src = p.x + (((int64_t)n * p.H + hi) * p.W + wi) * p.C + ci0 + bchk[i] * 8;
-        }
+      // bitwise, not short-circuit: no exec-mask branches around the select
+      const bool ok = (bm[i] < p.M) & ((p.direct != 0) | (((unsigned)bh[i] < (unsigned)p.H) &
+                                                        ((unsigned)(bw[i] + bsub[i]) < (unsigned)p.W)));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(b + (wid * B_INSTR + i) * 1024),
+                                               16, ok ? (uint32_t)boff[i] * 2u : kOOB, 0, 0, 0);
+      bm[i] += BKP;
+      boff[i] += dp_step;
+      if (!p.direct) {  // "c ? v + k : v" forms: one add + one v_cndmask each
+        bw[i] += p.dw_step;
+        const bool cw = bw[i] >= wlim;
+        bw[i] = cw ? bw[i] - p.wwrap : bw[i];
+        bh[i] = cw ? bh[i] + hstep1 : bh[i] + p.dh_step;
+        boff[i] = cw ? boff[i] + p.dp_wwrap : boff[i];
+        const bool ch = bh[i] >= hlim;
+        bh[i] = ch ? bh[i] - p.hwrap : bh[i];
+        boff[i] = ch ? boff[i] + p.dp_hwrap : boff[i];
       }
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(b + (wid * B_INSTR + i) * 1024),
-                                       16, 0, 0);
     }
   };
 
@@ -1774,6 +1813,23 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
   a.div_wo = make_fastdiv((uint32_t)pl.Wo);
   a.div_howo = make_fastdiv((uint32_t)(pl.Ho * pl.Wo));
   a.direct = (R == 1 && S == 1 && stride == 1 && pad == 0) ? 1 : 0;
+  // the kernel's 32-bit element offsets (rows up to one K-step past the end are addressed,
+  // never loaded)
+  if (((int64_t)a.M + 64) * Cout >= (1ll << 31) || ((int64_t)N + 1) * H * W * C >= (1ll << 31))
+    throw std::runtime_error("conv_wgrad: activation tensors beyond 2^31 elements are not supported");
+  {
+    const int howo = pl.Ho * pl.Wo, q = 64 / howo, rem = 64 % howo, bq = rem / pl.Wo, cq = rem % pl.Wo;
+    a.dw_step = cq * stride; a.wwrap = pl.Wo * stride;
+    a.dh_step = bq * stride; a.hwrap = pl.Ho * stride;
+    if (a.direct) {
+      a.dp_w = 64 * C; a.dp_wwrap = a.dp_h = a.dp_hwrap = 0;
+    } else {
+      a.dp_w = (cq * stride + q * H * W) * C;
+      a.dp_wwrap = (stride * W - pl.Wo * stride) * C;
+      a.dp_h = bq * stride * W * C;
+      a.dp_hwrap = (H * W - pl.Ho * stride * W) * C;
+    }
+  }
   const dim3 grid((unsigned)(a.co_tiles * a.n_tiles * a.splits)), block(conv::kThreads);
   const int v = a.f16 ? 0 : conv_variant();
   if (pl.bmw == 256) {  // conv_wgrad_plan chose the 8-wave 256 x 256 tile
