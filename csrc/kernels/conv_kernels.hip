@@ -556,10 +556,18 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
           b += bred[(w * NS3 + 1) * BN + tid];
           if (two) c3 += bred[(w * NS3 + 2) * BN + tid];
         }
-        const int64_t pc = (int64_t)(n0 + tid) * p.bp_ld + p.bp_off + mt;
+        // partials stay one column per 128-row sub-tile whatever BM is: a 256-row block
+        // writes its sum in its first column and zero in the second
+        constexpr int SUBB = BM / 128;
+        const int64_t pc = (int64_t)(n0 + tid) * p.bp_ld + p.bp_off + (int64_t)mt * SUBB;
         p.bp1[pc] = a;
         p.bp2[pc] = b;
         if (two) p.bp3[pc] = c3;
+        if (SUBB == 2 && ((int64_t)mt * 2 + 1) * 128 < p.M) {
+          p.bp1[pc + 1] = 0.f;
+          p.bp2[pc + 1] = 0.f;
+          if (two) p.bp3[pc + 1] = 0.f;
+        }
       }
     }
   }
@@ -1366,6 +1374,27 @@ static int conv_variant() {
 }
 void conv_set_variant(int v) { g_conv_variant = v; }
 
+// Production choice of the 8-wave 256-row tiles (variant 0): deep reductions onto narrow
+// outputs, where the 128 x 128 tile re-reads A from L2 once per 128 output channels and the
+// per-CU L2 -> LDS rate caps it (profiles/conv_variants_*.md, ResNet-50 batch 256):
+//   N = 256, K >= 1024, M >= 32768          -> 9  (256 x 256): 3x3 256->256 @14x14 709 -> 896 TF
+//   N = 512, K >= 2048, M <= 16384          -> 10 (256 x 128): 3x3 512->512 @7x7 714 -> 802 TF
+// Off by default: in the ResNet-50 training step (stats / BNB / BNR epilogues, L2 shared with
+// the neighbouring kernels) the per-shape wins did not show (11680/11521 vs 11659/11534 img/s,
+// same-box A/B).  DPT_CONV_BIG=1 / conv_set_big(1) turns it on.
+static int g_conv_big = -1;
+static int conv_big_auto(int64_t M, int N, int64_t K) {
+  if (g_conv_big < 0) {
+    const char* e = std::getenv("DPT_CONV_BIG");
+    g_conv_big = e ? std::atoi(e) : 0;
+  }
+  if (!g_conv_big) return 0;
+  if (N == 256 && K >= 1024 && M >= 32768) return 9;
+  if (N == 512 && K >= 2048 && M <= 16384) return 10;
+  return 0;
+}
+void conv_set_big(int on) { g_conv_big = on; }
+
 
 // Launch one conv_fwd_kernel instantiation in the element type of a.f16 (fp16 is instantiated
 // for the production 128-row, 1-stage, LDS-epilogue variants only).
@@ -1582,7 +1611,10 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
   a.mt256 = 0;
   const int v = conv_variant();
   if (!bkn && maybe_split(a, ws, psum != nullptr, false, false, false, s)) return;
-  if (!bkn && !a.f16 && v >= 9 && v <= 11 && conv_fwd_big(v, a, s)) return;
+  if (!bkn && !a.f16) {
+    const int vb = (v >= 9 && v <= 11) ? v : v == 0 ? conv_big_auto(a.M, Cout, (int64_t)R * S * C) : 0;
+    if (vb && conv_fwd_big(vb, a, s)) return;
+  }
   if (wide) conv_fwd_dispatch<128>(v, bkn, a, s);
   else conv_fwd_dispatch<64>(v, bkn, a, s);
 }
@@ -1617,9 +1649,29 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
     if (maybe_split(a, ws, false, true, res, res && bnx2 != nullptr, s)) return;
     a.bp_ld = keep_ld;
   }
+  const bool two = res && bnx2 != nullptr;
+  if (!f16 && conv_variant() == 0) {
+    // 8-wave 256-row tiles (conv_big_auto): N = C, K = Cout*R*S
+    const int vb = conv_big_auto(a.M, C, (int64_t)Cout * R * S);
+    if (vb) {
+      const int bn = vb == 10 ? 128 : 256;
+      a.n_tiles = C / bn;
+      a.mt256 = (int)((a.M + 255) / 256);
+      const dim3 g((unsigned)(a.mt256 * a.n_tiles));
+      if (vb == 9) {
+        if (two) fwd_launch<256, 256, 2, true, false, false, true, true, false, false, true, 512>(g, block, s, a);
+        else if (res) fwd_launch<256, 256, 2, true, false, false, true, true, false, false, false, 512>(g, block, s, a);
+        else fwd_launch<256, 256, 2, true, false, false, true, false, false, false, false, 512>(g, block, s, a);
+      } else {
+        if (two) fwd_launch<256, 128, 2, true, false, false, true, true, false, false, true, 512>(g, block, s, a);
+        else if (res) fwd_launch<256, 128, 2, true, false, false, true, true, false, false, false, 512>(g, block, s, a);
+        else fwd_launch<256, 128, 2, true, false, false, true, false, false, false, false, 512>(g, block, s, a);
+      }
+      return;
+    }
+  }
   a.n_tiles = C % 128 == 0 ? C / 128 : C / 64;
   const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
-  const bool two = res && bnx2 != nullptr;
   if (C % 128 == 0) {
     if (two) fwd_launch<128, 128, 1, true, false, false, true, true, false, false, true>(grid, block, s, a);
     else if (res) fwd_launch<128, 128, 1, true, false, false, true, true>(grid, block, s, a);

@@ -140,6 +140,7 @@ bool conv_supported(int C, int Cout);
 bool conv_supported_narrow(int C, int Cout, int S);  // C = 16/32 with S % (64/C) == 0 (fwd, wgrad)
 int conv_m_tiles(int64_t M);
 void conv_set_variant(int v);
+void conv_set_big(int on);  // 8-wave 256-row tiles where conv_big_auto picks them (default off)
 // Ho/Wo > 0: explicit output size (padding applied on top/left only beyond what it needs)
 // ws: split-K workspace of conv_fwd_splits(M, Cout, R*S*C) * M * Cout floats when that is > 1
 // (nullptr: never split).  Small tile grids split the K loop over blocks (fp32 partials).

@@ -619,3 +619,55 @@ def test_splitk_stride2_dgrad_matches_unsplit(cuda, shape):
     torch.testing.assert_close(outs[0][0].float(), ref, rtol=1e-2, atol=2e-2)
     for a, b in zip(*outs):
         torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * b.float().abs().max().item() + 1e-3)
+
+
+BIG_SHAPES = [
+    # N, C, H, W, Cout, k, pad: conv_big_auto picks 256x256 (N = 256, K >= 1024, M >= 32768)
+    (2, 256, 128, 130, 256, 3, 1),          # M = 33280: a partial last 256-row tile
+    (170, 1024, 14, 14, 256, 1, 0),         # ResNet-50 layer3 conv1 shape (M = 33320)
+    # and 256x128 (N = 512, K >= 2048, M <= 16384)
+    (64, 512, 7, 7, 512, 3, 1),
+    (40, 2048, 7, 7, 512, 1, 0),
+]
+
+
+@pytest.mark.parametrize("shape", BIG_SHAPES)
+def test_big_tile_auto_matches_128_tiles(cuda, shape):
+    """The 8-wave 256-row tiles conv_big_auto picks for deep reductions onto 256/512 channels:
+    forward + BN statistics, and the BN+ReLU (BNB), block-tail (BNR) and downsample (BNR2)
+    backward-data epilogues, against the 128-row tiles (conv_set_big(0)) and an fp32 reference.
+    The BN partials keep one column per 128 rows (a 256-row block zero-fills its second)."""
+    N, C, H, W, Cout, k, p = shape
+    C_ = ops.native()
+    x, w = _operands(cuda, N, C, H, W, Cout, k, seed=11)
+    # backward-data of the conv C_out=C <- C_in=Cout: dy has the C channels (GEMM K = C*k*k),
+    # dx the Cout channels (GEMM N), so both directions hit the rule
+    wd = (torch.randn(C, Cout, k, k, device=cuda) * 0.02).to(torch.bfloat16).contiguous(memory_format=CL)
+    cin = Cout
+    gy = torch.randn(N, C, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    wt = C_.conv_wt_flip_multi([wd])[0]
+    g = torch.Generator(device=cuda).manual_seed(12)
+    mk = lambda: torch.randn(N, cin, H, W, device=cuda, generator=g).to(torch.bfloat16).contiguous(memory_format=CL)
+    bnx, bnres, bnx2 = mk(), mk(), mk()
+    bny = torch.relu(mk().float()).to(torch.bfloat16).contiguous(memory_format=CL)
+    mean = torch.randn(cin, device=cuda, generator=g) * 0.1
+    mean2 = torch.randn(cin, device=cuda, generator=g) * 0.1
+    coef = torch.cat([torch.rand(cin, device=cuda, generator=g) + 0.5, torch.randn(cin, device=cuda, generator=g) * 0.1])
+    outs = []
+    try:
+        for on in (1, 0):
+            C_.conv_set_big(on)  # forced on: the production default is off
+            y, ps, pq = C_.conv_fwd(x, w, 1, p, True)
+            d1, p1, p2, _ = C_.conv_dgrad_bnstats(gy, wd, p, bnx, mean, coef, w_flipped=wt)
+            d2, q1, q2, _ = C_.conv_dgrad_bnstats(gy, wd, p, bnx, mean, None, bny, bnres, wt)
+            d3, r1, r2, r3 = C_.conv_dgrad_bnstats(gy, wd, p, bnx, mean, None, bny, bnres, wt, bnx2, mean2)
+            outs.append([y, ps.sum(1), pq.sum(1), d1, p1.sum(1), p2.sum(1), d2, q1.sum(1), q2.sum(1),
+                         d3, r1.sum(1), r2.sum(1), r3.sum(1)])
+    finally:
+        C_.conv_set_big(0)
+    ref = F.conv2d(x.float(), w.float(), padding=p)
+    torch.testing.assert_close(outs[0][0].float(), ref, rtol=1e-2, atol=1e-2)
+    dref = torch.nn.grad.conv2d_input((N, cin, H, W), wd.float(), gy.float(), padding=p)
+    torch.testing.assert_close(outs[0][3].float(), dref, rtol=1e-2, atol=2e-2)
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * b.float().abs().max().item() + 1e-3)
