@@ -36,6 +36,10 @@
 namespace dpt {
 
 
+#ifndef DPT_CONV_HALF_EPI
+#define DPT_CONV_HALF_EPI 0
+#endif
+
 namespace conv {
 
 constexpr int BM = 128;
@@ -177,7 +181,14 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   constexpr int C_STRIDE = BN * 2 + 16;  // epilogue image row stride (bytes), padded
   constexpr int RED = 2 * WM * BN * 4;   // BN-statistics cross-wave scratch
   constexpr int LDS_MAIN = STAGES * STAGE;
-  constexpr int LDS_EPI = (LDSEPI ? BM * C_STRIDE : 0) + RED;
+  // HALF: the 128-row, 4-wave LDS epilogue stages its output image 64 rows at a time, so the
+  // epilogue (17 KiB + statistics scratch) fits under the 32 KiB K-loop buffer of a 128 x 128
+  // tile: 5 resident blocks per CU instead of 4 (36 KiB), i.e. 25 % more bytes in flight for a
+  // K loop that is latency-bound on its L2 -> LDS loads (profiles/conv_pmc_r2.md)
+  constexpr bool HALF = DPT_CONV_HALF_EPI && LDSEPI && BM == 128 && NT == conv::kThreads && MI * 32 <= 64 && !BNB &&
+                        !SPLIT;
+  constexpr int EROWS = HALF ? 64 : BM;  // rows of the epilogue image
+  constexpr int LDS_EPI = (LDSEPI ? EROWS * C_STRIDE : 0) + RED;
   constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS];
 
@@ -200,8 +211,11 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   // Narrow inputs (C = 16/32): one 64-wide K-step spans 64/C consecutive taps along s, i.e.
   // consecutive input pixels, so a lane's 16-byte chunk sits at sub-tap (chunk*8)/C and the
   // address is unchanged (pixel stride = C elements); only its bounds check moves.
-  int hi0[A_PER_T], wi0[A_PER_T];
-  int64_t abase[A_PER_T];
+  // 32-bit element offsets and buffer loads into LDS (conv_check_offsets on the host): the
+  // descriptors hold the base addresses in SGPRs, the zero padding is the range check (offset
+  // kOOB), so a lane keeps 6 offsets instead of 6 64-bit pointers (fewer VGPRs: no spills at 5
+  // waves per SIMD) and selects nothing but an offset.
+  int hi0[A_PER_T], wi0[A_PER_T], aoff[A_PER_T];
   const int64_t HoWo = (int64_t)p.Ho * p.Wo;
 #pragma unroll
   for (int i = 0; i < A_PER_T; ++i) {
@@ -214,15 +228,15 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
       const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
       hi0[i] = ho * p.stride - p.pad;
       wi0[i] = wo * p.stride - p.pad + (p.C < BK ? achunk * 8 / p.C : 0);
-      abase[i] = ((n * p.H + hi0[i]) * (int64_t)p.W + wo * p.stride - p.pad) * p.C + achunk * 8;
+      aoff[i] = (int)(((n * p.H + hi0[i]) * (int64_t)p.W + wo * p.stride - p.pad) * p.C + achunk * 8);
     } else {
       hi0[i] = -(1 << 28);  // never in bounds
       wi0[i] = 0;
-      abase[i] = 0;
+      aoff[i] = 0;
     }
   }
   const int64_t Kg = (int64_t)p.R * p.S * p.C;
-  const uint16_t* wrow[B_PER_T];
+  int woff[B_PER_T];
   constexpr int RBK = BN * 2;              // BKN image row bytes (BK rows of BN channels)
   constexpr int KN_RPI = 1024 / RBK;       // rows per glds instruction
 #pragma unroll
@@ -232,13 +246,18 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
       // fills chunk wg_slot(row, lane % chunks) of it)
       const int krow = (wid * B_PER_T + i) * KN_RPI + lane / (RBK / 16);
       const int kchunk = wg_slot<RBK>(krow, lane % (RBK / 16));
-      wrow[i] = p.w + (int64_t)krow * p.Rw * p.Sw * p.Cout + n0 + kchunk * 8;
+      woff[i] = krow * p.Rw * p.Sw * p.Cout + n0 + kchunk * 8;
     } else {
       const int brow = (wid * B_PER_T + i) * 8 + (lane >> 3);
       const int bchunk = (lane & 7) ^ ((brow >> 1) & 7);
-      wrow[i] = p.w + (int64_t)(n0 + brow) * Kg + bchunk * 8;
+      woff[i] = (int)((n0 + brow) * Kg) + bchunk * 8;
     }
   }
+  constexpr uint32_t kOOB = 0xFFFFFF00u;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.x, 0, (int)((uint32_t)p.N * (uint32_t)(p.H * p.W * p.C) * 2u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.w, 0, (int)((uint32_t)(BKN ? p.Rw * p.Sw : p.R * p.S) * (uint32_t)(p.C * p.Cout) * 2u), 0x00020000);
 
   const int cblocks = p.C >= BK ? p.C / BK : 1;
   const int tps = p.C >= BK ? 1 : BK / p.C;  // taps per K-step (narrow inputs)
@@ -250,25 +269,23 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   auto stage = [&](int ks, int buf) {
     const int rs = (ks / cblocks) * tps, cb = ks - (ks / cblocks) * cblocks;
     const int r = rs / p.S, s = rs - r * p.S;
-    const int64_t koff = ((int64_t)r * p.W + s) * p.C + cb * BK;
+    const int koff = (r * p.W + s) * p.C + cb * BK;
     unsigned char* a = lds + buf * STAGE;
     unsigned char* b = a + A_BYTES;
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       const int hi = hi0[i] + r, wi = wi0[i] + s;
-      const bool ok = (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
-      const void* src = ok ? (const void*)(p.x + abase[i] + koff) : (const void*)g_conv_zero16;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(a + (wid * A_PER_T + i) * 1024),
-                                       16, 0, 0);
+      const bool ok = ((unsigned)hi < (unsigned)p.H) & ((unsigned)wi < (unsigned)p.W);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(a + (wid * A_PER_T + i) * 1024),
+                                               16, ok ? (uint32_t)(aoff[i] + koff) * 2u : kOOB, 0, 0, 0);
     }
     // BKN: rows co = cb*BK + krow, mapped tap (tr0 + trs*r, ts0 + tss*s)
-    const int64_t wk = BKN ? ((int64_t)cb * BK * p.Rw * p.Sw + (p.tr0 + p.trs * r) * p.Sw + (p.ts0 + p.tss * s)) * p.Cout
-                           : (int64_t)ks * BK;  // k = (r*S + s)*C + c: K-step ks is [64ks, 64ks+64)
+    const int wk = BKN ? (cb * BK * p.Rw * p.Sw + (p.tr0 + p.trs * r) * p.Sw + (p.ts0 + p.tss * s)) * p.Cout
+                       : ks * BK;  // k = (r*S + s)*C + c: K-step ks is [64ks, 64ks+64)
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(wrow[i] + wk),
-                                       (__attribute__((address_space(3))) void*)(b + (wid * B_PER_T + i) * 1024),
-                                       16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(b + (wid * B_PER_T + i) * 1024),
+                                               16, (uint32_t)(woff[i] + wk) * 2u, 0, 0, 0);
   };
 
   f32x16_t acc[MI][NI];
@@ -367,8 +384,10 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
         const uint32_t u = cpack<F16>(v);
         const uint16_t h0 = (uint16_t)u, h1 = (uint16_t)(u >> 16);
         if (LDSEPI) {
-          *reinterpret_cast<uint16_t*>(lds + r0 * C_STRIDE + col * 2) = h0;
-          *reinterpret_cast<uint16_t*>(lds + (r0 + 1) * C_STRIDE + col * 2) = h1;
+          if (!HALF) {
+            *reinterpret_cast<uint16_t*>(lds + r0 * C_STRIDE + col * 2) = h0;
+            *reinterpret_cast<uint16_t*>(lds + (r0 + 1) * C_STRIDE + col * 2) = h1;
+          }
         } else {
           if (m0 + r0 < p.M) p.y[(m0 + r0) * p.Cout + n0 + col] = h0;
           if (m0 + r0 + 1 < p.M) p.y[(m0 + r0 + 1) * p.Cout + n0 + col] = h1;
@@ -381,7 +400,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
         }
       }
     }
-  float* red = reinterpret_cast<float*>(lds + (LDSEPI ? BM * C_STRIDE : 0));  // [2][WM][BN]
+  float* red = reinterpret_cast<float*>(lds + (LDSEPI ? EROWS * C_STRIDE : 0));  // [2][WM][BN]
   if (stats) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -415,7 +434,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   if (LDSEPI) {
     constexpr int CPR = BN / 8;          // 16-byte chunks per output row
     constexpr int RPP = NT / CPR;  // rows per pass
-    constexpr int NPASS = BM / RPP;
+    constexpr int NPASS = EROWS / RPP;
     // global operands of the BN epilogues are loaded a group of passes at a time, before any
     // store of the group (the output may alias nothing, but the compiler cannot know that)
     constexpr int GRP = NPASS < 4 ? NPASS : 4;
@@ -443,13 +462,37 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
       const int a = (int)(rem / (uint32_t)p.Wo), b = (int)(rem - (uint32_t)a * (uint32_t)p.Wo);
       return ((int64_t)img * p.oH + 2 * a + p.oph) * p.oW + 2 * b + p.opw;
     };
+    for (int half = 0; half < (HALF ? 2 : 1); ++half) {
+    if (HALF) {
+      // this half's 64 rows: the waves that own them round their accumulators into the image
+      if (half) __syncthreads();  // every thread is done reading the first half
+      if ((wm * MI * 32) / 64 == half) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int col = wn * 64 + j * 32 + lr;
+            const int rbase = wm * (MI * 32) + i * 32 + 4 * lh - half * 64;
+#pragma unroll
+            for (int e = 0; e < 16; e += 2) {
+              const int r0 = rbase + (e & 3) + 8 * (e >> 2);
+              const f32x2_t v = {acc[i][j][e], acc[i][j][e + 1]};
+              const uint32_t u = cpack<F16>(v);
+              *reinterpret_cast<uint16_t*>(lds + r0 * C_STRIDE + col * 2) = (uint16_t)u;
+              *reinterpret_cast<uint16_t*>(lds + (r0 + 1) * C_STRIDE + col * 2) = (uint16_t)(u >> 16);
+            }
+          }
+      }
+      __syncthreads();
+    }
+    const int64_t mh = m0 + half * EROWS;  // first global row of the image
 #pragma unroll
     for (int g0 = 0; g0 < NPASS; g0 += GRP) {
       uint4 xv[GRP], yv[GRP], rv[GRP], x2v[GRP];
       if (BNB) {
 #pragma unroll
         for (int q = 0; q < GRP; ++q) {
-          const int64_t m = m0 + (g0 + q) * RPP + orow;
+          const int64_t m = mh + (g0 + q) * RPP + orow;
           const int64_t off = grow(m < p.M ? m : 0) * p.Cout + n0 + oc * 8;
           xv[q] = *reinterpret_cast<const uint4*>(p.bnx + off);
           if (BNR) {
@@ -463,7 +506,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
 #pragma unroll
       for (int q = 0; q < GRP; ++q) {
         const int row = (g0 + q) * RPP + orow;
-        const int64_t m = m0 + row;
+        const int64_t m = mh + row;
         if (m < p.M) {
           uint4 v = *reinterpret_cast<const uint4*>(lds + row * C_STRIDE + oc * 16);
           if (BNB) {
@@ -524,6 +567,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
         }
       }
     }
+    }  // half
     if (BNB) {
       // threads sharing a channel group: orow = tid / CPR -> lanes l, l+CPR, ... of a wave, then
       // the NW waves through LDS (the epilogue image is no longer read: reuse its space)
@@ -1398,10 +1442,20 @@ void conv_set_big(int on) { g_conv_big = on; }
 
 // Launch one conv_fwd_kernel instantiation in the element type of a.f16 (fp16 is instantiated
 // for the production 128-row, 1-stage, LDS-epilogue variants only).
+// conv_fwd_kernel addresses both operands with 32-bit byte offsets through buffer descriptors
+// (num_records < 2^32, padding reads at offset 0xFFFFFF00).
+static void conv_check_offsets(const ConvFwdArgs& a, bool bkn) {
+  const int64_t xb = (int64_t)a.N * a.H * a.W * a.C * 2;
+  const int64_t wb = (int64_t)(bkn ? a.Rw * a.Sw : a.R * a.S) * a.C * a.Cout * 2;
+  if (xb >= 0xFFFFFF00ll || wb >= 0x7FFFFFFFll)
+    throw std::runtime_error("conv: operand tensors beyond 2^31 elements are not supported");
+}
+
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
           bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, int NT = conv::kThreads>
 static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdArgs& a) {
   const dim3 block(NT);
+  conv_check_offsets(a, BKN);
   if constexpr (BMT == 128 && STAGES == 1 && LDSEPI && NT == conv::kThreads) {
     if (a.f16) {
       hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, STAGES, LDSEPI, BKN, STATS, BNB, BNR, REMAP, ZSIB, BNR2, true>),
@@ -1460,6 +1514,7 @@ int conv_fwd_splits_for(int64_t M, int Cout, int64_t K, bool graph, int* kps_out
 template <int BN, bool STATS, bool BNB, bool BNR, bool BNR2, bool BKN = false, bool REMAP = false, bool ZSIB = false>
 static void split_launch(const ConvFwdArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)(a.m_tiles * a.n_tiles * a.splits)), block(conv::kThreads);
+  conv_check_offsets(a, BKN);
   // the main loop's epilogue flags do not matter (SPLIT returns before it): one instantiation
   if (a.f16)
     hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, BKN, false, false, false, false, false, false, true,
