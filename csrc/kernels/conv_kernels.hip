@@ -36,6 +36,9 @@
 namespace dpt {
 
 
+#ifndef DPT_WGRAD_WAVES  // backward-weight occupancy target (waves per SIMD) for the 4-wave tiles
+#define DPT_WGRAD_WAVES 4
+#endif
 #ifndef DPT_CONV_HALF_EPI
 #define DPT_CONV_HALF_EPI 0
 #endif
@@ -1006,7 +1009,7 @@ struct ConvWgradArgs {
 // NT = 256: 2 x 2 waves; NT = 512 (256 x 256 tiles): 2 x 4 waves of 128 x 64 - twice the MFMA
 // work per staged byte, one block per CU.
 template <int BMW, int BNW, int STAGES, bool F16 = false, int NT = conv::kThreads>
-__global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(ConvWgradArgs p) {
+__global__ __launch_bounds__(NT, (NT == conv::kThreads && BNW <= 128) ? DPT_WGRAD_WAVES : 2) void conv_wgrad_kernel(ConvWgradArgs p) {
   using namespace conv;
   constexpr int NW = NT / 64;
   constexpr int WNW = NT == 512 ? 4 : 2, WMW = NW / WNW;  // waves along N / M
@@ -1059,23 +1062,41 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(ConvWgradArgs p) {
   int aoff[A_INSTR];
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) aoff[i] = (k0 * BKP + arow[i]) * p.Cout + co0 + achk[i] * 8;
-  int bm[B_INSTR], bh[B_INSTR], bw[B_INSTR], bsub[B_INSTR], boff[B_INSTR];
+  // Narrow inputs (C < BNW): the tile holds tps consecutive taps t = rs + sub, sub = this
+  // chunk's (chunk*8)/C, anywhere in the R x S window (a tile may span tap rows - the 16-tap
+  // 4x4 stem in one 256-column tile - and the last tile may run past R*S: ragged, those taps
+  // read zeros and are not stored).  A lane's chunk is fixed, so its tap offset (bdr, bds)
+  // from the block's base tap (r, s) and its address delta are constants.
+  const int bm0 = k0 * BKP + brow[0];  // rows of one lane differ by compile-time constants
+  int bh[B_INSTR], bw[B_INSTR], bdr[B_INSTR], bds[B_INSTR], boff[B_INSTR];
 #pragma unroll
   for (int i = 0; i < B_INSTR; ++i) {
     const int m = k0 * BKP + brow[i];
-    bm[i] = m;
-    bsub[i] = tps > 1 ? bchk[i] * 8 / p.C : 0;  // narrow inputs: this chunk's tap
+    int delta = bchk[i] * 8;
+    bdr[i] = 0; bds[i] = 0;
+    if (tps > 1) {
+      const int sub = bchk[i] * 8 / p.C, t = rs + sub;
+      if (t < p.R * p.S) {
+        const int tr = t / p.S, ts = t - tr * p.S;
+        bdr[i] = tr - r; bds[i] = ts - s;
+      } else {
+        bdr[i] = -(1 << 28);  // past the last tap: never in bounds
+      }
+      delta = (bdr[i] * p.W + bds[i]) * p.C + (bchk[i] * 8 - sub * p.C);
+      if (t >= p.R * p.S) delta = 0;
+    }
     if (p.direct) {
       bh[i] = 0; bw[i] = 0;
-      boff[i] = m * p.C + ci0 + bchk[i] * 8;
+      boff[i] = m * p.C + ci0 + delta;
     } else {
       const int n = m / (p.Ho * p.Wo), rem = m - n * (p.Ho * p.Wo);
       const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
       bh[i] = ho * p.stride - p.pad + r;
       bw[i] = wo * p.stride - p.pad + s;
-      boff[i] = ((n * p.H + bh[i]) * p.W + bw[i]) * p.C + ci0 + bchk[i] * 8;
+      boff[i] = ((n * p.H + bh[i]) * p.W + bw[i]) * p.C + ci0 + delta;
     }
   }
+  int bm = bm0;
   const int wlim = p.Wo * p.stride - p.pad + s;  // wo >= Wo
   const int hlim = p.Ho * p.stride - p.pad + r;  // ho >= Ho
   const int adelta = BKP * p.Cout;
@@ -1101,11 +1122,11 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(ConvWgradArgs p) {
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i) {
       // bitwise, not short-circuit: no exec-mask branches around the select
-      const bool ok = (bm[i] < p.M) & ((p.direct != 0) | (((unsigned)bh[i] < (unsigned)p.H) &
-                                                        ((unsigned)(bw[i] + bsub[i]) < (unsigned)p.W)));
+      const bool ok = (bm + (brow[i] - brow[0]) < p.M) &
+                      ((p.direct != 0) | (((unsigned)(bh[i] + bdr[i]) < (unsigned)p.H) &
+                                          ((unsigned)(bw[i] + bds[i]) < (unsigned)p.W)));
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(b + (wid * B_INSTR + i) * 1024),
                                                16, ok ? (uint32_t)boff[i] * 2u : kOOB, 0, 0, 0);
-      bm[i] += BKP;
       boff[i] += dp_step;
       if (!p.direct) {  // "c ? v + k : v" forms: one add + one v_cndmask each
         bw[i] += p.dw_step;
@@ -1118,6 +1139,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(ConvWgradArgs p) {
         boff[i] = ch ? boff[i] + p.dp_hwrap : boff[i];
       }
     }
+    bm += BKP;
   };
 
   f32x16_t acc[MI][NI];
@@ -1176,6 +1198,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(ConvWgradArgs p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int col = wn * WTN + j * 32 + lr;
+      if ((int64_t)nt * BNW + col >= Kg) continue;  // ragged last tile: taps past R*S
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int row = co0 + wm * WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
@@ -1885,10 +1908,14 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
   pl.Wo = Wo > 0 ? Wo : (W + 2 * pad - S) / stride + 1;
   const int64_t M = (int64_t)N * pl.Ho * pl.Wo;
   pl.bmw = Cout % 128 == 0 ? 128 : 64;
-  pl.bnw = C % 128 == 0 ? 128 : 64;
+  // column tile: 128 input channels of one tap; 64-channel inputs take two taps per tile (a
+  // ragged last tile for odd tap counts: 3x3 -> 5 tiles, 1/9 of the MFMA work wasted, twice
+  // the MFMA work per staged dy tile); the 16-channel space-to-depth stem takes all 16 taps of
+  // its 4x4 window in one 256-column tile (dy staged once instead of four times)
+  pl.bnw = C % 128 == 0 ? 128 : (C == 64 && R * S > 1) ? 128 : (C == 16 && R * S * C >= 256 && pl.bmw == 64) ? 256 : 64;
   // variant 12 (A/B): 8-wave 256 x 256 tiles where both channel counts allow them
   if (conv_variant() == 12 && Cout % 256 == 0 && C % 256 == 0) pl.bmw = pl.bnw = 256;
-  const int tiles = (Cout / pl.bmw) * (R * S * C / pl.bnw);
+  const int tiles = (Cout / pl.bmw) * ((R * S * C + pl.bnw - 1) / pl.bnw);
   const int steps = (int)((M + 63) / 64);
   // ~768 blocks (3 per CU) and at least 32 K-steps per split: a split's fp32 partial tile
   // (BMW x BNW x 4 B, written once and read once by the reduce) then costs < 1/8 of the
@@ -1914,7 +1941,7 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
   a.Ho = pl.Ho; a.Wo = pl.Wo;
   a.M = N * pl.Ho * pl.Wo;
   a.co_tiles = Cout / pl.bmw;
-  a.n_tiles = R * S * C / pl.bnw;
+  a.n_tiles = (R * S * C + pl.bnw - 1) / pl.bnw;
   a.splits = pl.splits;
   a.steps_per_split = pl.steps_per_split;
   a.div_wo = make_fastdiv((uint32_t)pl.Wo);
@@ -1942,7 +1969,7 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
   if (pl.bmw == 256) {  // conv_wgrad_plan chose the 8-wave 256 x 256 tile
     if (a.f16) throw std::runtime_error("conv_wgrad: the 256 x 256 variant is bf16 only");
     hipLaunchKernelGGL((conv_wgrad_kernel<256, 256, 2, false, 512>), grid, dim3(512), 0, st, a);
-  } else if (v == 1 || v == 2) {
+  } else if ((v == 1 || v == 2) && pl.bnw <= 128) {
     if (pl.bmw == 128 && pl.bnw == 128) wgrad_launch<128, 128, 2>(grid, block, st, a);
     else if (pl.bmw == 128) wgrad_launch<128, 64, 2>(grid, block, st, a);
     else if (pl.bnw == 128) wgrad_launch<64, 128, 2>(grid, block, st, a);
@@ -1950,6 +1977,7 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
   } else {
     if (pl.bmw == 128 && pl.bnw == 128) wgrad_launch<128, 128, 1>(grid, block, st, a);
     else if (pl.bmw == 128) wgrad_launch<128, 64, 1>(grid, block, st, a);
+    else if (pl.bnw == 256) wgrad_launch<64, 256, 1>(grid, block, st, a);
     else if (pl.bnw == 128) wgrad_launch<64, 128, 1>(grid, block, st, a);
     else wgrad_launch<64, 64, 1>(grid, block, st, a);
   }

@@ -671,3 +671,26 @@ def test_big_tile_auto_matches_128_tiles(cuda, shape):
     torch.testing.assert_close(outs[0][3].float(), dref, rtol=1e-2, atol=2e-2)
     for a, b in zip(*outs):
         torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * b.float().abs().max().item() + 1e-3)
+
+
+@pytest.mark.parametrize("shape", [
+    # N, C, H, W, Cout, k, stride, pad
+    (3, 16, 29, 29, 64, 4, 1, 0),     # space-to-depth stem shape: 16 taps of 16 channels in one 256-col tile
+    (2, 16, 12, 11, 64, 4, 1, 2),     # ... with padding on every side
+    (2, 64, 10, 10, 64, 3, 1, 1),     # 64-channel 3x3: 2 taps per tile, ragged 5th tile
+    (2, 64, 9, 9, 128, 3, 2, 1),      # ... strided
+    (2, 64, 7, 7, 64, 5, 1, 2),       # 25 taps: 13 tiles, the last one half empty
+])
+@pytest.mark.parametrize("fp32_out", [True, False])
+def test_conv_wgrad_multi_tap_tiles(cuda, shape, fp32_out):
+    """Backward-weight tiles holding several taps (conv_wgrad_plan: 64-channel inputs take two
+    taps per 128-column tile, the 16-channel stem all 16 taps per 256-column tile; taps past
+    R*S in the last tile read zeros and are not stored) against the fp32 reference."""
+    N, C, H, W, Cout, k, s, p = shape
+    x, w = _operands(cuda, N, C, H, W, Cout, k, seed=13)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    gy = torch.randn(N, Cout, Ho, Wo, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    dw = ops.native().conv_wgrad(gy, x, list(w.shape), s, p, fp32_out)
+    ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, gy.float(), stride=s, padding=p)
+    scale = ref.abs().max().item()
+    torch.testing.assert_close(dw.float(), ref, rtol=1e-2, atol=1e-3 * scale + 1e-3)
