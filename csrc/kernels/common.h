@@ -30,12 +30,11 @@ __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
   return __uint_as_float(((uint32_t)b) << 16);
 }
 
-// Round-to-nearest-even f32 -> bf16 (NaN stays a quiet NaN).
+// Round-to-nearest-even f32 -> bf16 (NaN stays a NaN): the plain cast is the hardware
+// v_cvt_pk_bf16_f32 on gfx950 - one instruction instead of the integer rounding sequence and
+// its exec-masked NaN branch (MI355X_MICROARCH.md, Correctness boundaries).
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
 
 __device__ __forceinline__ float f16_to_f32(uint16_t h) {
