@@ -1516,17 +1516,28 @@ int conv_fwd_splits(int64_t M, int Cout, int64_t K, int* kps_out, hipStream_t s)
   return conv_fwd_splits_for(M, Cout, K, capturing, kps_out);
 }
 
+// Thresholds of the policy below (DPT_CONV_SPLIT_TILES / _EAGER_TILES / _TARGET override them
+// for A/B runs): split grids of fewer than kSplitTiles tiles (eagerly: at most kSplitEager
+// tiles with >= 24 K-steps) to about kSplitTarget blocks.
+static int split_knob(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
 int conv_fwd_splits_for(int64_t M, int Cout, int64_t K, bool graph, int* kps_out) {
+  static const int kSplitTiles = split_knob("DPT_CONV_SPLIT_TILES", 160);
+  static const int kSplitEager = split_knob("DPT_CONV_SPLIT_EAGER_TILES", 32);
+  static const int kSplitTarget = split_knob("DPT_CONV_SPLIT_TARGET", 512);
   const int n_tiles = Cout % 128 == 0 ? Cout / 128 : Cout / 64;
   const int64_t tiles = (int64_t)conv_m_tiles(M) * n_tiles;
   const int nk = (int)(K / conv::BK);
   if (kps_out) *kps_out = nk;
   const int mode = splitk_mode();
-  if (mode == 0 || tiles >= 160 || nk < 4) return 1;
+  if (mode == 0 || tiles >= kSplitTiles || nk < 4) return 1;
   // Eager launches are host-bound at these sizes: the extra epilogue launch only pays where the
   // single-block K loop is long (tens of microseconds); inside a hipGraph capture it always does.
-  if (!graph && mode == 1 && (tiles > 32 || nk < 24)) return 1;
-  const int want = (int)((512 + tiles - 1) / tiles);
+  if (!graph && mode == 1 && (tiles > kSplitEager || nk < 24)) return 1;
+  const int want = (int)((kSplitTarget + tiles - 1) / tiles);
   const int kps = std::max(2, (nk + want - 1) / want);
   const int splits = (nk + kps - 1) / kps;
   if (splits <= 1) return 1;
