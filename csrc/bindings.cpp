@@ -249,6 +249,24 @@ void same_16(const Tensor& a, const Tensor& b, const char* op) {
   TORCH_CHECK(a.scalar_type() == b.scalar_type(), op, ": operands must share one 16-bit dtype (bf16 or fp16)");
 }
 
+// A backward-weight whose split-K reduce has not run yet (conv_wgrad_deferred): it keeps the
+// partials alive until a backward-data launch takes the reduce into its grid's tail
+// (dpt::AttachWgradReduce) or conv_reduce_flush launches it on its own.
+struct PendingReduce {
+  Tensor part, dw;
+  dpt::WgradReduce r{};
+  bool done() const { return r.consumed; }
+};
+using PendingReducePtr = std::shared_ptr<PendingReduce>;
+
+// Scoped attach of an optional pending reduce to the conv launches of one binding call.
+struct MaybeAttach {
+  std::unique_ptr<dpt::AttachWgradReduce> g;
+  MaybeAttach(const PendingReducePtr& p, hipStream_t s) {
+    if (p && !p->r.consumed) g = std::make_unique<dpt::AttachWgradReduce>(&p->r, s);
+  }
+};
+
 // Returns {y, psum, psq} (psum/psq empty unless want_stats): y = conv2d(x, w, stride, pad).
 // out_h/out_w > 0: explicit output size, no larger than the symmetric-padding one (the extra
 // padding rows/columns at the bottom/right are dropped: asymmetric padding).
@@ -312,7 +330,7 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
                                        c10::optional<Tensor> bn_coef,
                                        c10::optional<Tensor> bn_y, c10::optional<Tensor> bn_res,
                                        c10::optional<Tensor> w_flipped, c10::optional<Tensor> bn_x2,
-                                       c10::optional<Tensor> bn_mean2) {
+                                       c10::optional<Tensor> bn_mean2, PendingReducePtr wgrad_reduce) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
   check_cl_bf16(bn_x, "bn_x");
@@ -362,6 +380,7 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
   if (!pre)
     dpt::launch_conv_wt_flip(reinterpret_cast<const uint16_t*>(w.data_ptr()), reinterpret_cast<uint16_t*>(wt.data_ptr()),
                              Cout, R, S, C, st);
+  MaybeAttach att(wgrad_reduce, st);
   dpt::launch_conv_dgrad_bnstats(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                                  reinterpret_cast<const uint16_t*>(wt.data_ptr()), reinterpret_cast<uint16_t*>(dx.data_ptr()),
                                  N, Ho, Wo, Cout, C, R, S, (int)pad, reinterpret_cast<const uint16_t*>(bn_x.data_ptr()),
@@ -378,7 +397,8 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
 
 // Stride-2 backward-data: dx [N, C, H, W] (channels_last) of y = conv2d(x, w, stride 2, pad).
 std::vector<Tensor> conv_dgrad_s2(Tensor dy, Tensor w, int64_t pad, int64_t H, int64_t W, c10::optional<Tensor> bn_x,
-                                  c10::optional<Tensor> bn_mean, c10::optional<Tensor> bn_coef) {
+                                  c10::optional<Tensor> bn_mean, c10::optional<Tensor> bn_coef,
+                                  PendingReducePtr wgrad_reduce) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
   same_16(dy, w, "conv_dgrad_s2");
@@ -401,6 +421,7 @@ std::vector<Tensor> conv_dgrad_s2(Tensor dy, Tensor w, int64_t pad, int64_t H, i
     p1 = at::empty({C, plan.chunks}, dy.options().dtype(at::kFloat));
     p2 = at::empty({C, plan.chunks}, dy.options().dtype(at::kFloat));
   }
+  MaybeAttach att(wgrad_reduce, cur_stream(dy));
   dpt::launch_conv_dgrad_s2(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
                             reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, (int)pad, (int)H, (int)W,
                             cur_stream(dy), bnb ? reinterpret_cast<const uint16_t*>(bn_x->data_ptr()) : nullptr,
@@ -442,7 +463,7 @@ std::vector<Tensor> conv_wt_flip_multi(std::vector<Tensor> ws) {
 }
 
 // Stride-1 backward-data through an already flipped/transposed weight (conv_wt_flip_multi).
-Tensor conv_dgrad_preflipped(Tensor dy, Tensor wt, int64_t pad) {
+Tensor conv_dgrad_preflipped(Tensor dy, Tensor wt, int64_t pad, PendingReducePtr wgrad_reduce) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(wt, "w_flipped");
   same_16(dy, wt, "conv_dgrad_preflipped");
@@ -454,6 +475,7 @@ Tensor conv_dgrad_preflipped(Tensor dy, Tensor wt, int64_t pad) {
                       dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   c10::hip::HIPGuard guard(dy.device().index());
   Tensor ws = splitk_ws(dy, dx.size(0) * dx.size(2) * dx.size(3), C, (int64_t)R * S * Cout);
+  MaybeAttach att(wgrad_reduce, cur_stream(dy));
   dpt::launch_conv_fwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                        reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, 1, (int)(R - 1 - pad),
                        nullptr, nullptr, cur_stream(dy), 0, 0, is_f16(dy), ws.defined() ? ws.data_ptr<float>() : nullptr);
@@ -462,7 +484,7 @@ Tensor conv_dgrad_preflipped(Tensor dy, Tensor wt, int64_t pad) {
 
 // Same through an explicitly flipped/transposed weight copy (returned too): the reference
 // path the tests compare the folded addressing against.
-std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad) {
+std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad, PendingReducePtr wgrad_reduce) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
   same_16(dy, w, "conv_dgrad_flip");
@@ -479,6 +501,7 @@ std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad) {
   auto dx = at::empty({N, C, Ho + R - 1 - 2 * (int)pad, Wo + S - 1 - 2 * (int)pad},
                       dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor ws = splitk_ws(dy, dx.size(0) * dx.size(2) * dx.size(3), C, (int64_t)R * S * Cout);
+  MaybeAttach att(wgrad_reduce, st);
   dpt::launch_conv_fwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                        reinterpret_cast<uint16_t*>(dx.data_ptr()), N, Ho, Wo, Cout, C, R, S, 1, (int)(R - 1 - pad),
                        nullptr, nullptr, st, 0, 0, is_f16(dy), ws.defined() ? ws.data_ptr<float>() : nullptr);
@@ -486,7 +509,9 @@ std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad) {
 }
 
 // dw = conv2d backward-weight (fp32 or bf16 output, KRSC = channels_last [Cout, C, R, S]).
-Tensor conv_wgrad(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stride, int64_t pad, bool fp32_out) {
+// pending != nullptr: a split-K reduce is left for a backward-data launch (conv_wgrad_deferred).
+Tensor conv_wgrad_impl(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stride, int64_t pad, bool fp32_out,
+                       PendingReduce* pending) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(x, "x");
   same_16(dy, x, "conv_wgrad");
@@ -509,8 +534,33 @@ Tensor conv_wgrad(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stri
   c10::hip::HIPGuard guard(x.device().index());
   dpt::launch_conv_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
                          part.data_ptr<float>(), dw.data_ptr(), fp32_out ? 0 : (is_f16(x) ? 2 : 1), N, H, W, C, Cout, R,
-                         S, (int)stride, (int)pad, pl, cur_stream(x), is_f16(x));
+                         S, (int)stride, (int)pad, pl, cur_stream(x), is_f16(x), pending ? &pending->r : nullptr);
+  if (pending) {
+    pending->part = part;
+    pending->dw = dw;
+  }
   return dw;
+}
+
+Tensor conv_wgrad(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stride, int64_t pad, bool fp32_out) {
+  return conv_wgrad_impl(dy, x, wshape, stride, pad, fp32_out, nullptr);
+}
+
+// (dw, pending): the backward-weight kernel is launched, its split-K reduce (if the plan needs
+// one) is not - pass `pending` to the conv's backward-data binding (wgrad_reduce=) to run it in
+// that launch's tail, or conv_reduce_flush it.  pending is None when nothing is left to do.
+py::tuple conv_wgrad_deferred(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stride, int64_t pad) {
+  auto p = std::make_shared<PendingReduce>();
+  Tensor dw = conv_wgrad_impl(dy, x, wshape, stride, pad, false, p.get());
+  if (p->r.consumed) return py::make_tuple(dw, py::none());
+  return py::make_tuple(dw, p);
+}
+
+void conv_reduce_flush(PendingReducePtr p) {
+  if (!p || p->r.consumed) return;
+  c10::hip::HIPGuard guard(p->part.device().index());
+  dpt::launch_wgrad_reduce(p->r, cur_stream(p->part));
+  p->r.consumed = true;
 }
 
 // a = im2col(x) as a channels_last [N, Kp, Ho, Wo] bf16 tensor (x: channels_last fp32/bf16)
@@ -1074,15 +1124,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad_bnstats", &conv_dgrad_bnstats, py::arg("grad_output"), py::arg("w"), py::arg("pad"),
         py::arg("bn_x"), py::arg("bn_mean"), py::arg("bn_coef"), py::arg("bn_y") = py::none(),
         py::arg("bn_res") = py::none(), py::arg("w_flipped") = py::none(), py::arg("bn_x2") = py::none(),
-        py::arg("bn_mean2") = py::none());
+        py::arg("bn_mean2") = py::none(), py::arg("wgrad_reduce") = nullptr);
   m.def("conv_wt_flip_multi", &conv_wt_flip_multi, py::arg("ws"));
-  m.def("conv_dgrad_preflipped", &conv_dgrad_preflipped, py::arg("grad_output"), py::arg("w_flipped"), py::arg("pad"));
+  m.def("conv_dgrad_preflipped", &conv_dgrad_preflipped, py::arg("grad_output"), py::arg("w_flipped"), py::arg("pad"),
+        py::arg("wgrad_reduce") = nullptr);
   m.def("bn_bwd_partials", &bn_bwd_partials, py::arg("grad_output"), py::arg("x"), py::arg("weight"), py::arg("mean"),
         py::arg("invstd"), py::arg("coef"), py::arg("p1"), py::arg("p2"), py::arg("want_dparams"),
         py::arg("from_dz") = false);
   m.def("conv_dgrad_s2", &conv_dgrad_s2, py::arg("grad_output"), py::arg("w"), py::arg("pad"), py::arg("H"),
-        py::arg("W"), py::arg("bn_x") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_coef") = py::none());
-  m.def("conv_dgrad_flip", &conv_dgrad_flip, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
+        py::arg("W"), py::arg("bn_x") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_coef") = py::none(),
+        py::arg("wgrad_reduce") = nullptr);
+  m.def("conv_dgrad_flip", &conv_dgrad_flip, py::arg("grad_output"), py::arg("w"), py::arg("pad"),
+        py::arg("wgrad_reduce") = nullptr);
+  py::class_<PendingReduce, PendingReducePtr>(m, "PendingWgradReduce")
+      .def_property_readonly("done", &PendingReduce::done)
+      .def_property_readonly("splits", [](const PendingReduce& p) { return p.r.splits; });
+  m.def("conv_wgrad_deferred", &conv_wgrad_deferred, py::arg("grad_output"), py::arg("x"), py::arg("weight_shape"),
+        py::arg("stride"), py::arg("pad"));
+  m.def("conv_reduce_flush", &conv_reduce_flush, py::arg("pending"));
   m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
 
   // Collective seam (comm.h): RcclComm (production) and HostBridgeComm (ranks sharing a GPU)

@@ -126,7 +126,27 @@ struct ConvFwdArgs {
   // the epilogue (16-bit rounding, BN statistics, BNB/BNR) the unsplit kernel would have run
   float* part;
   int splits, kps;
+  // Piggybacked backward-weight reduce: the last red_blocks blocks of the grid sum the split-K
+  // partials of a backward-weight launched just before (the same conv's) instead of computing a
+  // conv tile - the reduce runs in this kernel's tail, without a launch of its own
+  // (AttachWgradReduce, kernels.h).  red_blocks = 0: none.
+  const float4* red_part = nullptr;
+  void* red_out = nullptr;
+  int64_t red_n4 = 0;
+  int red_splits = 0, red_kind = 0, red_blocks = 0, red_ph = 1;
 };
+
+// out[v] = sum_s part[s][v] for the float4s v of reduce block `bid`: PH phases per block split
+// the S loop, `red` (kBlock float4s of LDS) combines them.  Shared by the standalone reduce
+// kernel and the piggybacked blocks of conv_fwd_kernel.
+template <int PH>
+__device__ __forceinline__ void wgrad_reduce_body(const float4* __restrict__ part, int64_t n4, int S,
+                                                  void* __restrict__ out, int out_kind, int bid, float4* red);
+__device__ __forceinline__ void wgrad_reduce_any(const ConvFwdArgs& p, int bid, float4* red) {
+  if (p.red_ph == 16) wgrad_reduce_body<16>(p.red_part, p.red_n4, p.red_splits, p.red_out, p.red_kind, bid, red);
+  else if (p.red_ph == 4) wgrad_reduce_body<4>(p.red_part, p.red_n4, p.red_splits, p.red_out, p.red_kind, bid, red);
+  else wgrad_reduce_body<1>(p.red_part, p.red_n4, p.red_splits, p.red_out, p.red_kind, bid, red);
+}
 
 // K-major operands (rows of the LDS image = k) use the transposing reads and the swizzle of
 // mfma.h: wg_frag is its natural-k-order tr_frag.
@@ -194,6 +214,15 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   constexpr int LDS_EPI = (LDSEPI ? EROWS * C_STRIDE : 0) + RED;
   constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS];
+  if constexpr (NT == conv::kThreads) {
+    if (p.red_blocks) {  // piggybacked backward-weight reduce blocks (ConvFwdArgs::red_*)
+      const int nconv = (int)gridDim.x - p.red_blocks;
+      if ((int)blockIdx.x >= nconv) {
+        wgrad_reduce_any(p, (int)blockIdx.x - nconv, reinterpret_cast<float4*>(lds));
+        return;
+      }
+    }
+  }
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -1207,14 +1236,12 @@ __global__ __launch_bounds__(NT, (NT == conv::kThreads && BNW <= 128) ? DPT_WGRA
     }
 }
 
-// out[i] = sum_s part[s][i]: PH phases per block split the S loop, LDS combines them.
 template <int PH>
-__global__ __launch_bounds__(kBlock) void conv_wgrad_reduce_kernel(const float4* __restrict__ part, int64_t n4,
-                                                                   int S, void* __restrict__ out, int out_kind) {
+__device__ __forceinline__ void wgrad_reduce_body(const float4* __restrict__ part, int64_t n4, int S,
+                                                  void* __restrict__ out, int out_kind, int bid, float4* red) {
   constexpr int OUT = kBlock / PH;
-  __shared__ float4 red[kBlock];
   const int o = threadIdx.x % OUT, ph = threadIdx.x / OUT;
-  const int64_t v = (int64_t)blockIdx.x * OUT + o;
+  const int64_t v = (int64_t)bid * OUT + o;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (v < n4) {
     int q = ph;
@@ -1252,6 +1279,14 @@ __global__ __launch_bounds__(kBlock) void conv_wgrad_reduce_kernel(const float4*
     w.y = (uint32_t)f32_to_bf16(a.z) | ((uint32_t)f32_to_bf16(a.w) << 16);
     static_cast<uint2*>(out)[v] = w;
   }
+}
+
+// out[i] = sum_s part[s][i]: PH phases per block split the S loop, LDS combines them.
+template <int PH>
+__global__ __launch_bounds__(kBlock) void conv_wgrad_reduce_kernel(const float4* __restrict__ part, int64_t n4,
+                                                                   int S, void* __restrict__ out, int out_kind) {
+  __shared__ float4 red[kBlock];
+  wgrad_reduce_body<PH>(part, n4, S, out, out_kind, (int)blockIdx.x, red);
 }
 
 // ---- narrow-input convs (the 3-channel stem): explicit im2col -> the 1x1 MFMA GEMM ---------------
@@ -1474,10 +1509,55 @@ static void conv_check_offsets(const ConvFwdArgs& a, bool bkn) {
     throw std::runtime_error("conv: operand tensors beyond 2^31 elements are not supported");
 }
 
+// ---- piggybacked backward-weight reduce (AttachWgradReduce, kernels.h) -------------------------
+static thread_local WgradReduce* g_attached_reduce = nullptr;
+
+static int reduce_phases(int splits) { return splits >= 16 ? 16 : splits >= 4 ? 4 : 1; }
+
+void launch_wgrad_reduce(const WgradReduce& r, hipStream_t st) {
+  const float4* part = reinterpret_cast<const float4*>(r.part);
+  const int ph = reduce_phases(r.splits), out_per_block = kBlock / ph;
+  const dim3 grid((unsigned)((r.n4 + out_per_block - 1) / out_per_block)), block(kBlock);
+  if (ph == 16) hipLaunchKernelGGL(conv_wgrad_reduce_kernel<16>, grid, block, 0, st, part, r.n4, r.splits, r.out, r.kind);
+  else if (ph == 4) hipLaunchKernelGGL(conv_wgrad_reduce_kernel<4>, grid, block, 0, st, part, r.n4, r.splits, r.out, r.kind);
+  else hipLaunchKernelGGL(conv_wgrad_reduce_kernel<1>, grid, block, 0, st, part, r.n4, r.splits, r.out, r.kind);
+}
+
+AttachWgradReduce::AttachWgradReduce(WgradReduce* r, hipStream_t s) : r_(r), s_(s) {
+  if (g_attached_reduce != nullptr) throw std::runtime_error("AttachWgradReduce: a reduce is already attached");
+  g_attached_reduce = (r != nullptr && !r->consumed) ? r : nullptr;
+}
+
+AttachWgradReduce::~AttachWgradReduce() {
+  g_attached_reduce = nullptr;
+  if (r_ != nullptr && !r_->consumed) {
+    launch_wgrad_reduce(*r_, s_);
+    r_->consumed = true;
+  }
+}
+
+// The attached reduce (if any) moves into `a`: returns the blocks to append to the grid.
+static int take_attached_reduce(ConvFwdArgs& a) {
+  WgradReduce* r = g_attached_reduce;
+  if (r == nullptr || r->consumed) return 0;
+  r->consumed = true;
+  g_attached_reduce = nullptr;
+  a.red_part = reinterpret_cast<const float4*>(r->part);
+  a.red_out = r->out;
+  a.red_n4 = r->n4;
+  a.red_splits = r->splits;
+  a.red_kind = r->kind;
+  a.red_ph = reduce_phases(r->splits);
+  a.red_blocks = (int)((r->n4 + kBlock / a.red_ph - 1) / (kBlock / a.red_ph));
+  return a.red_blocks;
+}
+
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
           bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, int NT = conv::kThreads>
-static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdArgs& a) {
+static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdArgs& a0) {
   const dim3 block(NT);
+  ConvFwdArgs a = a0;
+  if constexpr (NT == conv::kThreads) grid.x += (unsigned)take_attached_reduce(a);
   conv_check_offsets(a, BKN);
   if constexpr (BMT == 128 && STAGES == 1 && LDSEPI && NT == conv::kThreads) {
     if (a.f16) {
@@ -1547,15 +1627,16 @@ int conv_fwd_splits_for(int64_t M, int Cout, int64_t K, bool graph, int* kps_out
 
 template <int BN, bool STATS, bool BNB, bool BNR, bool BNR2, bool BKN = false, bool REMAP = false, bool ZSIB = false>
 static void split_launch(const ConvFwdArgs& a, hipStream_t s) {
-  const dim3 grid((unsigned)(a.m_tiles * a.n_tiles * a.splits)), block(conv::kThreads);
+  ConvFwdArgs am = a;  // the main kernel takes an attached backward-weight reduce, the epilogue not
+  const dim3 grid((unsigned)(a.m_tiles * a.n_tiles * a.splits + take_attached_reduce(am))), block(conv::kThreads);
   conv_check_offsets(a, BKN);
   // the main loop's epilogue flags do not matter (SPLIT returns before it): one instantiation
   if (a.f16)
     hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, BKN, false, false, false, false, false, false, true,
-                                        conv::kThreads, true>), grid, block, 0, s, a);
+                                        conv::kThreads, true>), grid, block, 0, s, am);
   else
     hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, BKN, false, false, false, false, false, false, false,
-                                        conv::kThreads, true>), grid, block, 0, s, a);
+                                        conv::kThreads, true>), grid, block, 0, s, am);
   const dim3 egrid((unsigned)((a.M + kSplitRows - 1) / kSplitRows), (unsigned)(a.Cout / 64));
   if (a.f16)
     hipLaunchKernelGGL((conv_split_epilogue_kernel<STATS, BNB, BNR, BNR2, REMAP, ZSIB, true>), egrid, dim3(256), 0, s,
@@ -1943,10 +2024,11 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
 
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void* dw, int dw_kind, int N, int H,
                        int W, int C, int Cout, int R, int S, int stride, int pad, const ConvWgradPlan& pl,
-                       hipStream_t st, bool f16) {
+                       hipStream_t st, bool f16, WgradReduce* defer) {
   ConvWgradArgs a;
   a.f16 = f16 ? 1 : 0;
   const bool direct_out = pl.splits == 1 && dw_kind == 0;  // fp32 result written in place
+  if (defer != nullptr) defer->consumed = true;              // nothing pending unless set below
   a.dy = dy; a.x = x; a.part = direct_out ? static_cast<float*>(dw) : part;
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S; a.stride = stride; a.pad = pad;
   a.Ho = pl.Ho; a.Wo = pl.Wo;
@@ -1993,17 +2075,9 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
     else wgrad_launch<64, 64, 1>(grid, block, st, a);
   }
   if (direct_out) return;
-  const int64_t n4 = (int64_t)Cout * R * S * C / 4;
-  if (pl.splits >= 16) {
-    hipLaunchKernelGGL(conv_wgrad_reduce_kernel<16>, dim3((unsigned)((n4 + 15) / 16)), dim3(kBlock), 0, st,
-                       reinterpret_cast<const float4*>(part), n4, pl.splits, dw, dw_kind);
-  } else if (pl.splits >= 4) {
-    hipLaunchKernelGGL(conv_wgrad_reduce_kernel<4>, dim3((unsigned)((n4 + 63) / 64)), dim3(kBlock), 0, st,
-                       reinterpret_cast<const float4*>(part), n4, pl.splits, dw, dw_kind);
-  } else {
-    hipLaunchKernelGGL(conv_wgrad_reduce_kernel<1>, dim3((unsigned)((n4 + 255) / 256)), dim3(kBlock), 0, st,
-                       reinterpret_cast<const float4*>(part), n4, pl.splits, dw, dw_kind);
-  }
+  const WgradReduce r{part, dw, (int64_t)Cout * R * S * C / 4, pl.splits, dw_kind, false};
+  if (defer != nullptr) *defer = r;
+  else launch_wgrad_reduce(r, st);
 }
 
 void launch_conv_wt_flip(const uint16_t* w, uint16_t* wt, int Cout, int R, int S, int C, hipStream_t s) {

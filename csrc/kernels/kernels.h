@@ -162,9 +162,36 @@ struct ConvWgradPlan {
 };
 ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad, int Ho = 0,
                               int Wo = 0);
+// The split-K reduce of a backward-weight (partials [splits][n4 float4s] -> out, kind as dw_kind).
+struct WgradReduce {
+  const float* part;
+  void* out;
+  int64_t n4;
+  int splits, kind;
+  bool consumed;
+};
+void launch_wgrad_reduce(const WgradReduce& r, hipStream_t s);
+// defer != nullptr: the reduce is not launched but described in *defer (consumed = false) when
+// the plan needs one, for a conv backward-data launch to run in its tail (AttachWgradReduce).
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void* dw, int dw_kind, int N, int H,
                        int W, int C, int Cout, int R, int S, int stride, int pad, const ConvWgradPlan& plan,
-                       hipStream_t s, bool f16 = false);
+                       hipStream_t s, bool f16 = false, WgradReduce* defer = nullptr);
+// Scoped hand-over of a deferred backward-weight reduce (host thread-local, one binding call):
+// while the guard lives, the next 256-thread conv_fwd_kernel launch on this thread (forward,
+// backward-data, split-K main kernel) appends the reduce's blocks to its grid and marks it
+// consumed; the destructor launches it standalone on `s` if nothing did.  Saves the reduce's
+// own launch and ramp (53 per ResNet-50 step): its blocks fill the conv's tail.
+class AttachWgradReduce {
+ public:
+  AttachWgradReduce(WgradReduce* r, hipStream_t s);
+  ~AttachWgradReduce();
+  AttachWgradReduce(const AttachWgradReduce&) = delete;
+  AttachWgradReduce& operator=(const AttachWgradReduce&) = delete;
+
+ private:
+  WgradReduce* r_;
+  hipStream_t s_;
+};
 // stride-1 backward-data (flipped weight wt [C,R,S,Cout]) + the backward statistics of the
 // BatchNorm+ReLU (input bnx, mean, coef [a|b]) that produced the conv's input: bp1/bp2 [C][m_tiles]
 void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int Ho, int Wo, int Cout,

@@ -40,6 +40,9 @@ _BNB_PARTIALS = {}
 _GEN = [0]
 # Stride-2 backward-data on the MFMA kernels (four parity-class convs); 0 = MIOpen
 S2_DGRAD = os.environ.get("DPT_S2_DGRAD", "1") != "0"
+# Backward-weight before backward-data, its split-K reduce run by extra blocks in the
+# backward-data launch's tail (conv_wgrad_deferred / wgrad_reduce=): no reduce launch of its own
+WGRAD_REDUCE_FUSE = os.environ.get("DPT_WGRAD_REDUCE_FUSE", "1") != "0"
 # The im2col stem path is correct but measured slower than MIOpen on ResNet-50's 7x7/2 stem at
 # batch 256 (the [3.2M x 192] bf16 patch matrix is 1.2 GB written and read twice): opt-in only.
 STEM_ENABLED = os.environ.get("DPT_NATIVE_STEM", "0") == "1"
@@ -75,14 +78,20 @@ def _backward(ctx, dy):
     x, w = ctx.saved_tensors
     dy = _cl(dy.to(x.dtype))
     s, p = ctx.stride, ctx.pad
-    dx = dw = None
+    dx = dw = red = None
+    if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[0] and WGRAD_REDUCE_FUSE:
+            dw, red = native().conv_wgrad_deferred(dy, x, list(w.shape), s, p)
+        else:
+            dw = native().conv_wgrad(dy, x, list(w.shape), s, p, False)
     if ctx.needs_input_grad[0]:
         src = ctx.bn_src if (s == 1 and BN_BWD_FUSE) else None
         dres = None
         wt = _flipped(w) if s == 1 else None
         if src is not None and not isinstance(src[2], dict):  # BN+ReLU: (x, mean, coef)
             bn_x, bn_mean, bn_coef = src
-            dx, p1, p2, _ = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, bn_coef, w_flipped=wt)
+            dx, p1, p2, _ = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, bn_coef, w_flipped=wt,
+                                                        wgrad_reduce=red)
             _put_bnb(dx, p1, p2, None, None)
         elif src is not None and _dres_ok(dres := src[2].pop("dres", None), x):  # (x, mean, slot)
             # block-tail BN+add+ReLU (ops/bn.py pair outputs): the next block's tail already
@@ -92,23 +101,26 @@ def _backward(ctx, dy):
             # (x, mean, slot, x2, mean2): the tail's identity path was a downsample BatchNorm
             # folded into it (ops/bn.py _BN2AddReLUPair) - also sum that BN's statistic
             x2, mean2 = (src[3], src[4]) if len(src) > 3 else (None, None)
-            dx, p1, p2, p3 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, None, x, dres, wt, x2, mean2)
+            dx, p1, p2, p3 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, None, x, dres, wt, x2, mean2,
+                                                         wgrad_reduce=red)
             _put_bnb(dx, p1, p2, dres.data_ptr(), p3 if x2 is not None else None)
         elif s == 1:
-            dx = native().conv_dgrad_flip(dy, w, p)[0] if wt is None else native().conv_dgrad_preflipped(dy, wt, p)
+            dx = (native().conv_dgrad_flip(dy, w, p, wgrad_reduce=red)[0] if wt is None
+                  else native().conv_dgrad_preflipped(dy, wt, p, wgrad_reduce=red))
         elif s == 2 and S2_DGRAD and x.dim() == 4:
             src = ctx.bn_src if BN_BWD_FUSE else None
             if src is not None and not isinstance(src[2], dict) and w.shape[2] > 1:
                 # BN+ReLU input: its backward statistics from the parity-class epilogues too
-                dx, p1, p2 = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3], src[0], src[1], src[2])
+                dx, p1, p2 = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3], src[0], src[1], src[2],
+                                                    wgrad_reduce=red)
                 _put_bnb(dx, p1, p2, None, None)
             else:
-                dx = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3])[0]
+                dx = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3], wgrad_reduce=red)[0]
         else:
             dx = torch.ops.aten.convolution_backward(dy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
                                                      (True, False, False))[0]
-    if ctx.needs_input_grad[1]:
-        dw = native().conv_wgrad(dy, x, list(w.shape), s, p, False)
+    if red is not None and not red.done:
+        native().conv_reduce_flush(red)   # no native backward-data launch took it
     if dx is not None and ctx.res_slot is not None:
         # x is the identity alias of a fused block tail and this conv its downsample: hand the
         # identity-path gradient to the tail's conv-path consumer (see ops/bn.py)

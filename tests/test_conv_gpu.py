@@ -694,3 +694,54 @@ def test_conv_wgrad_multi_tap_tiles(cuda, shape, fp32_out):
     ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, gy.float(), stride=s, padding=p)
     scale = ref.abs().max().item()
     torch.testing.assert_close(dw.float(), ref, rtol=1e-2, atol=1e-3 * scale + 1e-3)
+
+
+# (N, C, H, W, Cout, k, stride, pad, dgrad path): every backward-data launcher that can take a
+# deferred backward-weight reduce into its grid's tail
+PIGGY_CASES = [
+    (8, 64, 28, 28, 64, 1, 1, 0, "preflipped"),   # many splits (PH = 16)
+    (2, 128, 9, 9, 256, 3, 1, 1, "flip"),         # few splits (PH = 1 / 4)
+    (2, 64, 15, 15, 128, 3, 2, 1, "s2"),          # stride 2: first parity-class launch takes it
+    (3, 64, 9, 9, 64, 1, 2, 0, "s2"),             # 1x1/2: zero-class (ZSIB) launch
+    (4, 512, 7, 7, 2048, 1, 1, 0, "preflipped"),  # eager split-K backward-data? (small grid)
+    (2, 64, 12, 12, 128, 3, 1, 1, "bnstats"),
+]
+
+
+@pytest.mark.parametrize("case", PIGGY_CASES, ids=[f"{c[-1]}-{c[1]}x{c[2]}-k{c[5]}s{c[6]}" for c in PIGGY_CASES])
+def test_wgrad_reduce_piggybacked_on_dgrad(cuda, case):
+    """conv_wgrad_deferred + a backward-data launch with wgrad_reduce=: the weight gradient is
+    bit-identical to conv_wgrad's (same partials, same reduce body), the input gradient to the
+    plain launch's, and the pending reduce is marked consumed (no second launch)."""
+    N, C, H, W, Cout, k, s, p, path = case
+    C_ = ops.native()
+    x, w = _operands(cuda, N, C, H, W, Cout, k, seed=7)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    gy = torch.randn(N, Cout, Ho, Wo, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    dw_ref = C_.conv_wgrad(gy, x, list(w.shape), s, p, False)
+    bn_x = torch.randn_like(x)
+    bn_mean = torch.randn(C, device=cuda)
+    bn_coef = torch.randn(2 * C, device=cuda)
+
+    def dgrad(red):
+        if path == "preflipped":
+            wt = C_.conv_wt_flip_multi([w])[0]
+            return C_.conv_dgrad_preflipped(gy, wt, p, wgrad_reduce=red)
+        if path == "flip":
+            return C_.conv_dgrad_flip(gy, w, p, wgrad_reduce=red)[0]
+        if path == "s2":
+            return C_.conv_dgrad_s2(gy, w, p, H, W, wgrad_reduce=red)[0]
+        return C_.conv_dgrad_bnstats(gy, w, p, bn_x, bn_mean, bn_coef, wgrad_reduce=red)[0]
+
+    dx_ref = dgrad(None)
+    dw, red = C_.conv_wgrad_deferred(gy, x, list(w.shape), s, p)
+    assert red is not None and not red.done, "every case here needs a split-K reduce"
+    dx = dgrad(red)
+    assert red.done
+    torch.cuda.synchronize()
+    assert torch.equal(dw.view(torch.int16), dw_ref.view(torch.int16)), (dw.float() - dw_ref.float()).abs().max()
+    assert torch.equal(dx.view(torch.int16), dx_ref.view(torch.int16))
+    # a pending reduce nobody took is launched by conv_reduce_flush
+    dw2, red2 = C_.conv_wgrad_deferred(gy, x, list(w.shape), s, p)
+    C_.conv_reduce_flush(red2)
+    assert red2.done and torch.equal(dw2.view(torch.int16), dw_ref.view(torch.int16))
