@@ -348,6 +348,11 @@ def test_weight_flip_multi_and_preflipped_dgrad(cuda):
     w, wt = ws[1], wts[1]
     gy = torch.randn(2, 128, 9, 9, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
     assert torch.equal(ops.native().conv_dgrad_preflipped(gy, wt, 1), ops.native().conv_dgrad_flip(gy, w, 1)[0])
+    # a batch with a channel count off the 64 grid takes the per-element gather kernel instead of
+    # the 64 x 64 LDS tiles
+    odd = [ws[0], torch.randn(72, 40, 3, 3, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)]
+    for w, wt in zip(odd, ops.native().conv_wt_flip_multi(odd)):
+        assert torch.equal(wt, w.flip(2, 3).transpose(0, 1).contiguous(memory_format=CL))
 
 
 def test_downsample_bn_folded_into_block_tail(cuda, monkeypatch):
