@@ -25,6 +25,7 @@
 // -> fp64 per-channel sums in a finalize kernel (one wave per 2 channels).  No atomics.
 #include <cstdlib>
 
+#include "carry.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -156,37 +157,6 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_stats_kernel(const void* __rest
   }
 }
 
-// Sum `chunks` partials of channel c with 32 lanes (one half-wave) in fp64.  Eight
-// independent loads in flight per lane: the partials are L2-resident, so this loop is
-// latency-bound, not bandwidth-bound.
-__device__ __forceinline__ void half_wave_sum2(const float* p1, const float* p2, int64_t c, int chunks,
-                                               int part, double& s1, double& s2) {
-  constexpr int U = 8;
-  double a[U], b[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) { a[u] = 0.0; b[u] = 0.0; }
-  const float* q1 = p1 + c * chunks;
-  const float* q2 = p2 + c * chunks;
-  int k = part;
-  for (; k + 32 * (U - 1) < chunks; k += 32 * U) {
-    float x[U], y[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) { x[u] = q1[k + 32 * u]; y[u] = q2[k + 32 * u]; }
-#pragma unroll
-    for (int u = 0; u < U; ++u) { a[u] += (double)x[u]; b[u] += (double)y[u]; }
-  }
-  for (; k < chunks; k += 32) { a[0] += (double)q1[k]; b[0] += (double)q2[k]; }
-  s1 = 0.0;
-  s2 = 0.0;
-#pragma unroll
-  for (int u = 0; u < U; ++u) { s1 += a[u]; s2 += b[u]; }
-#pragma unroll
-  for (int off = 16; off > 0; off >>= 1) {
-    s1 += __shfl_xor(s1, off, 64);
-    s2 += __shfl_xor(s2, off, 64);
-  }
-}
-
 __global__ __launch_bounds__(kBlock) void bn_fwd_finalize_kernel(
     const float* __restrict__ psum, const float* __restrict__ psq, int chunks, int C, int64_t M,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
@@ -222,35 +192,6 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_finalize_kernel(
 // Wave-reduced fp64 sums of two contiguous fp32 rows of `chunks` partials (one block per
 // channel): 8 loads of each row in flight per thread - the finalize is a latency chain of
 // chunks / (kBlock * U) dependent round trips, not a bandwidth problem.
-__device__ __forceinline__ void block_row_sum2(const float* __restrict__ q1, const float* __restrict__ q2,
-                                               int chunks, double& s, double& q) {
-  constexpr int U = 8;
-  double a[U], b[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) { a[u] = 0.0; b[u] = 0.0; }
-  int k = threadIdx.x;
-  for (; k + (U - 1) * kBlock < chunks; k += U * kBlock) {
-    float x[U], y[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) { x[u] = q1[k + u * kBlock]; y[u] = q2[k + u * kBlock]; }
-#pragma unroll
-    for (int u = 0; u < U; ++u) { a[u] += (double)x[u]; b[u] += (double)y[u]; }
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int kk = k + u * kBlock;
-    if (kk < chunks) { a[u] += (double)q1[kk]; b[u] += (double)q2[kk]; }
-  }
-  s = 0.0;
-  q = 0.0;
-#pragma unroll
-  for (int u = 0; u < U; ++u) { s += a[u]; q += b[u]; }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    s += __shfl_xor(s, off, 64);
-    q += __shfl_xor(q, off, 64);
-  }
-}
 
 __global__ __launch_bounds__(kBlock) void bn_fwd_finalize_wide_kernel(
     const float* __restrict__ psum, const float* __restrict__ psq, int chunks, int C, int64_t M,
@@ -452,25 +393,30 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_stats_kernel(const void* __rest
   }
 }
 
-__global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(
-    const float* __restrict__ p1, const float* __restrict__ p2, int chunks, int C, int64_t M,
-    const float* __restrict__ gamma, const float* __restrict__ invstd, float* dgamma, float* dbeta,
-    float* k1, float* k2, float* k3) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t c = (int64_t)blockIdx.x * 8 + wave * 2 + (lane >> 5);
-  const int part = lane & 31;
-  if (c >= C) return;
-  double s1, s2;
-  half_wave_sum2(p1, p2, c, chunks, part, s1, s2);
-  if (part != 0) return;
-  const double is = (double)invstd[c];
-  const double g = gamma ? (double)gamma[c] : 1.0;
-  if (dgamma) dgamma[c] = (float)(s2 * is);
-  if (dbeta) dbeta[c] = (float)s1;
-  const double a = g * is;
-  k1[c] = (float)a;
-  k2[c] = (float)(-a * is * is * s2 / (double)M);
-  k3[c] = (float)(-a * s1 / (double)M);
+__global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(BnBwdFin f) {
+  __shared__ double red[2 * (kBlock / 64)];
+  bn_bwd_finalize_block(f, (int)blockIdx.x, red);
+}
+
+BnBwdFin make_bn_bwd_fin(const float* p1, const float* p2, int chunks, int C, int64_t M, const float* gamma,
+                         const float* invstd, float* dgamma, float* dbeta, float* k1, float* k2, float* k3,
+                         int wide) {
+  BnBwdFin f;
+  f.p1 = p1; f.p2 = p2; f.chunks = chunks; f.C = C; f.M = M; f.gamma = gamma; f.invstd = invstd;
+  f.dgamma = dgamma; f.dbeta = dbeta; f.k1 = k1; f.k2 = k2; f.k3 = k3;
+  f.wide = wide < 0 ? bn_bwd_fin_wide(chunks) : wide;
+  f.blocks = bn_bwd_fin_blocks(C, f.wide);
+  return f;
+}
+
+static void launch_bn_bwd_fin(const BnBwdFin& f, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)f.blocks), dim3(kBlock), 0, s, f);
+}
+
+void launch_bn_bwd_finalize(const BnBwdFinArgs& a, hipStream_t s) {
+  launch_bn_bwd_fin(make_bn_bwd_fin(a.p1, a.p2, a.chunks, a.C, a.M, a.gamma, a.invstd, a.dgamma, a.dbeta, a.kbuf,
+                                    a.kbuf + a.C, a.kbuf + 2 * a.C, -1),
+                    s);
 }
 
 // dx = k1*dz + k2*(x - mean) + k3, dz = dy*(y>0) recomputed (RELU; mask from x if MX) or
@@ -484,8 +430,18 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const void* __rest
                                                               const float* __restrict__ k1,
                                                               const float* __restrict__ k2,
                                                               const float* __restrict__ k3, void* dx,
-                                                              int64_t M, int C, int rev) {
+                                                              int64_t M, int C, int rev, ReduceCarry rc) {
+  if (rc.blocks) {  // carried backward-weight reduce (carry.h): the grid's last rc.blocks blocks
+    const int napply = (int)gridDim.x - rc.blocks;
+    if ((int)blockIdx.x >= napply) {
+      __shared__ float4 red[kBlock];
+      carry_reduce(rc, (int)blockIdx.x - napply, red);
+      return;
+    }
+  }
   const int tpr = C >> 3, rpi = kBlock / tpr;
+  // grid-stride over the apply blocks only (carry blocks excluded)
+  const int apply_grid = (int)gridDim.x - rc.blocks;
   const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
   float mu[8], c1[8], c2[8], c3[8], fa[8], fb[8];
 #pragma unroll
@@ -497,7 +453,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const void* __rest
     fa[k] = MX ? coef[cg * 8 + k] : 0.f;
     fb[k] = MX ? coef[C + cg * 8 + k] : 0.f;
   }
-  const int64_t stride = (int64_t)gridDim.x * rpi;
+  const int64_t stride = (int64_t)apply_grid * rpi;
   for (int64_t rf = (int64_t)blockIdx.x * rpi + rr; rf < M; rf += stride) {
     const int64_t r = rev ? M - 1 - rf : rf;  // see bn_fwd_apply_kernel
     float g[8], xv[8], o[8];
@@ -697,13 +653,12 @@ static void bwd_dispatch(bool relu, const void* dy, const void* dy2, const void*
   } else {
     bwd_stats_dispatch<IO, 2>(relu, dy, dy2, y, x, mean, coef, M, C, g, p1, p2, dz, s);
   }
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p2, g.chunks, C, M, gamma,
-                     invstd, dgamma, dbeta, k1, k2, k3);
+  launch_bn_bwd_fin(make_bn_bwd_fin(p1, p2, g.chunks, C, M, gamma, invstd, dgamma, dbeta, k1, k2, k3, 0), s);
   dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
-  if (dz != nullptr) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, true, false>), ga, bl, 0, s, dz, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse);
-  else if (relu && coef) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false, true>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse);
-  else if (relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false, false>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse);
-  else hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, false, false>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse);
+  if (dz != nullptr) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, true, false>), ga, bl, 0, s, dz, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse, ReduceCarry{});
+  else if (relu && coef) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false, true>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse, ReduceCarry{});
+  else if (relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false, false>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse, ReduceCarry{});
+  else hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, false, false>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse, ReduceCarry{});
 }
 
 // dz: if non-null, receives dz = (dy [+ dy2]) * relu_mask (the residual-path gradient);
@@ -727,34 +682,35 @@ void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, co
 
 // Backward finalize over MANY [C][chunks] partials (the dgrad epilogue of the consuming conv
 // writes one per 128 rows): one 256-thread block per channel, fp64 block reduce.
-__global__ __launch_bounds__(kBlock) void bn_bwd_finalize_wide_kernel(
-    const float* __restrict__ p1, const float* __restrict__ p2, int chunks, int C, int64_t M,
-    const float* __restrict__ gamma, const float* __restrict__ invstd, float* dgamma, float* dbeta,
-    float* k1, float* k2, float* k3) {
-  __shared__ double red[2][kBlock / 64];
-  const int c = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  double s1, s2;
-  block_row_sum2(p1 + (int64_t)c * chunks, p2 + (int64_t)c * chunks, chunks, s1, s2);
-  if (lane == 0) { red[0][wave] = s1; red[1][wave] = s2; }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  s1 = 0.0;
-  s2 = 0.0;
-#pragma unroll
-  for (int w = 0; w < kBlock / 64; ++w) { s1 += red[0][w]; s2 += red[1][w]; }
-  const double is = (double)invstd[c];
-  const double g = gamma ? (double)gamma[c] : 1.0;
-  if (dgamma) dgamma[c] = (float)(s2 * is);
-  if (dbeta) dbeta[c] = (float)s1;
-  const double a = g * is;
-  k1[c] = (float)a;
-  k2[c] = (float)(-a * is * is * s2 / (double)M);
-  k3[c] = (float)(-a * s1 / (double)M);
-}
 
 // BN+ReLU backward whose statistics (s1 = sum dz, s2 = sum dz*(x - mean), dz = dy * relu mask)
 // were summed by the dgrad epilogue of the conv that consumed this BN's output: [C][chunks]
 // partials -> finalize -> apply (mask recomputed from x and the forward coefficients).
+void launch_bn_bwd_apply_pre(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* mean,
+                             const float* coef, const float* kbuf, void* dx, hipStream_t s, bool from_dz) {
+  BnGeometry g = bn_geometry(M, C);
+  const float* k1 = kbuf;
+  const float* k2 = k1 + C;
+  const float* k3 = k2 + C;
+  dim3 bl(kBlock);
+  ReduceCarry rc;
+  const int ga = (g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2) +
+                 take_attached_reduce(rc);
+  if (from_dz) {  // dy is already the masked gradient dz (block-tail BN, ops/conv.py BNR)
+    switch (dtype) {
+      case 0: hipLaunchKernelGGL((bn_bwd_apply_kernel<F32, false, true, false>), dim3(ga), bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse, rc); break;
+      case 1: hipLaunchKernelGGL((bn_bwd_apply_kernel<BF16, false, true, false>), dim3(ga), bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse, rc); break;
+      default: hipLaunchKernelGGL((bn_bwd_apply_kernel<F16, false, true, false>), dim3(ga), bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse, rc); break;
+    }
+    return;
+  }
+  switch (dtype) {
+    case 0: hipLaunchKernelGGL((bn_bwd_apply_kernel<F32, true, false, true>), dim3(ga), bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse, rc); break;
+    case 1: hipLaunchKernelGGL((bn_bwd_apply_kernel<BF16, true, false, true>), dim3(ga), bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse, rc); break;
+    default: hipLaunchKernelGGL((bn_bwd_apply_kernel<F16, true, false, true>), dim3(ga), bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse, rc); break;
+  }
+}
+
 void launch_bn_bwd_from_partials(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* gamma,
                                  const float* mean, const float* invstd, const float* coef, const float* p1,
                                  const float* p2, int chunks, float* dgamma, float* dbeta, void* dx, float* kbuf,
@@ -764,26 +720,8 @@ void launch_bn_bwd_from_partials(int dtype, const void* dy, const void* x, int64
   float* k2 = k1 + C;
   float* k3 = k2 + C;
   dim3 bl(kBlock);
-  if (chunks > 256)
-    hipLaunchKernelGGL(bn_bwd_finalize_wide_kernel, dim3((unsigned)C), bl, 0, s, p1, p2, chunks, (int)C, M, gamma,
-                       invstd, dgamma, dbeta, k1, k2, k3);
-  else
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p2, chunks, (int)C, M,
-                       gamma, invstd, dgamma, dbeta, k1, k2, k3);
-  dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
-  if (from_dz) {  // dy is already the masked gradient dz (block-tail BN, ops/conv.py BNR)
-    switch (dtype) {
-      case 0: hipLaunchKernelGGL((bn_bwd_apply_kernel<F32, false, true, false>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
-      case 1: hipLaunchKernelGGL((bn_bwd_apply_kernel<BF16, false, true, false>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
-      default: hipLaunchKernelGGL((bn_bwd_apply_kernel<F16, false, true, false>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
-    }
-    return;
-  }
-  switch (dtype) {
-    case 0: hipLaunchKernelGGL((bn_bwd_apply_kernel<F32, true, false, true>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
-    case 1: hipLaunchKernelGGL((bn_bwd_apply_kernel<BF16, true, false, true>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
-    default: hipLaunchKernelGGL((bn_bwd_apply_kernel<F16, true, false, true>), ga, bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse); break;
-  }
+  launch_bn_bwd_fin(make_bn_bwd_fin(p1, p2, chunks, (int)C, M, gamma, invstd, dgamma, dbeta, k1, k2, k3, -1), s);
+  launch_bn_bwd_apply_pre(dtype, dy, x, M, C, mean, coef, kbuf, dx, s, from_dz);
 }
 
 void launch_bn_apply_aff(int dtype, const void* x, const void* x2, void* y, int64_t M, int64_t C, const float* a,
@@ -809,17 +747,11 @@ void launch_bn2_bwd_from_partials(int dtype, const void* dz, const void* x, cons
   float* k = kbuf;          // [3C] tail
   float* j = kbuf + 3 * C;  // [3C] downsample
   dim3 bl(kBlock);
-  if (chunks > 256) {
-    hipLaunchKernelGGL(bn_bwd_finalize_wide_kernel, dim3((unsigned)C), bl, 0, s, p1, p2, chunks, (int)C, M, gamma,
-                       invstd, dgamma, dbeta, k, k + C, k + 2 * C);
-    hipLaunchKernelGGL(bn_bwd_finalize_wide_kernel, dim3((unsigned)C), bl, 0, s, p1, p3, chunks, (int)C, M, gamma2,
-                       invstd2, dgamma2, dbeta2, j, j + C, j + 2 * C);
-  } else {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p2, chunks, (int)C, M,
-                       gamma, invstd, dgamma, dbeta, k, k + C, k + 2 * C);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, p1, p3, chunks, (int)C, M,
-                       gamma2, invstd2, dgamma2, dbeta2, j, j + C, j + 2 * C);
-  }
+  launch_bn_bwd_fin(make_bn_bwd_fin(p1, p2, chunks, (int)C, M, gamma, invstd, dgamma, dbeta, k, k + C, k + 2 * C, -1),
+                    s);
+  launch_bn_bwd_fin(make_bn_bwd_fin(p1, p3, chunks, (int)C, M, gamma2, invstd2, dgamma2, dbeta2, j, j + C, j + 2 * C,
+                                    -1),
+                    s);
   dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
   switch (dtype) {
     case 0: hipLaunchKernelGGL(bn_bwd_apply2_kernel<F32>, ga, bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, kBnReverse); break;

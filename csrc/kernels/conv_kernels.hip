@@ -29,6 +29,7 @@
 #include <cstdlib>
 #include <stdexcept>
 
+#include "carry.h"
 #include "common.h"
 #include "kernels.h"
 #include "mfma.h"
@@ -126,27 +127,12 @@ struct ConvFwdArgs {
   // the epilogue (16-bit rounding, BN statistics, BNB/BNR) the unsplit kernel would have run
   float* part;
   int splits, kps;
-  // Piggybacked backward-weight reduce: the last red_blocks blocks of the grid sum the split-K
-  // partials of a backward-weight launched just before (the same conv's) instead of computing a
-  // conv tile - the reduce runs in this kernel's tail, without a launch of its own
-  // (AttachWgradReduce, kernels.h).  red_blocks = 0: none.
-  const float4* red_part = nullptr;
-  void* red_out = nullptr;
-  int64_t red_n4 = 0;
-  int red_splits = 0, red_kind = 0, red_blocks = 0, red_ph = 1;
+  // Carried backward-weight reduce (carry.h): the last red.blocks blocks of the grid sum the
+  // split-K partials of a backward-weight launched just before (the same conv's) instead of
+  // computing a conv tile (AttachWgradReduce, kernels.h).  red.blocks = 0: none.
+  ReduceCarry red;
 };
 
-// out[v] = sum_s part[s][v] for the float4s v of reduce block `bid`: PH phases per block split
-// the S loop, `red` (kBlock float4s of LDS) combines them.  Shared by the standalone reduce
-// kernel and the piggybacked blocks of conv_fwd_kernel.
-template <int PH>
-__device__ __forceinline__ void wgrad_reduce_body(const float4* __restrict__ part, int64_t n4, int S,
-                                                  void* __restrict__ out, int out_kind, int bid, float4* red);
-__device__ __forceinline__ void wgrad_reduce_any(const ConvFwdArgs& p, int bid, float4* red) {
-  if (p.red_ph == 16) wgrad_reduce_body<16>(p.red_part, p.red_n4, p.red_splits, p.red_out, p.red_kind, bid, red);
-  else if (p.red_ph == 4) wgrad_reduce_body<4>(p.red_part, p.red_n4, p.red_splits, p.red_out, p.red_kind, bid, red);
-  else wgrad_reduce_body<1>(p.red_part, p.red_n4, p.red_splits, p.red_out, p.red_kind, bid, red);
-}
 
 // K-major operands (rows of the LDS image = k) use the transposing reads and the swizzle of
 // mfma.h: wg_frag is its natural-k-order tr_frag.
@@ -215,10 +201,10 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS];
   if constexpr (NT == conv::kThreads) {
-    if (p.red_blocks) {  // piggybacked backward-weight reduce blocks (ConvFwdArgs::red_*)
-      const int nconv = (int)gridDim.x - p.red_blocks;
+    if (p.red.blocks) {  // carried backward-weight reduce blocks (ConvFwdArgs::red)
+      const int nconv = (int)gridDim.x - p.red.blocks;
       if ((int)blockIdx.x >= nconv) {
-        wgrad_reduce_any(p, (int)blockIdx.x - nconv, reinterpret_cast<float4*>(lds));
+        carry_reduce(p.red, (int)blockIdx.x - nconv, lds);
         return;
       }
     }
@@ -1033,6 +1019,8 @@ struct ConvWgradArgs {
   int dw_step, wwrap, dh_step, hwrap;
   int dp_w, dp_wwrap, dp_h, dp_hwrap;
   int f16;             // fp16 operands (bf16 otherwise)
+  // carried BatchNorm backward finalize (carry.h): the grid's last fin.blocks blocks
+  BnBwdFin fin;
 };
 
 // NT = 256: 2 x 2 waves; NT = 512 (256 x 256 tiles): 2 x 4 waves of 128 x 64 - twice the MFMA
@@ -1053,6 +1041,15 @@ __global__ __launch_bounds__(NT, (NT == conv::kThreads && BNW <= 128) ? DPT_WGRA
   constexpr int MI = WTM / 32, NI = WTN / 32;
   static_assert(MI >= 1 && NI >= 1 && A_INSTR >= 1 && B_INSTR >= 1, "conv_wgrad_kernel: bad tiling");
   __shared__ __attribute__((aligned(16))) unsigned char lds[STAGES * STAGE];
+  if constexpr (NT == conv::kThreads) {
+    if (p.fin.blocks) {  // carried BatchNorm backward finalize blocks (ConvWgradArgs::fin)
+      const int nw = (int)gridDim.x - p.fin.blocks;
+      if ((int)blockIdx.x >= nw) {
+        bn_bwd_finalize_block(p.fin, (int)blockIdx.x - nw, lds);
+        return;
+      }
+    }
+  }
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WNW, wn = wid % WNW;
@@ -1234,51 +1231,6 @@ __global__ __launch_bounds__(NT, (NT == conv::kThreads && BNW <= 128) ? DPT_WGRA
         out[(int64_t)row * Kg + col] = acc[i][j][e];
       }
     }
-}
-
-template <int PH>
-__device__ __forceinline__ void wgrad_reduce_body(const float4* __restrict__ part, int64_t n4, int S,
-                                                  void* __restrict__ out, int out_kind, int bid, float4* red) {
-  constexpr int OUT = kBlock / PH;
-  const int o = threadIdx.x % OUT, ph = threadIdx.x / OUT;
-  const int64_t v = (int64_t)bid * OUT + o;
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (v < n4) {
-    int q = ph;
-    for (; q + 3 * PH < S; q += 4 * PH) {
-      const float4 b0 = part[(int64_t)q * n4 + v], b1 = part[(int64_t)(q + PH) * n4 + v];
-      const float4 b2 = part[(int64_t)(q + 2 * PH) * n4 + v], b3 = part[(int64_t)(q + 3 * PH) * n4 + v];
-      a.x += (b0.x + b1.x) + (b2.x + b3.x);
-      a.y += (b0.y + b1.y) + (b2.y + b3.y);
-      a.z += (b0.z + b1.z) + (b2.z + b3.z);
-      a.w += (b0.w + b1.w) + (b2.w + b3.w);
-    }
-    for (; q < S; q += PH) {
-      const float4 b = part[(int64_t)q * n4 + v];
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-    }
-  }
-  red[threadIdx.x] = a;
-  __syncthreads();
-  if (ph != 0 || v >= n4) return;
-#pragma unroll
-  for (int k = 1; k < PH; ++k) {
-    const float4 b = red[k * OUT + o];
-    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-  }
-  if (out_kind == 0) {
-    static_cast<float4*>(out)[v] = a;
-  } else if (out_kind == 2) {  // fp16
-    uint2 w;
-    w.x = cpack<true>(f32x2_t{a.x, a.y});
-    w.y = cpack<true>(f32x2_t{a.z, a.w});
-    static_cast<uint2*>(out)[v] = w;
-  } else {
-    uint2 w;
-    w.x = (uint32_t)f32_to_bf16(a.x) | ((uint32_t)f32_to_bf16(a.y) << 16);
-    w.y = (uint32_t)f32_to_bf16(a.z) | ((uint32_t)f32_to_bf16(a.w) << 16);
-    static_cast<uint2*>(out)[v] = w;
-  }
 }
 
 // out[i] = sum_s part[s][i]: PH phases per block split the S loop, LDS combines them.
@@ -1593,21 +1545,22 @@ AttachWgradReduce::~AttachWgradReduce() {
   }
 }
 
-// The attached reduce (if any) moves into `a`: returns the blocks to append to the grid.
-static int take_attached_reduce(ConvFwdArgs& a) {
+// The attached reduce (if any) moves into `rc`: returns the blocks to append to the grid.
+int take_attached_reduce(ReduceCarry& rc) {
   WgradReduce* r = g_attached_reduce;
   if (r == nullptr || r->consumed) return 0;
   r->consumed = true;
   g_attached_reduce = nullptr;
-  a.red_part = reinterpret_cast<const float4*>(r->part);
-  a.red_out = r->out;
-  a.red_n4 = r->n4;
-  a.red_splits = r->splits;
-  a.red_kind = r->kind;
-  a.red_ph = reduce_phases(r->splits);
-  a.red_blocks = (int)((r->n4 + kBlock / a.red_ph - 1) / (kBlock / a.red_ph));
-  return a.red_blocks;
+  rc.part = reinterpret_cast<const float4*>(r->part);
+  rc.out = r->out;
+  rc.n4 = r->n4;
+  rc.splits = r->splits;
+  rc.kind = r->kind;
+  rc.ph = reduce_phases(r->splits);
+  rc.blocks = (int)((r->n4 + kBlock / rc.ph - 1) / (kBlock / rc.ph));
+  return rc.blocks;
 }
+static int take_attached_reduce(ConvFwdArgs& a) { return take_attached_reduce(a.red); }
 
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
           bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, int NT = conv::kThreads>
@@ -2081,7 +2034,7 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
 
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void* dw, int dw_kind, int N, int H,
                        int W, int C, int Cout, int R, int S, int stride, int pad, const ConvWgradPlan& pl,
-                       hipStream_t st, bool f16, WgradReduce* defer) {
+                       hipStream_t st, bool f16, WgradReduce* defer, const BnBwdFinArgs* fin) {
   ConvWgradArgs a;
   a.f16 = f16 ? 1 : 0;
   const bool direct_out = pl.splits == 1 && dw_kind == 0;  // fp32 result written in place
@@ -2114,8 +2067,18 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
       a.dp_hwrap = (H * W - pl.Ho * stride * W) * C;
     }
   }
-  const dim3 grid((unsigned)(a.co_tiles * a.n_tiles * a.splits)), block(conv::kThreads);
+  dim3 grid((unsigned)(a.co_tiles * a.n_tiles * a.splits)), block(conv::kThreads);
   const int v = a.f16 ? 0 : conv_variant();
+  if (fin != nullptr) {
+    a.fin = make_bn_bwd_fin(fin->p1, fin->p2, fin->chunks, fin->C, fin->M, fin->gamma, fin->invstd, fin->dgamma,
+                            fin->dbeta, fin->kbuf, fin->kbuf + fin->C, fin->kbuf + 2 * fin->C, -1);
+    if (pl.bmw == 256) {  // the 512-thread variant carries nothing: finalize on its own
+      launch_bn_bwd_finalize(*fin, st);
+      a.fin = BnBwdFin{};
+    } else {
+      grid.x += (unsigned)a.fin.blocks;
+    }
+  }
   if (pl.bmw == 256) {  // conv_wgrad_plan chose the 8-wave 256 x 256 tile
     if (a.f16) throw std::runtime_error("conv_wgrad: the 256 x 256 variant is bf16 only");
     hipLaunchKernelGGL((conv_wgrad_kernel<256, 256, 2, false, 512>), grid, dim3(512), 0, st, a);

@@ -171,11 +171,37 @@ struct WgradReduce {
   bool consumed;
 };
 void launch_wgrad_reduce(const WgradReduce& r, hipStream_t s);
+// A BatchNorm backward finalize (carry.h BnBwdFin): [C][chunks] partials p1 = sum dz,
+// p2 = sum dz*(x - mean) -> dgamma, dbeta (optional) and kbuf = [k1 | k2 | k3] (3C floats).
+struct BnBwdFinArgs {
+  const float* p1;
+  const float* p2;
+  int chunks, C;
+  int64_t M;
+  const float* gamma;  // nullptr: 1
+  const float* invstd;
+  float* dgamma;
+  float* dbeta;
+  float* kbuf;
+};
 // defer != nullptr: the reduce is not launched but described in *defer (consumed = false) when
 // the plan needs one, for a conv backward-data launch to run in its tail (AttachWgradReduce).
+// fin != nullptr: the backward-weight grid also carries that BatchNorm finalize (its blocks
+// run in the backward-weight's tail; standalone for the 8-wave variant).
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void* dw, int dw_kind, int N, int H,
                        int W, int C, int Cout, int R, int S, int stride, int pad, const ConvWgradPlan& plan,
-                       hipStream_t s, bool f16 = false, WgradReduce* defer = nullptr);
+                       hipStream_t s, bool f16 = false, WgradReduce* defer = nullptr,
+                       const BnBwdFinArgs* fin = nullptr);
+void launch_bn_bwd_finalize(const BnBwdFinArgs& f, hipStream_t s);
+// BatchNorm backward apply with precomputed kbuf (launch_bn_bwd_finalize / a carried one):
+// dx = k1*dz + k2*(x - mean) + k3, dz = dy * relu-mask(fma(x, coef_a, coef_b) > 0), or dz = dy
+// when from_dz.  Takes an attached backward-weight reduce into its grid (AttachWgradReduce).
+void launch_bn_bwd_apply_pre(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* mean,
+                             const float* coef, const float* kbuf, void* dx, hipStream_t s, bool from_dz);
+struct ReduceCarry;
+// The reduce attached by a live AttachWgradReduce (if any) is described in rc and marked
+// consumed; returns the carry blocks to append to the launching kernel's grid (0: none).
+int take_attached_reduce(ReduceCarry& rc);
 // Scoped hand-over of a deferred backward-weight reduce (host thread-local, one binding call):
 // while the guard lives, the next 256-thread conv_fwd_kernel launch on this thread (forward,
 // backward-data, split-K main kernel) appends the reduce's blocks to its grid and marks it
