@@ -903,6 +903,27 @@ std::vector<Tensor> maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int
 }
 
 // dx = broadcast of g [N, C] / (H*W) over an [N, C, H, W] channels_last tensor of dtype like_dtype
+// {dz, p1, p2}: global-average-pool backward through a block tail y = relu(bn(x) + res):
+// dz = g/(H*W) * (y > 0) (y's dtype) and the tail BN's backward statistics partials.
+std::vector<Tensor> gap_bwd_bnr(Tensor g, Tensor y, Tensor x, Tensor mean) {
+  TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous(), "gap_bwd_bnr: g must be a contiguous [N, C]");
+  auto [M, C] = bn_rows(y, "y");
+  auto [Mx, Cx] = bn_rows(x, "x");
+  TORCH_CHECK(M == Mx && C == Cx && x.scalar_type() == y.scalar_type() && g.size(1) == C && g.size(0) == y.size(0),
+              "gap_bwd_bnr: shape mismatch");
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "gap_bwd_bnr: needs C/8 | 256");
+  const int64_t N = y.size(0), HW = y.size(2) * y.size(3);
+  auto dz = at::empty_like(y);
+  const int chunks = dpt::gap_bwd_bnr_chunks(M, C);
+  auto p1 = at::empty({C, chunks}, y.options().dtype(at::kFloat));
+  auto p2 = at::empty({C, chunks}, y.options().dtype(at::kFloat));
+  c10::hip::HIPGuard guard(y.device().index());
+  dpt::launch_gap_bwd_bnr(bn_dtype(y), bn_dtype(g), g.data_ptr(), dz.data_ptr(), y.data_ptr(), x.data_ptr(),
+                          f32_param(mean, C, "mean"), N, HW, C, p1.data_ptr<float>(), p2.data_ptr<float>(),
+                          cur_stream(y));
+  return {dz, p1, p2};
+}
+
 Tensor gap_bwd(Tensor g, int64_t H, int64_t W, at::ScalarType dtype) {
   TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() && g.size(1) % 8 == 0, "gap_bwd: g must be [N, C], C % 8 == 0");
   TORCH_CHECK(dtype == at::kFloat || dtype == at::kBFloat16 || dtype == at::kHalf, "gap_bwd: dtype");
@@ -1143,6 +1164,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("stride"), py::arg("pad"),
         py::arg("bn_coef") = py::none());
   m.def("gap_bwd", &gap_bwd, py::arg("g"), py::arg("H"), py::arg("W"), py::arg("dtype"));
+  m.def("gap_bwd_bnr", &gap_bwd_bnr, py::arg("g"), py::arg("y"), py::arg("x"), py::arg("mean"));
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("grad_output"), py::arg("idx"), py::arg("H"), py::arg("W"),
         py::arg("k"), py::arg("stride"), py::arg("pad"), py::arg("grad_output2") = py::none(),
         py::arg("bn_x") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_coef") = py::none());

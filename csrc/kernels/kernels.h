@@ -87,6 +87,11 @@ void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t
                         int Wo, int K, int S, int P, hipStream_t s, const float* coef = nullptr);
 // global-average-pool backward: dx [N, HW, C] (dtype) = g [N, C] (gdtype) / HW
 void launch_gap_bwd(int dtype, int gdtype, const void* g, void* dx, int64_t N, int64_t HW, int64_t C, hipStream_t s);
+// gap_bwd of a block-tail output y (mask) whose BN input is x: dz = g/HW * (y > 0) and that BN's
+// backward statistics partials p1/p2 [C][gap_bwd_bnr_chunks(N*HW, C)]; C/8 must divide 256.
+int gap_bwd_bnr_chunks(int64_t M, int64_t C);
+void launch_gap_bwd_bnr(int dtype, int gdtype, const void* g, void* dz, const void* y, const void* x,
+                        const float* mean, int64_t N, int64_t HW, int64_t C, float* p1, float* p2, hipStream_t s);
 // dy2: optional second output gradient, summed in (pool output with two consumers)
 // bnx/bn_mean/bn_coef (3x3/2/1 pools only): the input was relu(bn(bnx)); also write that BN's
 // backward-statistics partials [C][maxpool_bwd_bn_chunks(...)] to bp1/bp2

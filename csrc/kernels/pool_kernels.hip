@@ -606,6 +606,81 @@ __global__ __launch_bounds__(kBlock) void gap_bwd_kernel(const void* __restrict_
   pool_store8(DT, dx, (int64_t)t * 8, v);
 }
 
+// Global-average-pool backward of a block-tail output y = relu(bn(x) + res) (the network's last
+// residual block): dz = (g[n, c] / HW) * (y > 0) - the tail's masked gradient, stored in the
+// storage type - plus that BatchNorm's backward statistics s1 = sum dz, s2 = sum dz*(x - mean)
+// summed from the stored values, per block of `rpb` rows into [C][gridDim.x] partials.  The
+// BN backward then applies from the partials (no statistics pass over dy, y and x, no separate
+// broadcast pass).  C/8 threads per row, kBlock % (C/8) == 0.
+template <int DT, int GT>
+__global__ __launch_bounds__(kBlock) void gap_bwd_bnr_kernel(const void* __restrict__ g, void* __restrict__ dz,
+                                                             const void* __restrict__ y, const void* __restrict__ x,
+                                                             const float* __restrict__ mean, int64_t M, uint32_t HW,
+                                                             int C, int rpb, float inv, float* __restrict__ p1,
+                                                             float* __restrict__ p2) {
+  __shared__ float red[2][kBlock * 8];
+  const int tpr = C >> 3, rpp = kBlock / tpr;
+  const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
+  float mu[8], s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { mu[k] = mean[cg * 8 + k]; s1[k] = 0.f; s2[k] = 0.f; }
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < M ? r0 + rpb : M;
+  for (int64_t r = r0 + rr; r < r1; r += rpp) {
+    const int64_t n = r / HW, off = r * C + cg * 8;
+    float gv[8], yv[8], xv[8], o[8];
+    pool_load8(GT, g, n * C + cg * 8, gv);
+    pool_load8(DT, y, off, yv);
+    pool_load8(DT, x, off, xv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = yv[k] > 0.0f ? gv[k] * inv : 0.0f;
+    pool_store8(DT, dz, off, o);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      // statistics from the stored (rounded) values: what the BN backward apply reads
+      const float d = DT == 0 ? o[k] : DT == 1 ? bf16_to_f32(f32_to_bf16(o[k])) : f16_to_f32(pool_to16(2, o[k]));
+      s1[k] += d;
+      s2[k] = __builtin_fmaf(d, xv[k] - mu[k], s2[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[0][rr * C + cg * 8 + k] = s1[k];
+    red[1][rr * C + cg * 8 + k] = s2[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += kBlock) {
+    float a1 = 0.f, a2 = 0.f;
+    for (int j = 0; j < rpp; ++j) { a1 += red[0][j * C + c]; a2 += red[1][j * C + c]; }
+    p1[(int64_t)c * gridDim.x + blockIdx.x] = a1;
+    p2[(int64_t)c * gridDim.x + blockIdx.x] = a2;
+  }
+}
+
+int gap_bwd_bnr_chunks(int64_t M, int64_t C) {
+  const int rpp = kBlock / (int)(C / 8);
+  int64_t rpb = (M + 1023) / 1024;  // ~1024 blocks
+  rpb = (rpb + rpp - 1) / rpp * rpp;
+  return (int)((M + rpb - 1) / rpb);
+}
+
+void launch_gap_bwd_bnr(int dtype, int gdtype, const void* g, void* dz, const void* y, const void* x,
+                        const float* mean, int64_t N, int64_t HW, int64_t C, float* p1, float* p2, hipStream_t s) {
+  const int64_t M = N * HW;
+  const int chunks = gap_bwd_bnr_chunks(M, C);
+  const int rpb = (int)((M + chunks - 1) / chunks);
+  const dim3 grid((unsigned)chunks), block(kBlock);
+  const float inv = 1.0f / (float)HW;
+#define DPT_GAPB(D, G) hipLaunchKernelGGL((gap_bwd_bnr_kernel<D, G>), grid, block, 0, s, g, dz, y, x, mean, M, (uint32_t)HW, (int)C, rpb, inv, p1, p2)
+  if (gdtype == 0) {
+    if (dtype == 0) DPT_GAPB(0, 0); else if (dtype == 1) DPT_GAPB(1, 0); else DPT_GAPB(2, 0);
+  } else if (gdtype == 1) {
+    if (dtype == 0) DPT_GAPB(0, 1); else if (dtype == 1) DPT_GAPB(1, 1); else DPT_GAPB(2, 1);
+  } else {
+    if (dtype == 0) DPT_GAPB(0, 2); else if (dtype == 1) DPT_GAPB(1, 2); else DPT_GAPB(2, 2);
+  }
+#undef DPT_GAPB
+}
+
 void launch_gap_bwd(int dtype, int gdtype, const void* g, void* dx, int64_t N, int64_t HW, int64_t C, hipStream_t s) {
   const int64_t total = N * HW * (C / 8);
   if (total == 0) return;

@@ -22,7 +22,7 @@ import torch
 import os
 
 from . import native, native_available
-from .conv import take_bnb_partials
+from .conv import MASKED_NO_RES, take_bnb_partials
 
 # Block-tail BN+add+ReLU backward statistics in the consuming conv's dgrad epilogue (see _bwd)
 BNR_FUSE = os.environ.get("DPT_BNR_FUSE", "1") != "0"
@@ -123,6 +123,16 @@ def _bwd(ctx, dy, dy2):
             else:
                 dx, dg, db = native().bn_bwd_partials(dy, x, weight, mean, invstd, None, part[0], part[1],
                                                       bool(want_params), True)
+            if ctx.res_slot is not None:
+                ctx.res_slot["dres"] = dy
+            return (dx, dy if want_dz else None, dg if want_params else None, db if want_params else None)
+    if dy2 is None and ctx.relu and ctx.has_res:
+        part = take_bnb_partials(dy)
+        if part is not None and part[2] == MASKED_NO_RES:
+            # the last block tail: the average-pool backward formed dz = dy * (y > 0) and summed
+            # the statistics (ops/pool.py gap_bwd_bnr); dz is also the residual gradient
+            dx, dg, db = native().bn_bwd_partials(dy, x, weight, mean, invstd, None, part[0], part[1],
+                                                  bool(want_params), True)
             if ctx.res_slot is not None:
                 ctx.res_slot["dres"] = dy
             return (dx, dy if want_dz else None, dg if want_params else None, db if want_params else None)

@@ -279,10 +279,16 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bo
     return y
 
 
-def register_bnb_partials(dx: torch.Tensor, p1: torch.Tensor, p2: torch.Tensor) -> None:
-    """Hand BN+ReLU backward-statistics partials summed by dx's producer to the BN backward
-    that receives dx as its output gradient (other producers than convs: the stem pool)."""
-    _put_bnb(dx, p1, p2, None, None)
+# dres_ptr of an entry whose gradient is a block tail's already-masked gradient with no
+# identity-path gradient folded in (the last tail, whose output only fed the average pool)
+MASKED_NO_RES = -1
+
+
+def register_bnb_partials(dx: torch.Tensor, p1: torch.Tensor, p2: torch.Tensor, masked: bool = False) -> None:
+    """Hand BN backward-statistics partials summed by dx's producer to the BN backward that
+    receives dx as its output gradient (other producers than convs: the stem pool for BN+ReLU;
+    the average-pool backward for the last block tail, ``masked``: dx is already dz)."""
+    _put_bnb(dx, p1, p2, MASKED_NO_RES if masked else None, None)
 
 
 def take_bnb_partials(dy: torch.Tensor):

@@ -99,12 +99,30 @@ class _GlobalAvgPoolNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
         ctx.cfg = (x.shape[2], x.shape[3], x.dtype)
+        # x is the output of the network's last fused block tail (ops/bn.py: (BN input, mean,
+        # slot), no downsample BN folded in): the backward also forms that tail's masked
+        # gradient and sums its BN statistics (gap_bwd_bnr), as a conv's backward-data epilogue
+        # does for every other tail - the BN backward then skips its statistics pass
+        src = x.__dict__.get("_dpt_bn_src")
+        from .conv import BN_BWD_FUSE
+        ctx.bn_src = None
+        if (BN_BWD_FUSE and src is not None and len(src) == 3 and isinstance(src[2], dict)
+                and x.dtype in (torch.bfloat16, torch.float16) and 256 % (x.shape[1] // 8) == 0):
+            ctx.bn_src = src
+            ctx.save_for_backward(x)
         return torch.nn.functional.adaptive_avg_pool2d(x, 1)
 
     @staticmethod
     def backward(ctx, g):
         H, W, dt = ctx.cfg
-        return native().gap_bwd(g.reshape(g.shape[0], g.shape[1]).contiguous(), H, W, dt)
+        g2 = g.reshape(g.shape[0], g.shape[1]).contiguous()
+        if ctx.bn_src is not None:
+            from .conv import register_bnb_partials
+            (y,) = ctx.saved_tensors
+            dz, p1, p2 = native().gap_bwd_bnr(g2, y, ctx.bn_src[0], ctx.bn_src[1])
+            register_bnb_partials(dz, p1, p2, masked=True)
+            return dz
+        return native().gap_bwd(g2, H, W, dt)
 
 
 def gap_supported(x: torch.Tensor) -> bool:

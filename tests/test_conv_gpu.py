@@ -810,3 +810,38 @@ def test_bn_backward_run_by_consuming_conv_is_bitwise(cuda, monkeypatch, ds):
     assert len(calls) == 3
     for a, b in zip(*grads):
         assert torch.equal(a, b), (a.float() - b.float()).abs().max()
+
+
+@pytest.mark.parametrize("C,hw", [(2048, 7), (512, 4)])
+def test_last_tail_statistics_from_avgpool_backward(cuda, monkeypatch, C, hw):
+    """The network's last block tail feeds the global average pool: its backward forms the
+    tail's masked gradient dz = g/HW * (y > 0) and sums the BN statistics (gap_bwd_bnr), the BN
+    backward applies from the partials.  Gradients must match the unfused path (broadcast pass +
+    the BN backward's own statistics pass) up to summation order."""
+    from distributed_pytorch_training_amd.ops import bn as fbn
+    from distributed_pytorch_training_amd.ops import conv as nc
+    from distributed_pytorch_training_amd.ops import pool as fpool
+
+    g = torch.Generator(device=cuda).manual_seed(13)
+    N = 8
+    x0 = torch.randn(N, C, hw, hw, device=cuda, generator=g).to(torch.bfloat16).contiguous(memory_format=CL)
+    r0 = torch.randn(N, C, hw, hw, device=cuda, generator=g).to(torch.bfloat16).contiguous(memory_format=CL)
+    w0 = torch.rand(C, device=cuda, generator=g) + 0.5
+    b0 = torch.randn(C, device=cuda, generator=g) * 0.1
+    head = torch.randn(N, C, device=cuda, generator=g)
+    res = []
+    for fuse in (True, False):
+        monkeypatch.setattr(nc, "BN_BWD_FUSE", fuse)
+        nc.reset_side_channels()
+        x, r = x0.clone().requires_grad_(True), r0.clone().requires_grad_(True)
+        w, b = w0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+        nb = torch.zeros((), dtype=torch.long, device=cuda)
+        yc, _ = fbn.bn_act_train(x, r, w, b, rm, rv, nb, 0.1, 1e-5, True, True)
+        pooled = fpool.global_avg_pool_nhwc(yc).flatten(1)
+        (pooled.float() * head).sum().backward()
+        torch.cuda.synchronize()
+        assert not nc._BNB_PARTIALS
+        res.append([x.grad.float(), r.grad.float(), w.grad, b.grad])
+    for a, ref in zip(*res):
+        torch.testing.assert_close(a, ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item() + 1e-6)
