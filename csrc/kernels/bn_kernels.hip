@@ -398,6 +398,13 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(BnBwdFin f) {
   bn_bwd_finalize_block(f, (int)blockIdx.x, red);
 }
 
+// Two BatchNorms' finalizes in one launch (a block tail with its downsample BN folded in)
+__global__ __launch_bounds__(kBlock) void bn_bwd_finalize2_kernel(BnBwdFin f, BnBwdFin h) {
+  __shared__ double red[2 * (kBlock / 64)];
+  if ((int)blockIdx.x < f.blocks) bn_bwd_finalize_block(f, (int)blockIdx.x, red);
+  else bn_bwd_finalize_block(h, (int)blockIdx.x - f.blocks, red);
+}
+
 BnBwdFin make_bn_bwd_fin(const float* p1, const float* p2, int chunks, int C, int64_t M, const float* gamma,
                          const float* invstd, float* dgamma, float* dbeta, float* k1, float* k2, float* k3,
                          int wide) {
@@ -747,11 +754,10 @@ void launch_bn2_bwd_from_partials(int dtype, const void* dz, const void* x, cons
   float* k = kbuf;          // [3C] tail
   float* j = kbuf + 3 * C;  // [3C] downsample
   dim3 bl(kBlock);
-  launch_bn_bwd_fin(make_bn_bwd_fin(p1, p2, chunks, (int)C, M, gamma, invstd, dgamma, dbeta, k, k + C, k + 2 * C, -1),
-                    s);
-  launch_bn_bwd_fin(make_bn_bwd_fin(p1, p3, chunks, (int)C, M, gamma2, invstd2, dgamma2, dbeta2, j, j + C, j + 2 * C,
-                                    -1),
-                    s);
+  const BnBwdFin f1 = make_bn_bwd_fin(p1, p2, chunks, (int)C, M, gamma, invstd, dgamma, dbeta, k, k + C, k + 2 * C, -1);
+  const BnBwdFin f2 =
+      make_bn_bwd_fin(p1, p3, chunks, (int)C, M, gamma2, invstd2, dgamma2, dbeta2, j, j + C, j + 2 * C, -1);
+  hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((unsigned)(f1.blocks + f2.blocks)), dim3(kBlock), 0, s, f1, f2);
   dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
   switch (dtype) {
     case 0: hipLaunchKernelGGL(bn_bwd_apply2_kernel<F32>, ga, bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, kBnReverse); break;

@@ -1320,8 +1320,60 @@ __global__ __launch_bounds__(kBlock) void space_to_depth2_kernel(const T* __rest
   }
 }
 
+// The 3-channel fp32 image (the ResNet input) two output pixels per thread: the 4 x 2 input
+// pixels are two rows of 48 contiguous, 16-byte-aligned bytes - 6 float4 loads and 4 16-byte
+// stores per thread instead of 24 scalar loads (69 us -> memory-bound on ResNet-50's 154 MB).
+template <bool F16>
+__global__ __launch_bounds__(kBlock) void space_to_depth2_c3_kernel(const float* __restrict__ x, uint16_t* __restrict__ a,
+                                                                    int64_t n2, int H, int W) {
+  const int H2 = H / 2, Q = W / 4;  // Q pixel pairs per output row
+  for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < n2; t += (int64_t)gridDim.x * kBlock) {
+    const int64_t n = t / ((int64_t)H2 * Q);
+    const int rem = (int)(t - n * H2 * Q);
+    const int i = rem / Q, q = rem - i * Q;
+    float v[2][12];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const float4* src = reinterpret_cast<const float4*>(x + ((n * H + 2 * i + r) * (int64_t)W + 4 * q) * 3);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float4 f = src[k];
+        v[r][4 * k] = f.x; v[r][4 * k + 1] = f.y; v[r][4 * k + 2] = f.z; v[r][4 * k + 3] = f.w;
+      }
+    }
+    // output pixel p (= 2q + p) gathers input pixels (2i + r, 4q + 2p + b): channel (r*2 + b)*4 + c
+    uint32_t pk[2][8];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int ab = 0; ab < 4; ++ab) {
+        const int r = ab >> 1, b = ab & 1, base = (2 * p + b) * 3;
+        const f32x2_t v0 = {v[r][base], v[r][base + 1]}, v1 = {v[r][base + 2], 0.f};
+        pk[p][2 * ab] = cpack<F16>(v0);
+        pk[p][2 * ab + 1] = cpack<F16>(v1);
+      }
+    uint4* dst = reinterpret_cast<uint4*>(a + (t * 2) * 16);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      dst[2 * p] = make_uint4(pk[p][0], pk[p][1], pk[p][2], pk[p][3]);
+      dst[2 * p + 1] = make_uint4(pk[p][4], pk[p][5], pk[p][6], pk[p][7]);
+    }
+  }
+}
+
 void launch_space_to_depth2(const void* x, bool x_bf16, uint16_t* a, int N, int H, int W, int C, hipStream_t st,
                             bool out_f16) {
+  if (!x_bf16 && C == 3 && W % 4 == 0 && H % 2 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0) {
+    const int64_t n2 = (int64_t)N * (H / 2) * (W / 4);
+    const dim3 grid((unsigned)grid_for(n2, 1));
+    if (out_f16)
+      hipLaunchKernelGGL(space_to_depth2_c3_kernel<true>, grid, dim3(kBlock), 0, st, static_cast<const float*>(x), a, n2,
+                         H, W);
+    else
+      hipLaunchKernelGGL(space_to_depth2_c3_kernel<false>, grid, dim3(kBlock), 0, st, static_cast<const float*>(x), a,
+                         n2, H, W);
+    return;
+  }
   const int64_t npix = (int64_t)N * (H / 2) * (W / 2);
   const dim3 grid((unsigned)grid_for(npix, 2));
   if (x_bf16)

@@ -845,3 +845,19 @@ def test_last_tail_statistics_from_avgpool_backward(cuda, monkeypatch, C, hw):
         res.append([x.grad.float(), r.grad.float(), w.grad, b.grad])
     for a, ref in zip(*res):
         torch.testing.assert_close(a, ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item() + 1e-6)
+
+
+@pytest.mark.parametrize("hw", [(224, 224), (34, 30), (32, 32)])
+@pytest.mark.parametrize("f16", [False, True])
+def test_space_to_depth2_exact(cuda, hw, f16):
+    """space_to_depth2: X2[n, (a*2 + b)*4 + c, i, j] = x[n, c, 2i + a, 2j + b] (c < 3; channel 3 of
+    each tap zero), rounded once - the 3-channel fp32 fast path (W % 4 == 0) and the generic one."""
+    g = torch.Generator(device=cuda).manual_seed(17)
+    x = torch.randn(3, 3, *hw, device=cuda, generator=g).contiguous(memory_format=CL)
+    out = ops.native().space_to_depth2(x, f16)
+    n, c, H, W = x.shape
+    xp = torch.nn.functional.pad(x.float(), (0, 0, 0, 0, 0, 1))            # channel 3 = 0
+    ref = xp.reshape(n, 4, H // 2, 2, W // 2, 2).permute(0, 3, 5, 1, 2, 4).reshape(n, 16, H // 2, W // 2)
+    ref = ref.to(torch.float16 if f16 else torch.bfloat16)
+    assert out.shape == ref.shape
+    assert torch.equal(out.view(torch.int16), ref.contiguous(memory_format=CL).view(torch.int16))
