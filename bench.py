@@ -66,10 +66,20 @@ def parse(argv=None):
                     help="native reducer collective (host = gloo staging, debug only)")
     ap.add_argument("--rccl-channels", type=int, default=0,
                     help="NCCL_MIN/MAX_NCHANNELS for the framework's RCCL communicator (0 = RCCL default)")
+    ap.add_argument("--rehearse-shared-gpu", action="store_true",
+                    help="testing: the torchrun ranks share cuda:0 over a gloo process group and the "
+                         "host-bridge collective (--comm host) - the N > 1 path of this script on a "
+                         "1-GPU box (RCCL itself is not exercised; timings are not representative)")
     ap.add_argument("--fake-pg", action="store_true",
                     help="testing: run as rank 0 of a --gpus-rank job on torch's fake process group (CPU)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
+
+
+def _red_dev(device):
+    """Where to all-reduce a host-read scalar: gloo reduces host tensors (its device path is
+    not used here), RCCL device tensors."""
+    return "cpu" if dist.is_initialized() and dist.get_backend() == "gloo" else device
 
 
 def _rccl_version():
@@ -111,9 +121,17 @@ def main(argv=None) -> int:
     from distributed_pytorch_training_amd.utils.dist import init_distributed, set_seed
     from distributed_pytorch_training_amd.utils.env import setup_miopen_env, setup_tunableop
 
+    if a.rehearse_shared_gpu:
+        a.comm = "host"
     setup_miopen_env()
     args = train_args(a)
-    if a.fake_pg:
+    if a.rehearse_shared_gpu:
+        from distributed_pytorch_training_amd.utils.dist import DistInfo
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", init_method="env://")
+        info = DistInfo(dist.get_rank(), dist.get_world_size(), 0, "gloo", dev)
+    elif a.fake_pg:
         from torch.testing._internal.distributed.fake_pg import FakeStore
 
         from distributed_pytorch_training_amd.utils.dist import DistInfo
@@ -155,7 +173,7 @@ def main(argv=None) -> int:
     fence()
     dt = time.time() - t0
     if ws > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        t = torch.tensor([dt], dtype=torch.float64, device=_red_dev(device))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms = 1e3 * dt / max(a.steps, 1)
@@ -178,7 +196,7 @@ def main(argv=None) -> int:
         fence()
         pdt = time.time() - t1
         if ws > 1:
-            t = torch.tensor([pdt], dtype=torch.float64, device=device)
+            t = torch.tensor([pdt], dtype=torch.float64, device=_red_dev(device))
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             pdt = float(t.item())
         prof = trainer.timeline.summary(skip=0)

@@ -67,3 +67,26 @@ def test_bench_torchrun_gloo_two_ranks(tmp_path):
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout  # rank 0 only
     _check(lines[0], 2)
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_sharing_one_gpu(tmp_path):
+    """bench.py's N > 1 path on a real GPU step (2 torchrun ranks on cuda:0, gloo control plane,
+    host-bridge collective: --rehearse-shared-gpu): barrier + synchronize fences, MAX of the rank
+    times, the second profiled window with per-bucket comm events, and the JSON line."""
+    port = 29000 + os.getpid() % 2000
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--batch-size", "32", "--image-size", "64", "--steps", "2", "--warmup", "1",
+           "--profile-steps", "2", "--rehearse-shared-gpu"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = lines[0]
+    assert KEYS <= set(rec) and rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["config"]["global_batch"] == 64 and rec["comm"]["kind"] == "host"
+    assert rec["value"] == pytest.approx(64 * 1e3 / rec["ms_per_step"], rel=0.02)
+    # a real collective ran: the sync share is a measured number and buckets were formed
+    assert isinstance(rec["pct_step_allreduce"], float) and rec["pct_step_allreduce"] > 0
+    assert rec["comm"]["buckets_mib"] and rec["sync_profile_window"]["steps"] == 2
