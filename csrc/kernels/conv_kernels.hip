@@ -171,9 +171,17 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 // 256-row block per CU: twice the MFMA work per staged byte, the large-tile regime of
 // cdna_hip_programming.md §5 where the 2-stage glds pipeline is MFMA-bound rather than
 // L2-bound).
+// HALO (3x3 / stride 1 / pad 1 with Ho = H, Wo = W, C % 64 == 0, 1 stage, 128 rows, not split):
+// the K loop runs tap row r, channel block cb, then the three taps s of that row.  The 128 output
+// rows of a tile are consecutive flattened pixels, so for tap (r, s) they read the consecutive
+// input pixels m0 + (r-1)*W + (s-1) + row: ONE 136-row halo strip per (r, cb) serves all three s
+// (the MFMA reads LDS row row + s), and each fragment row that falls in the zero padding (an
+// image border, where the flattened index wraps into the neighbouring row or image) is zeroed
+// in registers.  A operand bytes per three K-steps: 17 KiB instead of 48 KiB - the 128 x 128
+// tile is bound by what one CU can pull from L2 into LDS (docs/DESIGN.md 7.1).
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
           bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, bool F16 = false,
-          int NT = conv::kThreads, bool SPLIT = false>
+          int NT = conv::kThreads, bool SPLIT = false, bool HALO = false>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
   constexpr int BM = BMT;
@@ -185,7 +193,9 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   static_assert(WM * WN == NW && MI >= 1 && MI * WM * 32 == BM, "conv_fwd_kernel: bad wave tiling");
   constexpr int A_PER_T = BM * 8 / NT;  // glds instructions per wave per K-step (A)
   constexpr int B_PER_T = BN * 8 / NT;  // (B)
-  constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
+  static_assert(!HALO || (BMT == 128 && STAGES == 1 && !BKN && !SPLIT && NT == conv::kThreads), "HALO config");
+  constexpr int HROWS = 136;  // halo strip rows: 128 + 2, rounded up to whole 8-row glds instructions
+  constexpr int A_BYTES = (HALO ? HROWS : BM) * kRowBytes, B_BYTES = BN * kRowBytes;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int C_STRIDE = BN * 2 + 16;  // epilogue image row stride (bytes), padded
   constexpr int RED = 2 * WM * BN * 4;   // BN-statistics cross-wave scratch
@@ -344,7 +354,84 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
     }
   };
 
-  if (STAGES == 2) {
+  if constexpr (HALO) {
+    // per-lane fragment rows: output pixel coordinates, fixed for the whole loop
+    int fho[MI], fwo[MI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int64_t m = m0 + wm * (MI * 32) + i * 32 + lr;
+      if (m < p.M) {
+        const int rem = (int)(m % HoWo);
+        fho[i] = rem / p.Wo;
+        fwo[i] = rem - fho[i] * p.Wo;
+      } else {
+        fho[i] = -(1 << 28);  // never valid
+        fwo[i] = 0;
+      }
+    }
+    const int64_t npix = (int64_t)p.N * p.H * p.W;
+    const unsigned char* hb = lds;            // halo strip [HROWS][128 B]
+    unsigned char* bb = lds + A_BYTES;        // B [BN][128 B]
+    auto stage_b = [&](int r, int sx, int cb) {
+      const int wk = (r * 3 + sx) * p.C + cb * BK;
+#pragma unroll
+      for (int i = 0; i < B_PER_T; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bb + (wid * B_PER_T + i) * 1024),
+                                                 16, (uint32_t)(woff[i] + wk) * 2u, 0, 0, 0);
+    };
+    auto stage_halo = [&](int r, int cb) {
+      const int64_t q0 = m0 + (int64_t)(r - 1) * p.W - 1;  // input pixel of halo row 0
+      for (int gi = wid; gi < HROWS / 8; gi += NW) {      // 17 instructions over the 4 waves
+        const int j = gi * 8 + (lane >> 3);
+        const int chunk = (lane & 7) ^ ((j >> 1) & 7);
+        const int64_t q = q0 + j;
+        const bool ok = q >= 0 && q < npix;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rx, (__attribute__((address_space(3))) void*)(hb + gi * 1024), 16,
+            ok ? (uint32_t)((int)q * p.C + cb * BK + chunk * 8) * 2u : kOOB, 0, 0, 0);
+      }
+    };
+    auto mma_h = [&](int r, int sx) {
+      bool ok[MI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        ok[i] = ((unsigned)(fho[i] + r - 1) < (unsigned)p.H) & ((unsigned)(fwo[i] + sx - 1) < (unsigned)p.W);
+#pragma unroll
+      for (int kk = 0; kk < BK / 16; ++kk) {
+        const int ch = kk * 2 + lh;
+        bf16x8_t fa[MI], fb[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int hrow = wm * (MI * 32) + i * 32 + lr + sx;
+          fa[i] = *reinterpret_cast<const bf16x8_t*>(hb + hrow * kRowBytes + conv::swz(hrow, ch) * 16);
+          if (!ok[i]) fa[i] = bf16x8_t{};
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int row = wn * 64 + j * 32 + lr;
+          fb[j] = *reinterpret_cast<const bf16x8_t*>(bb + row * kRowBytes + conv::swz(row, ch) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = cmfma<F16>(fa[i], fb[j], acc[i][j]);
+      }
+    };
+    for (int r = 0; r < 3; ++r) {
+      for (int cb = 0; cb < cblocks; ++cb) {
+#pragma unroll 1
+        for (int sx = 0; sx < 3; ++sx) {
+          if (sx == 0) stage_halo(r, cb);
+          stage_b(r, sx, cb);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          mma_h(r, sx);
+          __syncthreads();
+        }
+      }
+    }
+  } else if (STAGES == 2) {
     stage(ks0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1614,6 +1701,19 @@ int take_attached_reduce(ReduceCarry& rc) {
 }
 static int take_attached_reduce(ConvFwdArgs& a) { return take_attached_reduce(a.red); }
 
+// 3x3 / stride 1 / pad 1 convs (and their backward-data) take the HALO K loop (conv_fwd_kernel);
+// DPT_CONV_HALO=0 keeps the per-tap loop (A/B)
+static int g_conv_halo = -1;
+static bool halo_ok(const ConvFwdArgs& a) {
+  if (g_conv_halo < 0) {
+    const char* e = std::getenv("DPT_CONV_HALO");
+    g_conv_halo = e ? std::atoi(e) : 1;
+  }
+  return g_conv_halo && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 64 == 0 && a.Ho == a.H &&
+         a.Wo == a.W;
+}
+void conv_set_halo(int on) { g_conv_halo = on; }
+
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
           bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, int NT = conv::kThreads>
 static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdArgs& a0) {
@@ -1621,6 +1721,17 @@ static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdAr
   ConvFwdArgs a = a0;
   if constexpr (NT == conv::kThreads) grid.x += (unsigned)take_attached_reduce(a);
   conv_check_offsets(a, BKN);
+  if constexpr (BMT == 128 && STAGES == 1 && LDSEPI && !BKN && !REMAP && NT == conv::kThreads) {
+    if (halo_ok(a)) {
+      if (a.f16)
+        hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, 1, true, false, STATS, BNB, BNR, false, ZSIB, BNR2, true,
+                                            conv::kThreads, false, true>), grid, block, 0, s, a);
+      else
+        hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, 1, true, false, STATS, BNB, BNR, false, ZSIB, BNR2, false,
+                                            conv::kThreads, false, true>), grid, block, 0, s, a);
+      return;
+    }
+  }
   if constexpr (BMT == 128 && STAGES == 1 && LDSEPI && NT == conv::kThreads) {
     if (a.f16) {
       hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, STAGES, LDSEPI, BKN, STATS, BNB, BNR, REMAP, ZSIB, BNR2, true>),

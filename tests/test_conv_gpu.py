@@ -861,3 +861,42 @@ def test_space_to_depth2_exact(cuda, hw, f16):
     ref = ref.to(torch.float16 if f16 else torch.bfloat16)
     assert out.shape == ref.shape
     assert torch.equal(out.view(torch.int16), ref.contiguous(memory_format=CL).view(torch.int16))
+
+
+HALO_SHAPES = [
+    (4, 64, 14, 14, 64),     # tiles cross image boundaries (196 pixels per image)
+    (3, 256, 7, 7, 512),     # 4 channel blocks, tiles spanning several images
+    (2, 128, 28, 28, 128),
+    (1, 64, 5, 6, 128),      # non-square, one partial tile
+]
+
+
+@pytest.mark.parametrize("shape", HALO_SHAPES)
+def test_halo_3x3_matches_per_tap_loop(cuda, shape):
+    """3x3 / stride-1 convs through the HALO K loop (one halo strip per tap row, padding rows
+    zeroed in registers) vs the per-tap loop and an fp32 reference: forward with BN statistics,
+    backward-data with the BN+ReLU statistics epilogue."""
+    N, C, H, W, Cout = shape
+    C_ = ops.native()
+    x, w = _operands(cuda, N, C, H, W, Cout, 3, seed=21)
+    gy = torch.randn(N, Cout, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    bn_x = torch.randn_like(x)
+    bn_mean = torch.randn(C, device=cuda)
+    bn_coef = torch.randn(2 * C, device=cuda)
+    out = {}
+    try:
+        for halo in (1, 0):
+            C_.conv_set_halo(halo)
+            y, ps, pq = C_.conv_fwd(x, w, 1, 1, True)
+            dx, p1, p2, _ = C_.conv_dgrad_bnstats(gy, w, 1, bn_x, bn_mean, bn_coef)
+            out[halo] = (y.float(), ps, pq, dx.float(), p1, p2)
+    finally:
+        C_.conv_set_halo(1)
+    ref = F.conv2d(x.float(), w.float(), padding=1)
+    torch.testing.assert_close(out[1][0], ref, rtol=1e-2, atol=1e-2)
+    dref = torch.nn.grad.conv2d_input(x.shape, w.float(), gy.float(), padding=1)
+    torch.testing.assert_close(out[1][3], dref, rtol=1e-2, atol=2e-2)
+    # same products summed in another order: within a bf16 rounding step of the per-tap loop
+    for a, b in zip(out[1], out[0]):
+        torch.testing.assert_close(a.sum(1) if a.dim() == 2 else a, b.sum(1) if b.dim() == 2 else b,
+                                   rtol=1e-2, atol=1e-2 * b.abs().max().item() + 1e-3)
