@@ -181,7 +181,7 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 // tile is bound by what one CU can pull from L2 into LDS (docs/DESIGN.md 7.1).
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
           bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, bool F16 = false,
-          int NT = conv::kThreads, bool SPLIT = false, bool HALO = false>
+          int NT = conv::kThreads, bool SPLIT = false, bool HALO = false, int HB = 1>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
   constexpr int BM = BMT;
@@ -195,8 +195,11 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   constexpr int B_PER_T = BN * 8 / NT;  // (B)
   static_assert(!HALO || (BMT == 128 && STAGES == 1 && !BKN && !SPLIT && NT == conv::kThreads), "HALO config");
   constexpr int HROWS = 136;  // halo strip rows: 128 + 2, rounded up to whole 8-row glds instructions
+  // HB (HALO): B taps staged per load phase - 1: one per K-step; 3: all three taps of the row
+  // with the halo strip, one wait per three K-steps (more LDS: fewer resident blocks)
+  static_assert(HB == 1 || (HALO && HB == 3), "HB");
   constexpr int A_BYTES = (HALO ? HROWS : BM) * kRowBytes, B_BYTES = BN * kRowBytes;
-  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int STAGE = A_BYTES + HB * B_BYTES;
   constexpr int C_STRIDE = BN * 2 + 16;  // epilogue image row stride (bytes), padded
   constexpr int RED = 2 * WM * BN * 4;   // BN-statistics cross-wave scratch
   constexpr int LDS_MAIN = STAGES * STAGE;
@@ -374,9 +377,10 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
     unsigned char* bb = lds + A_BYTES;        // B [BN][128 B]
     auto stage_b = [&](int r, int sx, int cb) {
       const int wk = (r * 3 + sx) * p.C + cb * BK;
+      unsigned char* bd = bb + (HB == 3 ? sx * B_BYTES : 0);
 #pragma unroll
       for (int i = 0; i < B_PER_T; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bb + (wid * B_PER_T + i) * 1024),
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bd + (wid * B_PER_T + i) * 1024),
                                                  16, (uint32_t)(woff[i] + wk) * 2u, 0, 0, 0);
     };
     auto stage_halo = [&](int r, int cb) {
@@ -406,10 +410,11 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
           fa[i] = *reinterpret_cast<const bf16x8_t*>(hb + hrow * kRowBytes + conv::swz(hrow, ch) * 16);
           if (!ok[i]) fa[i] = bf16x8_t{};
         }
+        const unsigned char* bs = bb + (HB == 3 ? sx * B_BYTES : 0);
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           const int row = wn * 64 + j * 32 + lr;
-          fb[j] = *reinterpret_cast<const bf16x8_t*>(bb + row * kRowBytes + conv::swz(row, ch) * 16);
+          fb[j] = *reinterpret_cast<const bf16x8_t*>(bs + row * kRowBytes + conv::swz(row, ch) * 16);
         }
 #pragma unroll
         for (int i = 0; i < MI; ++i)
@@ -420,14 +425,25 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
     };
     for (int r = 0; r < 3; ++r) {
       for (int cb = 0; cb < cblocks; ++cb) {
-#pragma unroll 1
-        for (int sx = 0; sx < 3; ++sx) {
-          if (sx == 0) stage_halo(r, cb);
-          stage_b(r, sx, cb);
+        if constexpr (HB == 3) {
+          stage_halo(r, cb);
+#pragma unroll
+          for (int sx = 0; sx < 3; ++sx) stage_b(r, sx, cb);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __syncthreads();
-          mma_h(r, sx);
+#pragma unroll 1
+          for (int sx = 0; sx < 3; ++sx) mma_h(r, sx);
           __syncthreads();
+        } else {
+#pragma unroll 1
+          for (int sx = 0; sx < 3; ++sx) {
+            if (sx == 0) stage_halo(r, cb);
+            stage_b(r, sx, cb);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            mma_h(r, sx);
+            __syncthreads();
+          }
         }
       }
     }
@@ -1701,9 +1717,17 @@ int take_attached_reduce(ReduceCarry& rc) {
 }
 static int take_attached_reduce(ConvFwdArgs& a) { return take_attached_reduce(a.red); }
 
-// 3x3 / stride 1 / pad 1 convs (and their backward-data) take the HALO K loop (conv_fwd_kernel);
-// DPT_CONV_HALO=0 keeps the per-tap loop (A/B)
+// 3x3 / stride 1 / pad 1 convs (and their backward-data) take the HALO K loop (conv_fwd_kernel).
+// DPT_CONV_HALO: 0 = per-tap loop (A/B), 1 = auto (default): all three B taps per load phase
+// (HB = 3) when the tile grid is at most two blocks per CU - there the grid, not LDS, limits the
+// resident blocks and one wait per three K-steps wins (3x3 512->512 @7x7: 0.075 -> 0.064 ms) -
+// else one B tap per phase (HB = 1; HB = 3 everywhere lost 1.2 % in the step), 2 / 3 = force HB
 static int g_conv_halo = -1;
+static int halo_hb(const ConvFwdArgs& a, int bn) {
+  if (g_conv_halo == 2) return 1;
+  if (g_conv_halo == 3) return 3;
+  return (int64_t)a.m_tiles * (a.Cout / bn) <= 512 ? 3 : 1;
+}
 static bool halo_ok(const ConvFwdArgs& a) {
   if (g_conv_halo < 0) {
     const char* e = std::getenv("DPT_CONV_HALO");
@@ -1723,6 +1747,15 @@ static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdAr
   conv_check_offsets(a, BKN);
   if constexpr (BMT == 128 && STAGES == 1 && LDSEPI && !BKN && !REMAP && NT == conv::kThreads) {
     if (halo_ok(a)) {
+      if (halo_hb(a, BN) == 3) {  // all three B taps with the halo strip
+        if (a.f16)
+          hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, 1, true, false, STATS, BNB, BNR, false, ZSIB, BNR2, true,
+                                              conv::kThreads, false, true, 3>), grid, block, 0, s, a);
+        else
+          hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, 1, true, false, STATS, BNB, BNR, false, ZSIB, BNR2, false,
+                                              conv::kThreads, false, true, 3>), grid, block, 0, s, a);
+        return;
+      }
       if (a.f16)
         hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, 1, true, false, STATS, BNB, BNR, false, ZSIB, BNR2, true,
                                             conv::kThreads, false, true>), grid, block, 0, s, a);

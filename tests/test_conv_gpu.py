@@ -885,7 +885,7 @@ def test_halo_3x3_matches_per_tap_loop(cuda, shape):
     bn_coef = torch.randn(2 * C, device=cuda)
     out = {}
     try:
-        for halo in (1, 0):
+        for halo in (2, 3, 0):   # 2 / 3: one / all three B taps staged per phase (1 = auto picks)
             C_.conv_set_halo(halo)
             y, ps, pq = C_.conv_fwd(x, w, 1, 1, True)
             dx, p1, p2, _ = C_.conv_dgrad_bnstats(gy, w, 1, bn_x, bn_mean, bn_coef)
@@ -893,10 +893,12 @@ def test_halo_3x3_matches_per_tap_loop(cuda, shape):
     finally:
         C_.conv_set_halo(1)
     ref = F.conv2d(x.float(), w.float(), padding=1)
-    torch.testing.assert_close(out[1][0], ref, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(out[2][0], ref, rtol=1e-2, atol=1e-2)
     dref = torch.nn.grad.conv2d_input(x.shape, w.float(), gy.float(), padding=1)
-    torch.testing.assert_close(out[1][3], dref, rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(out[2][3], dref, rtol=1e-2, atol=2e-2)
     # same products summed in another order: within a bf16 rounding step of the per-tap loop
-    for a, b in zip(out[1], out[0]):
+    for a, b in zip(out[2], out[0]):
         torch.testing.assert_close(a.sum(1) if a.dim() == 2 else a, b.sum(1) if b.dim() == 2 else b,
                                    rtol=1e-2, atol=1e-2 * b.abs().max().item() + 1e-3)
+    for a, b in zip(out[3], out[2]):   # same summation order as HALO with one B tap per phase
+        assert torch.equal(a, b)
