@@ -1124,6 +1124,9 @@ struct ConvWgradArgs {
   int f16;             // fp16 operands (bf16 otherwise)
   // carried BatchNorm backward finalize (carry.h): the grid's last fin.blocks blocks
   BnBwdFin fin;
+  // conv_wgrad_halo_kernel: padded pixel count N*H*(W+2) and divisors by W+2 and H
+  int Mp = 0;
+  FastDiv div_wp{}, div_h{};
 };
 
 // NT = 256: 2 x 2 waves; NT = 512 (256 x 256 tiles): 2 x 4 waves of 128 x 64 - twice the MFMA
@@ -1334,6 +1337,161 @@ __global__ __launch_bounds__(NT, (NT == conv::kThreads && BNW <= 128) ? DPT_WGRA
         out[(int64_t)row * Kg + col] = acc[i][j][e];
       }
     }
+}
+
+// ---- backward-weight HALO: the three taps (r, 0..2) of a 3x3 / stride-1 / pad-1 conv ---------
+//
+// conv_wgrad_kernel stages a dy tile and an x tile per tap: 9 dy + 9 x tiles per 64 pixels.
+// Here the K loop runs over PADDED output pixels p = (n*H + ho)*(W+2) + wo, wo in [0, W+2):
+// the two dummy columns per image row have dy = 0, and the input pixel of tap (r, s) is the
+// padded input index q = p + (r-1)*(W+2) + s whose columns 0 and W+1 are the zero padding -
+// an image row never wraps into the next.  So one strip of 68 consecutive padded x rows serves
+// all three taps of tap row r (tap s = the strip read s rows further down), and one dy tile
+// serves all three: 1 dy + 1 strip per 64 pixels and 3 taps.  dy rows whose tap row
+// ho + r - 1 leaves the image are zero-filled (kOOB), which also kills the strip rows read from
+// the neighbouring image rows.  Tile: 64 output channels x BNW input channels x 3 taps; 2 x 2
+// waves of 32 x BNW/2 x 3 (BNW = 128: 6 accumulators, 2 waves per SIMD; BNW = 64: 3, 4 waves
+// per SIMD - the one that pays, see wgrad_halo_mode).  Costs (W+2)/W more MFMA work (7 % at
+// W = 28, 29 % at W = 7) for ~2.9x fewer staged bytes.
+template <int BNW, int STAGES, bool F16>
+__global__ __launch_bounds__(conv::kThreads, BNW == 64 ? 4 : 2) void conv_wgrad_halo_kernel(ConvWgradArgs p) {
+  using namespace conv;
+  constexpr int NW = 4, BKP = 64;
+  constexpr int RBA = 128, RBB = BNW * 2;  // dy rows: 64 channels, x rows: BNW channels
+  constexpr int B_RPI = 1024 / RBB;        // strip rows per glds instruction (4 or 8)
+  constexpr int HROWS = (BKP + 2 + B_RPI - 1) / B_RPI * B_RPI;  // 68 or 72
+  constexpr int NI = BNW / 64;             // 32-column accumulators per wave and tap
+  constexpr int A_BYTES = BKP * RBA, B_BYTES = HROWS * RBB, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = A_BYTES / 1024 / NW, A_RPI = 1024 / RBA;  // 2 per wave, 8 rows each
+  constexpr int B_GI = B_BYTES / 1024;                              // 17 or 9 per block
+  constexpr int B_PW = (B_GI + NW - 1) / NW;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[STAGES * STAGE];
+  if (p.fin.blocks) {  // carried BatchNorm backward finalize blocks (ConvWgradArgs::fin)
+    const int nw = (int)gridDim.x - p.fin.blocks;
+    if ((int)blockIdx.x >= nw) {
+      bn_bwd_finalize_block(p.fin, (int)blockIdx.x - nw, lds);
+      return;
+    }
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles = p.co_tiles * p.n_tiles;
+  const int bid = conv::xcd_remap(blockIdx.x, tiles * p.splits);
+  const int sp = bid / tiles, tile = bid - sp * tiles;
+  const int ct = tile / p.n_tiles, nt = tile - ct * p.n_tiles;
+  const int cblocks = p.C / BNW;
+  const int r = nt / cblocks, cb = nt - r * cblocks;
+  const int co0 = ct * 64, ci0 = cb * BNW;
+  const int k0 = sp * p.steps_per_split;
+  const int k1 = min(k0 + p.steps_per_split, (p.Mp + BKP - 1) / BKP);
+  const int Wp = p.W + 2, NH = p.N * p.H;
+
+  int arow[A_INSTR], achk[A_INSTR], brow[B_PW], bchk[B_PW];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    arow[i] = (wid * A_INSTR + i) * A_RPI + lane / (RBA / 16);
+    achk[i] = wg_slot<RBA>(arow[i], lane % (RBA / 16));
+  }
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    brow[i] = (wid + i * NW) * B_RPI + lane / (RBB / 16);
+    bchk[i] = wg_slot<RBB>(brow[i], lane % (RBB / 16));
+  }
+  constexpr uint32_t kOOB = 0xFFFFFF00u;
+  const __amdgpu_buffer_rsrc_t rdy =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, 0, (int)((uint32_t)p.M * (uint32_t)p.Cout * 2u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.x, 0, (int)((uint32_t)p.N * (uint32_t)(p.H * p.W * p.C) * 2u), 0x00020000);
+  const int qbase = (r - 1) * Wp;  // strip row j of K-step ks = padded input ks*64 + qbase + j
+
+  auto stage = [&](int ks, int buf) {
+    unsigned char* a = lds + buf * STAGE;
+    unsigned char* b = a + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i) {
+      const int pp = ks * BKP + arow[i];
+      const int R = (int)fdiv((uint32_t)pp, p.div_wp), wo = pp - R * Wp;
+      const int ho = R - (int)fdiv((uint32_t)R, p.div_h) * p.H;
+      const bool ok = (pp < p.Mp) & (wo < p.W) & ((unsigned)(ho + r - 1) < (unsigned)p.H);
+      const uint32_t off = (((uint32_t)R * p.W + wo) * p.Cout + co0 + achk[i] * 8) * 2u;  // used when ok
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rdy, (__attribute__((address_space(3))) void*)(a + (wid * A_INSTR + i) * 1024),
+                                               16, ok ? off : kOOB, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      if (wid + i * NW < B_GI) {  // wave-uniform
+        const int q = ks * BKP + qbase + brow[i];
+        const int qc = max(q, 0);
+        const int R = (int)fdiv((uint32_t)qc, p.div_wp), c = qc - R * Wp;
+        const bool ok = (q >= 0) & (R < NH) & (c >= 1) & (c <= p.W);
+        const uint32_t off = (((uint32_t)R * p.W + c - 1) * p.C + ci0 + bchk[i] * 8) * 2u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(b + (wid + i * NW) * 1024),
+                                                 16, ok ? off : kOOB, 0, 0, 0);
+      }
+    }
+  };
+
+  f32x16_t acc[3][NI];
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[s][j][e] = 0.f;
+
+  auto mma = [&](int buf) {
+    const unsigned char* a = lds + buf * STAGE;
+    const unsigned char* b = a + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BKP / 16; ++kk) {
+      const bf16x8_t fa = wg_frag<RBA>(a, kk * 16, wm * 32, lane);
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        bf16x8_t fb[NI];
+#pragma unroll
+        for (int j = 0; j < NI; ++j) fb[j] = wg_frag<RBB>(b, kk * 16 + s, wn * (BNW / 2) + j * 32, lane);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[s][j] = cmfma<F16>(fa, fb[j], acc[s][j]);
+      }
+    }
+  };
+  if (STAGES == 2) {
+    if (k0 < k1) {
+      stage(k0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int ks = k0; ks < k1; ++ks) {
+        const int cur = (ks - k0) & 1;
+        if (ks + 1 < k1) stage(ks + 1, cur ^ 1);
+        mma(cur);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    }
+  } else {
+    for (int ks = k0; ks < k1; ++ks) {
+      stage(ks, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      mma(0);
+      __syncthreads();
+    }
+  }
+  const int64_t Kg = (int64_t)9 * p.C;
+  const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    float* out = p.part + (int64_t)sp * p.Cout * Kg + (int64_t)(r * 3 + s) * p.C + ci0;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = wn * (BNW / 2) + j * 32 + lr;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = co0 + wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        out[(int64_t)row * Kg + col] = acc[s][j][e];
+      }
+    }
+  }
 }
 
 // out[i] = sum_s part[s][i]: PH phases per block split the S loop, LDS combines them.
@@ -2186,6 +2344,23 @@ void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, i
   }
 }
 
+// conv_wgrad_halo_kernel modes: 0 off, 1 / 2: 128-channel strips, 3 / 4: 64-channel strips
+// (even: double-buffered), 5 auto (default, DPT_WGRAD_HALO): mode 3 for 64-channel inputs,
+// where the per-tap kernel's two-tap tiles waste 1/9 of their MFMA work on a ragged last tile
+// (64x56x56 -> 64: 0.118 -> 0.085-0.095 ms); the per-tap kernel elsewhere (the halo's W+2
+// padding costs 7-29 % more MFMA work and measured level or slower at 128-512 channels,
+// profiles/wgrad_halo_r2.md)
+static int g_wgrad_halo = -1;
+static int wgrad_halo_mode(int C = 0) {
+  if (g_wgrad_halo < 0) {
+    const char* e = std::getenv("DPT_WGRAD_HALO");
+    g_wgrad_halo = e ? std::atoi(e) : 5;
+  }
+  if (g_wgrad_halo == 5) return C == 64 ? 3 : 0;
+  return g_wgrad_halo;
+}
+void conv_set_wgrad_halo(int on) { g_wgrad_halo = on; }
+
 static FastDiv make_fastdiv(uint32_t d) {
   FastDiv f;
   f.d = d;
@@ -2205,6 +2380,29 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
   pl.Ho = Ho > 0 ? Ho : (H + 2 * pad - R) / stride + 1;
   pl.Wo = Wo > 0 ? Wo : (W + 2 * pad - S) / stride + 1;
   const int64_t M = (int64_t)N * pl.Ho * pl.Wo;
+  const int hmode = wgrad_halo_mode(C);
+  if (hmode && R == 3 && S == 3 && stride == 1 && pad == 1 && pl.Ho == H && pl.Wo == W &&
+      C % (hmode >= 3 ? 64 : 128) == 0 && Cout % 64 == 0 && (int64_t)N * H * (W + 2) + 128 < (1ll << 31)) {
+    // conv_wgrad_halo_kernel: 64 x BNW x 3-tap tiles over N*H*(W+2) padded pixels (modes 1/2:
+    // BNW = 128, 2 blocks per CU; 3/4: BNW = 64, 4 per CU; even modes double-buffer)
+    pl.halo = hmode;
+    pl.bmw = 64;
+    pl.bnw = pl.halo >= 3 ? 64 : 128;
+    const int tiles = (Cout / 64) * 3 * (C / pl.bnw);
+    const int steps = (int)(((int64_t)N * H * (W + 2) + 63) / 64);
+    static const int env_target = [] {
+      const char* e = std::getenv("DPT_WGRAD_HALO_TARGET");
+      return e ? std::atoi(e) : 0;
+    }();
+    const int target = env_target > 0 ? env_target : pl.bnw == 128 ? 512 : 768;
+    int splits = (target + tiles - 1) / tiles;
+    const int min_steps = (int64_t)tiles * (steps / 32) >= 512 ? 32 : 2;
+    splits = std::max(1, std::min(splits, steps / min_steps));
+    pl.steps_per_split = (steps + splits - 1) / splits;
+    pl.splits = (steps + pl.steps_per_split - 1) / pl.steps_per_split;
+    pl.part_floats = pl.splits > 1 ? (int64_t)pl.splits * Cout * 9 * C : 0;
+    return pl;
+  }
   pl.bmw = Cout % 128 == 0 ? 128 : 64;
   // column tile: 128 input channels of one tap; 64-channel inputs take two taps per tile (a
   // ragged last tile for odd tap counts: 3x3 -> 5 tiles, 1/9 of the MFMA work wasted, twice
@@ -2263,6 +2461,13 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
       a.dp_hwrap = (H * W - pl.Ho * stride * W) * C;
     }
   }
+  if (pl.halo) {
+    a.co_tiles = Cout / 64;
+    a.n_tiles = 3 * (C / pl.bnw);
+    a.Mp = N * H * (W + 2);
+    a.div_wp = make_fastdiv((uint32_t)(W + 2));
+    a.div_h = make_fastdiv((uint32_t)H);
+  }
   dim3 grid((unsigned)(a.co_tiles * a.n_tiles * a.splits)), block(conv::kThreads);
   const int v = a.f16 ? 0 : conv_variant();
   if (fin != nullptr) {
@@ -2275,7 +2480,20 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
       grid.x += (unsigned)a.fin.blocks;
     }
   }
-  if (pl.bmw == 256) {  // conv_wgrad_plan chose the 8-wave 256 x 256 tile
+  if (pl.halo) {
+#define DPT_WH(BNW, ST)                                                                      \
+  do {                                                                                       \
+    if (a.f16) hipLaunchKernelGGL((conv_wgrad_halo_kernel<BNW, ST, true>), grid, block, 0, st, a);  \
+    else hipLaunchKernelGGL((conv_wgrad_halo_kernel<BNW, ST, false>), grid, block, 0, st, a);       \
+  } while (0)
+    switch (pl.halo) {
+      case 2: DPT_WH(128, 2); break;
+      case 3: DPT_WH(64, 1); break;
+      case 4: DPT_WH(64, 2); break;
+      default: DPT_WH(128, 1); break;
+    }
+#undef DPT_WH
+  } else if (pl.bmw == 256) {  // conv_wgrad_plan chose the 8-wave 256 x 256 tile
     if (a.f16) throw std::runtime_error("conv_wgrad: the 256 x 256 variant is bf16 only");
     hipLaunchKernelGGL((conv_wgrad_kernel<256, 256, 2, false, 512>), grid, dim3(512), 0, st, a);
   } else if ((v == 1 || v == 2) && pl.bnw <= 128) {

@@ -165,7 +165,9 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, i
 struct ConvWgradPlan {
   int Ho, Wo, bmw, bnw, splits, steps_per_split;
   int64_t part_floats;
+  int halo = 0;  // 3x3 / stride-1: the three taps of a tap row share one x strip (conv_wgrad_halo_kernel)
 };
+void conv_set_wgrad_halo(int mode);  // 0 off, 1-4 forced, 5 auto (default, DPT_WGRAD_HALO)
 ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad, int Ho = 0,
                               int Wo = 0);
 // The split-K reduce of a backward-weight (partials [splits][n4 float4s] -> out, kind as dw_kind).

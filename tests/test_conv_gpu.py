@@ -902,3 +902,41 @@ def test_halo_3x3_matches_per_tap_loop(cuda, shape):
                                    rtol=1e-2, atol=1e-2 * b.abs().max().item() + 1e-3)
     for a, b in zip(out[3], out[2]):   # same summation order as HALO with one B tap per phase
         assert torch.equal(a, b)
+
+
+WGRAD_HALO_SHAPES = [
+    (2, 128, 28, 28, 128),
+    (3, 256, 7, 7, 64),      # 3 tap rows x 2 channel blocks, K-steps spanning images
+    (4, 128, 6, 9, 192),     # non-square, Cout not a multiple of 128
+    (1, 128, 3, 5, 64),      # a single partial K-step
+    (2, 64, 14, 14, 128),    # 64-channel inputs: modes 3 / 4 only (64-channel strip)
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD_HALO_SHAPES)
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_wgrad_halo_matches_reference(cuda, shape, mode, dtype):
+    """3x3 / stride-1 backward-weight through conv_wgrad_halo_kernel (padded-pixel K loop, one x
+    strip for the three taps of a tap row; modes 1 / 2: 128-channel strips, 3 / 4: 64-channel
+    strips; even modes double-buffered) vs an fp32 reference and vs the per-tap kernel (same
+    products, another summation order)."""
+    N, C, H, W, Cout = shape
+    C_ = ops.native()
+    g = torch.Generator(device=cuda).manual_seed(5)
+    x = torch.randn(N, C, H, W, device=cuda, generator=g).to(dtype).contiguous(memory_format=CL)
+    gy = torch.randn(N, Cout, H, W, device=cuda, generator=g).to(dtype).contiguous(memory_format=CL)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (Cout, C, 3, 3), gy.float(), padding=1)
+    scale = ref.abs().max().item()
+    try:
+        C_.conv_set_wgrad_halo(0)
+        base = C_.conv_wgrad(gy, x, [Cout, C, 3, 3], 1, 1, True)
+        C_.conv_set_wgrad_halo(mode)
+        dw = C_.conv_wgrad(gy, x, [Cout, C, 3, 3], 1, 1, True)
+        dw16 = C_.conv_wgrad(gy, x, [Cout, C, 3, 3], 1, 1, False)
+    finally:
+        C_.conv_set_wgrad_halo(5)
+    assert dw.is_contiguous(memory_format=CL) and dw16.dtype == dtype
+    torch.testing.assert_close(dw, ref, rtol=1e-3, atol=1e-4 * scale + 1e-3)
+    torch.testing.assert_close(dw, base, rtol=1e-4, atol=1e-5 * scale + 1e-4)
+    torch.testing.assert_close(dw16.float(), ref, rtol=1e-2, atol=1e-2 * scale)
