@@ -193,23 +193,24 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_finalize_kernel(
 // channel): 8 loads of each row in flight per thread - the finalize is a latency chain of
 // chunks / (kBlock * U) dependent round trips, not a bandwidth problem.
 
-__global__ __launch_bounds__(kBlock) void bn_fwd_finalize_wide_kernel(
+template <int NT>
+__global__ __launch_bounds__(NT) void bn_fwd_finalize_wide_kernel(
     const float* __restrict__ psum, const float* __restrict__ psq, int chunks, int C, int64_t M,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
     float* run_mean, float* run_var, int64_t* num_batches, float* save_mean, float* save_invstd,
     float* coef_a, float* coef_b) {
-  __shared__ double red[2][kBlock / 64];
+  __shared__ double red[2][NT / 64];
   const int c = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (c == 0 && threadIdx.x == 0 && num_batches) num_batches[0] += 1;
   double s, q;
-  block_row_sum2(psum + (int64_t)c * chunks, psq + (int64_t)c * chunks, chunks, s, q);
+  block_row_sum2<NT>(psum + (int64_t)c * chunks, psq + (int64_t)c * chunks, chunks, s, q);
   if (lane == 0) { red[0][wave] = s; red[1][wave] = q; }
   __syncthreads();
   if (threadIdx.x != 0) return;
   s = 0.0;
   q = 0.0;
 #pragma unroll
-  for (int w = 0; w < kBlock / 64; ++w) { s += red[0][w]; q += red[1][w]; }
+  for (int w = 0; w < NT / 64; ++w) { s += red[0][w]; q += red[1][w]; }
   const double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -393,9 +394,23 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_stats_kernel(const void* __rest
   }
 }
 
-__global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(BnBwdFin f) {
-  __shared__ double red[2 * (kBlock / 64)];
-  bn_bwd_finalize_block(f, (int)blockIdx.x, red);
+template <int NT>
+__global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(BnBwdFin f) {
+  __shared__ double red[2 * (NT / 64)];
+  bn_bwd_finalize_block<NT>(f, (int)blockIdx.x, red);
+}
+
+// Threads per block of the standalone WIDE finalizes (one block per channel, thousands of
+// partials each): a latency chain of chunks / (NT * 8) dependent load rounds (DPT_BN_FIN_THREADS,
+// 256 / 512 / 1024).
+static int g_fin_threads = -1;
+static int fin_threads() {
+  if (g_fin_threads < 0) {
+    const char* e = std::getenv("DPT_BN_FIN_THREADS");
+    const int v = e ? std::atoi(e) : 256;
+    g_fin_threads = (v == 512 || v == 1024) ? v : 256;
+  }
+  return g_fin_threads;
 }
 
 // Two BatchNorms' finalizes in one launch (a block tail with its downsample BN folded in)
@@ -417,7 +432,10 @@ BnBwdFin make_bn_bwd_fin(const float* p1, const float* p2, int chunks, int C, in
 }
 
 static void launch_bn_bwd_fin(const BnBwdFin& f, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)f.blocks), dim3(kBlock), 0, s, f);
+  const int nt = f.wide ? fin_threads() : kBlock;
+  if (nt == 1024) hipLaunchKernelGGL(bn_bwd_finalize_kernel<1024>, dim3((unsigned)f.blocks), dim3(1024), 0, s, f);
+  else if (nt == 512) hipLaunchKernelGGL(bn_bwd_finalize_kernel<512>, dim3((unsigned)f.blocks), dim3(512), 0, s, f);
+  else hipLaunchKernelGGL(bn_bwd_finalize_kernel<kBlock>, dim3((unsigned)f.blocks), dim3(kBlock), 0, s, f);
 }
 
 void launch_bn_bwd_finalize(const BnBwdFinArgs& a, hipStream_t s) {
@@ -602,10 +620,16 @@ void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void
   BnGeometry g = bn_geometry(M, C);
   float* ca = save_coef;
   float* cb = ca + C;
-  if (chunks > 256)
-    hipLaunchKernelGGL(bn_fwd_finalize_wide_kernel, dim3((unsigned)C), dim3(kBlock), 0, s, psum, psq, chunks, (int)C,
-                       M, gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd, ca, cb);
-  else
+  if (chunks > 256) {
+#define DPT_FWD_FIN(NT)                                                                                        \
+  hipLaunchKernelGGL(bn_fwd_finalize_wide_kernel<NT>, dim3((unsigned)C), dim3(NT), 0, s, psum, psq, chunks, (int)C, \
+                     M, gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd, ca, cb)
+    const int nt = fin_threads();
+    if (nt == 1024) DPT_FWD_FIN(1024);
+    else if (nt == 512) DPT_FWD_FIN(512);
+    else DPT_FWD_FIN(kBlock);
+#undef DPT_FWD_FIN
+  } else
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), dim3(kBlock), 0, s, psum, psq, chunks,
                        (int)C, M, gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd,
                        ca, cb);

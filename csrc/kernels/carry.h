@@ -117,6 +117,7 @@ __device__ __forceinline__ void half_wave_sum2(const float* p1, const float* p2,
 // per thread; 16 measured slower: 21 -> 25 us for the stem's 25,088 partials per channel, 6.4 ->
 // 7.2 us averaged over the step's wide finalizes); the result is reduced within each wave (lane 0
 // of every wave holds its wave's sum).
+template <int NT = kBlock>
 __device__ __forceinline__ void block_row_sum2(const float* __restrict__ q1, const float* __restrict__ q2,
                                                int chunks, double& s, double& q) {
   constexpr int U = 8;
@@ -124,16 +125,16 @@ __device__ __forceinline__ void block_row_sum2(const float* __restrict__ q1, con
 #pragma unroll
   for (int u = 0; u < U; ++u) { a[u] = 0.0; b[u] = 0.0; }
   int k = threadIdx.x;
-  for (; k + (U - 1) * kBlock < chunks; k += U * kBlock) {
+  for (; k + (U - 1) * NT < chunks; k += U * NT) {
     float x[U], y[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) { x[u] = q1[k + u * kBlock]; y[u] = q2[k + u * kBlock]; }
+    for (int u = 0; u < U; ++u) { x[u] = q1[k + u * NT]; y[u] = q2[k + u * NT]; }
 #pragma unroll
     for (int u = 0; u < U; ++u) { a[u] += (double)x[u]; b[u] += (double)y[u]; }
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int kk = k + u * kBlock;
+    const int kk = k + u * NT;
     if (kk < chunks) { a[u] += (double)q1[kk]; b[u] += (double)q2[kk]; }
   }
   s = 0.0;
@@ -185,23 +186,24 @@ __device__ __forceinline__ void bn_bwd_fin_store(const BnBwdFin& f, int64_t c, d
   f.k3[c] = (float)(-a * s1 / (double)f.M);
 }
 
-// Block `bid` of the finalize (kBlock threads; lds: >= 64 bytes).
+// Block `bid` of the finalize (NT threads - wide only, kBlock otherwise; lds: >= NT bytes).
+template <int NT = kBlock>
 __device__ __forceinline__ void bn_bwd_finalize_block(const BnBwdFin& f, int bid, void* lds) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (f.wide) {
-    double* red = static_cast<double*>(lds);  // [2][kBlock / 64]
+    double* red = static_cast<double*>(lds);  // [2][NT / 64]
     const int c = bid;
     double s1, s2;
-    block_row_sum2(f.p1 + (int64_t)c * f.chunks, f.p2 + (int64_t)c * f.chunks, f.chunks, s1, s2);
-    if (lane == 0) { red[wave] = s1; red[kBlock / 64 + wave] = s2; }
+    block_row_sum2<NT>(f.p1 + (int64_t)c * f.chunks, f.p2 + (int64_t)c * f.chunks, f.chunks, s1, s2);
+    if (lane == 0) { red[wave] = s1; red[NT / 64 + wave] = s2; }
     __syncthreads();
     if (threadIdx.x != 0) return;
     s1 = 0.0;
     s2 = 0.0;
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) { s1 += red[w]; s2 += red[kBlock / 64 + w]; }
+    for (int w = 0; w < NT / 64; ++w) { s1 += red[w]; s2 += red[NT / 64 + w]; }
     bn_bwd_fin_store(f, c, s1, s2);
-  } else {
+  } else if constexpr (NT == kBlock) {
     const int64_t c = (int64_t)bid * 8 + wave * 2 + (lane >> 5);
     const int part = lane & 31;
     if (c >= f.C) return;
