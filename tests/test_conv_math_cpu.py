@@ -72,3 +72,59 @@ def test_deferred_downsample_bn_falls_back():
     # a deferral reaching a tail that cannot fuse materialises the downsample BN first
     d = DeferredBN(ds[1], ds[0](x))
     torch.testing.assert_close(bn_act_block_out(tail, h, d), ref)
+
+
+def halo_flat_fwd(x, w):
+    """The forward HALO K loop's index algebra (conv_fwd_kernel, HALO): output row m of tap (r, s)
+    reads flattened input pixel m + (r-1)*W + (s-1) - a strip shifted by s rows - and the rows
+    whose (ho + r - 1, wo + s - 1) falls in the padding (where the flat index wraps) are zeroed."""
+    N, C, H, W = x.shape
+    Cout = w.shape[0]
+    xf = x.permute(0, 2, 3, 1).reshape(-1, C)
+    M = xf.shape[0]
+    m = torch.arange(M)
+    ho, wo = (m // W) % H, m % W
+    y = torch.zeros(M, Cout, dtype=x.dtype)
+    for r in range(3):
+        for s in range(3):
+            q = m + (r - 1) * W + (s - 1)
+            ok = (ho + r - 1 >= 0) & (ho + r - 1 < H) & (wo + s - 1 >= 0) & (wo + s - 1 < W)
+            a = torch.where(ok[:, None], xf[q.clamp(0, M - 1)], torch.zeros(()))
+            y += a @ w[:, :, r, s].T
+    return y.reshape(N, H, W, Cout).permute(0, 3, 1, 2)
+
+
+def halo_padded_wgrad(x, dy):
+    """conv_wgrad_halo_kernel's index algebra: K runs over padded output pixels p = (n*H + ho)*(W+2)
+    + wo (dy = 0 for wo >= W); tap (r, s) pairs dy row p with padded input index p + (r-1)*(W+2) +
+    s (padded columns 0 and W+1 are zero), and dy rows whose tap row leaves the image are zeroed -
+    no per-element masks, one strip per tap row."""
+    N, C, H, W = x.shape
+    Cout = dy.shape[1]
+    Wp = W + 2
+    xp = F.pad(x, (1, 1)).permute(0, 2, 3, 1).reshape(-1, C)                 # [N*H*Wp, C]
+    dyp = F.pad(dy, (0, 2)).permute(0, 2, 3, 1).reshape(-1, Cout)          # [N*H*Wp, Cout]
+    Mp = dyp.shape[0]
+    p = torch.arange(Mp)
+    ho = (p // Wp) % H
+    dw = torch.zeros(Cout, C, 3, 3, dtype=x.dtype)
+    for r in range(3):
+        rows_ok = (ho + r - 1 >= 0) & (ho + r - 1 < H)
+        dr = torch.where(rows_ok[:, None], dyp, torch.zeros(()))
+        for s in range(3):
+            q = p + (r - 1) * Wp + s
+            inb = (q >= 0) & (q < Mp)
+            xs = torch.where(inb[:, None], xp[q.clamp(0, Mp - 1)], torch.zeros(()))
+            dw[:, :, r, s] = dr.T @ xs
+    return dw
+
+
+@pytest.mark.parametrize("N,C,H,W,Cout", [(2, 3, 5, 7, 4), (1, 2, 4, 4, 3), (3, 4, 6, 2, 2)])
+def test_halo_index_algebra(N, C, H, W, Cout):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(N, C, H, W, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, C, 3, 3, generator=g, dtype=torch.float64)
+    dy = torch.randn(N, Cout, H, W, generator=g, dtype=torch.float64)
+    torch.testing.assert_close(halo_flat_fwd(x, w), F.conv2d(x, w, padding=1))
+    torch.testing.assert_close(halo_padded_wgrad(x, dy),
+                               torch.nn.grad.conv2d_weight(x, w.shape, dy, padding=1))
