@@ -1181,6 +1181,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_set_big", &dpt::conv_set_big, py::arg("on"));
   m.def("conv_set_halo", &dpt::conv_set_halo, py::arg("on"));
   m.def("conv_set_wgrad_halo", &dpt::conv_set_wgrad_halo, py::arg("mode"));
+  m.def("conv_set_wgrad_wide", &dpt::conv_set_wgrad_wide, py::arg("on"));
   m.def("conv_fwd_splits", [](int64_t M, int Cout, int64_t K, bool graph) {
           return dpt::conv_fwd_splits_for(M, Cout, K, graph);
         }, py::arg("M"), py::arg("Cout"), py::arg("K"), py::arg("graph") = false);

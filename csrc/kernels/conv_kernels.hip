@@ -2361,6 +2361,16 @@ static int wgrad_halo_mode(int C = 0) {
 }
 void conv_set_wgrad_halo(int on) { g_wgrad_halo = on; }
 
+static int g_wgrad_wide = -1;
+static int wgrad_wide_mode() {
+  if (g_wgrad_wide < 0) {
+    const char* e = std::getenv("DPT_WGRAD_WIDE");
+    g_wgrad_wide = e ? std::atoi(e) : 0;
+  }
+  return g_wgrad_wide;
+}
+void conv_set_wgrad_wide(int on) { g_wgrad_wide = on; }
+
 static FastDiv make_fastdiv(uint32_t d) {
   FastDiv f;
   f.d = d;
@@ -2411,6 +2421,14 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
   pl.bnw = C % 128 == 0 ? 128 : (C == 64 && R * S > 1) ? 128 : (C == 16 && R * S * C >= 256 && pl.bmw == 64) ? 256 : 64;
   // variant 12 (A/B): 8-wave 256 x 256 tiles where both channel counts allow them
   if (conv_variant() == 12 && Cout % 256 == 0 && C % 256 == 0) pl.bmw = pl.bnw = 256;
+  // 1x1 with a 64-channel side (DPT_WGRAD_WIDE, A/B knob): one tile spans all 256 channels of
+  // the other side, so neither operand is streamed twice (64->256: x read once instead of per
+  // 128-channel output tile; 256->64: dy likewise)
+  const int wide = wgrad_wide_mode();
+  if (wide && R == 1 && S == 1 && conv_variant() == 0) {
+    if (C == 64 && Cout == 256) { pl.bmw = 256; pl.bnw = 64; }
+    else if (Cout == 64 && C == 256) { pl.bmw = 64; pl.bnw = 256; }
+  }
   const int tiles = (Cout / pl.bmw) * ((R * S * C + pl.bnw - 1) / pl.bnw);
   const int steps = (int)((M + 63) / 64);
   // ~768 blocks (3 per CU) and at least 32 K-steps per split: a split's fp32 partial tile
@@ -2473,7 +2491,7 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
   if (fin != nullptr) {
     a.fin = make_bn_bwd_fin(fin->p1, fin->p2, fin->chunks, fin->C, fin->M, fin->gamma, fin->invstd, fin->dgamma,
                             fin->dbeta, fin->kbuf, fin->kbuf + fin->C, fin->kbuf + 2 * fin->C, -1);
-    if (pl.bmw == 256) {  // the 512-thread variant carries nothing: finalize on its own
+    if (pl.bmw == 256 && pl.bnw == 256) {  // the 512-thread variant carries nothing: finalize on its own
       launch_bn_bwd_finalize(*fin, st);
       a.fin = BnBwdFin{};
     } else {
@@ -2493,6 +2511,8 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
       default: DPT_WH(128, 1); break;
     }
 #undef DPT_WH
+  } else if (pl.bmw == 256 && pl.bnw == 64) {
+    wgrad_launch<256, 64, 1>(grid, block, st, a);
   } else if (pl.bmw == 256) {  // conv_wgrad_plan chose the 8-wave 256 x 256 tile
     if (a.f16) throw std::runtime_error("conv_wgrad: the 256 x 256 variant is bf16 only");
     hipLaunchKernelGGL((conv_wgrad_kernel<256, 256, 2, false, 512>), grid, dim3(512), 0, st, a);

@@ -167,6 +167,7 @@ struct ConvWgradPlan {
   int64_t part_floats;
   int halo = 0;  // 3x3 / stride-1: the three taps of a tap row share one x strip (conv_wgrad_halo_kernel)
 };
+void conv_set_wgrad_wide(int on);   // 1x1 64<->256-channel wgrad in one 256-wide tile (DPT_WGRAD_WIDE)
 void conv_set_wgrad_halo(int mode);  // 0 off, 1-4 forced, 5 auto (default, DPT_WGRAD_HALO)
 ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad, int Ho = 0,
                               int Wo = 0);

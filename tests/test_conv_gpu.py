@@ -940,3 +940,26 @@ def test_wgrad_halo_matches_reference(cuda, shape, mode, dtype):
     torch.testing.assert_close(dw, ref, rtol=1e-3, atol=1e-4 * scale + 1e-3)
     torch.testing.assert_close(dw, base, rtol=1e-4, atol=1e-5 * scale + 1e-4)
     torch.testing.assert_close(dw16.float(), ref, rtol=1e-2, atol=1e-2 * scale)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 14, 14, 256), (3, 256, 9, 7, 64), (1, 64, 5, 5, 256)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_wgrad_wide_1x1_tiles(cuda, shape, dtype):
+    """1x1 backward-weight with one 256-wide tile over the 256-channel side (conv_set_wgrad_wide:
+    256x64 / 64x256 tiles) vs an fp32 reference and the default 128-wide tiles."""
+    N, C, H, W, Cout = shape
+    C_ = ops.native()
+    g = torch.Generator(device=cuda).manual_seed(9)
+    x = torch.randn(N, C, H, W, device=cuda, generator=g).to(dtype).contiguous(memory_format=CL)
+    gy = torch.randn(N, Cout, H, W, device=cuda, generator=g).to(dtype).contiguous(memory_format=CL)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (Cout, C, 1, 1), gy.float())
+    scale = ref.abs().max().item()
+    try:
+        C_.conv_set_wgrad_wide(0)
+        base = C_.conv_wgrad(gy, x, [Cout, C, 1, 1], 1, 0, True)
+        C_.conv_set_wgrad_wide(1)
+        dw = C_.conv_wgrad(gy, x, [Cout, C, 1, 1], 1, 0, True)
+    finally:
+        C_.conv_set_wgrad_wide(0)
+    torch.testing.assert_close(dw, ref, rtol=1e-3, atol=1e-4 * scale + 1e-3)
+    torch.testing.assert_close(dw, base, rtol=1e-4, atol=1e-5 * scale + 1e-4)
