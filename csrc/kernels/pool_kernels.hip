@@ -658,7 +658,15 @@ __global__ __launch_bounds__(kBlock) void gap_bwd_bnr_kernel(const void* __restr
 
 int gap_bwd_bnr_chunks(int64_t M, int64_t C) {
   const int rpp = kBlock / (int)(C / 8);
-  int64_t rpb = (M + 1023) / 1024;  // ~1024 blocks
+  // ~one block per CU (DPT_GAP_BNR_BLOCKS): each block ends with C scattered stores per partial
+  // array into the [C][blocks] layout the finalize reads, which at C = 2048 costs more than the
+  // extra rows per block - ResNet-50's tail, 7x7x2048 x 256 images: 1024 blocks 62 us, 256
+  // blocks 42 us, 128 blocks 62 us
+  static const int target = [] {
+    const char* e = std::getenv("DPT_GAP_BNR_BLOCKS");
+    return e ? std::max(1, std::atoi(e)) : 256;
+  }();
+  int64_t rpb = (M + target - 1) / target;
   rpb = (rpb + rpp - 1) / rpp * rpp;
   return (int)((M + rpb - 1) / rpb);
 }
