@@ -364,11 +364,12 @@ __global__ __launch_bounds__(kBlock) void maxpool3s2_bwd_kernel(const void* __re
                                                                 const float* __restrict__ bn_coef = nullptr,
                                                                 float* __restrict__ bp1 = nullptr,
                                                                 float* __restrict__ bp2 = nullptr) {
-  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   float s1[8], s2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
-  if (t < total) {
+  // grid-stride (BNS launches at most kPoolBnBlocks blocks: one partial per block and channel;
+  // the stride is a multiple of kBlock, so a lane's channel group never changes)
+  for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < total; t += gridDim.x * kBlock) {
   const uint32_t cg8 = (uint32_t)C >> 3;
   const int cg = (int)(t % cg8);
   uint32_t q = t / cg8;
@@ -457,7 +458,7 @@ __global__ __launch_bounds__(kBlock) void maxpool3s2_bwd_kernel(const void* __re
       }
     }
   }
-  }  // t < total
+  }  // grid-stride loop
   if (BNS) {
     // threads of one channel group: t % (C/8) equal -> lanes l, l + C/8, ... then the 4 waves
     __shared__ float red[2][kBlock / 64][64 * 8];
@@ -554,9 +555,22 @@ void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t
   else maxpool_fwd_dispatch<uint64_t>(dtype, grid, x, y, idx, B, H, W, C, Ho, Wo, K, S, P, s);
 }
 
+// Blocks of the statistics-summing 3x3/s2 max-pool backward: capped, because every block ends
+// with C scattered partial stores per array ([C][blocks], the layout the finalize reads) and the
+// finalize reads them all - ResNet-50's stem at batch 256 had 25,088 blocks (DPT_POOL_BN_BLOCKS;
+// in-step rocprofv3: uncapped 268 us, 4096 blocks 241, 2048 237, 1024 234, and the stem's BN
+// finalize drops from ~21 us to a few, profiles/pool_bn_blocks_r2.txt).
+static int pool_bn_blocks() {
+  static const int v = [] {
+    const char* e = std::getenv("DPT_POOL_BN_BLOCKS");
+    return e ? std::max(1, std::atoi(e)) : 1024;
+  }();
+  return v;
+}
+
 int maxpool_bwd_bn_chunks(int64_t B, int H, int W, int C) {
   const int64_t total2 = B * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
-  return (int)((total2 + kBlock - 1) / kBlock);
+  return (int)std::min<int64_t>((total2 + kBlock - 1) / kBlock, pool_bn_blocks());
 }
 
 void launch_maxpool_bwd(int dtype, const void* dy, const void* dy2, const uint8_t* idx, void* dx, int64_t B, int H,
@@ -567,8 +581,11 @@ void launch_maxpool_bwd(int dtype, const void* dy, const void* dy2, const uint8_
   const int Ha = (H + 1) / 2, Wa = (W + 1) / 2;
   const int64_t total2 = B * Ha * Wa * (C / 8);
   if (K == 3 && S == 2 && P == 1 && Ho == Ha && Wo == Wa && total2 + kBlock < (int64_t(1) << 32)) {
-    const dim3 g2((unsigned)((total2 + kBlock - 1) / kBlock)), block(kBlock);
+    dim3 g2((unsigned)((total2 + kBlock - 1) / kBlock)), block(kBlock);
     if (bnx != nullptr) {
+      g2.x = (unsigned)maxpool_bwd_bn_chunks(B, H, W, C);  // grid-stride; t + stride stays < 2^32
+      if (total2 + (int64_t)g2.x * kBlock >= (int64_t(1) << 32))
+        throw std::runtime_error("maxpool_bwd: too many elements for the fused statistics path");
       switch (dtype) {
         case 0: hipLaunchKernelGGL((maxpool3s2_bwd_kernel<0, true>), g2, block, 0, s, dy, dy2, idx, dx, H, W, C, Ho, Wo, Ha, Wa, (uint32_t)total2, bnx, bn_mean, bn_coef, bp1, bp2); break;
         case 1: hipLaunchKernelGGL((maxpool3s2_bwd_kernel<1, true>), g2, block, 0, s, dy, dy2, idx, dx, H, W, C, Ho, Wo, Ha, Wa, (uint32_t)total2, bnx, bn_mean, bn_coef, bp1, bp2); break;
