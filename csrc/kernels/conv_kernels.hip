@@ -1884,7 +1884,11 @@ static int g_conv_halo = -1;
 static int halo_hb(const ConvFwdArgs& a, int bn) {
   if (g_conv_halo == 2) return 1;
   if (g_conv_halo == 3) return 3;
-  return (int64_t)a.m_tiles * (a.Cout / bn) <= 512 ? 3 : 1;
+  static const int hb3_tiles = [] {  // DPT_CONV_HALO_HB3_TILES: the grid-size cut-off (A/B knob)
+    const char* e = std::getenv("DPT_CONV_HALO_HB3_TILES");
+    return e ? std::atoi(e) : 512;
+  }();
+  return (int64_t)a.m_tiles * (a.Cout / bn) <= hb3_tiles ? 3 : 1;
 }
 static bool halo_ok(const ConvFwdArgs& a) {
   if (g_conv_halo < 0) {
