@@ -1,8 +1,18 @@
 """Headline benchmark: ResNet-50 bf16 AMP data-parallel training throughput (images/s, whole job).
 
-    python bench.py [--gpus N --steps K --warmup W]                       # N = 1
+    python bench.py [--gpus N --steps K --warmup W]       # N ranks, launched by this script
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+Run directly with ``--gpus N > 1`` (no launcher environment), the script is its own launcher:
+the parent process spawns N rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=
+127.0.0.1 / a free MASTER_PORT - the env:// contract of reference train_ddp.py:50,61-65)
+before anything touches the GPU, waits for them and exits with the worst rank's status.  It
+fails (non-zero) instead of running fewer ranks: fewer than N visible GPUs, a dead rank, or
+a launcher WORLD_SIZE that differs from ``--gpus`` are errors.  The JSON line records the
+rank count the framework communicator was created with (``comm.world_size``), each rank's
+device (``comm.rank_devices``), the launcher and every DPT_/NCCL_/RCCL_/MIOPEN_/HIP_ variable
+in effect (``config.env``), so a record can be reproduced from itself.
 
 Metric/config from BASELINE.json: "images/sec (whole node) ResNet-50 bf16 at 1/2/4/8
 MI355X; % step in all-reduce".  Synthetic ImageNet-shape data (3x224x224, 1000 classes),
@@ -20,6 +30,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -47,6 +60,8 @@ def parse(argv=None):
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adam", "adamw"])
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--first-bucket-mb", type=float, default=1.0)
+    ap.add_argument("--last-bucket-mb", type=float, default=1.0,
+                    help="cap of the bucket that becomes ready last (0 = torch DDP's plan)")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--no-fused-bn", action="store_true", help="A/B: MIOpen BN + separate ReLU/add")
     ap.add_argument("--find", action="store_true",
@@ -72,8 +87,99 @@ def parse(argv=None):
                          "1-GPU box (RCCL itself is not exercised; timings are not representative)")
     ap.add_argument("--fake-pg", action="store_true",
                     help="testing: run as rank 0 of a --gpus-rank job on torch's fake process group (CPU)")
+    ap.add_argument("--fail-rank", type=int, default=-1,
+                    help="testing: this rank exits with status 17 right after the process group is up")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
+
+
+ENV_PREFIXES = ("DPT_", "NCCL_", "RCCL_", "MIOPEN_", "HIP_", "HSA_", "AMD_", "GPU_MAX_HW_QUEUES",
+                "PYTORCH_TUNABLEOP", "TORCH_NCCL", "OMP_NUM_THREADS")
+CHILD_MARK = "DPT_BENCH_LAUNCHER"
+
+
+def env_in_effect() -> dict:
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith(ENV_PREFIXES) and k != CHILD_MARK}
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _visible_gpus() -> int:
+    """Device count WITHOUT initialising the GPU runtime in this (launcher) process."""
+    try:
+        return int(torch.cuda.device_count())
+    except Exception:
+        return 0
+
+
+def launch_ranks(a, argv, grace_s: float = 30.0) -> int:
+    """Spawn ``--gpus`` rank processes of this script (self-launch, no torchrun needed).
+
+    Nothing here touches the GPU: the children are fresh interpreters.  Returns the worst
+    child exit status; when one rank fails, the survivors get ``grace_s`` to finish (they
+    normally error out of their collective) and are then terminated, so a dead peer can not
+    leave the node hanging."""
+    n = a.gpus
+    ngpu = _visible_gpus()
+    if a.rehearse_shared_gpu:
+        if ngpu < 1:
+            print("error: --rehearse-shared-gpu needs one visible GPU", file=sys.stderr)
+            return 2
+    elif ngpu == 0:
+        print(f"bench: no GPU visible - {n} gloo ranks on the CPU", file=sys.stderr)
+    elif ngpu < n:
+        print(f"error: --gpus {n} but only {ngpu} GPU(s) are visible; refusing to run fewer ranks",
+              file=sys.stderr)
+        return 2
+    port = _free_port()
+    script = os.path.abspath(__file__)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", ROLE_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env[CHILD_MARK] = "self"
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, script, *argv], env=env))
+    rcs = [None] * n
+    failed_at = None
+    try:
+        while any(rc is None for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    rcs[i] = p.poll()
+                    if rcs[i] not in (None, 0) and failed_at is None:
+                        failed_at = time.time()
+                        print(f"bench: rank {i} exited with status {rcs[i]}", file=sys.stderr)
+            if failed_at is not None and time.time() - failed_at > grace_s:
+                for i, p in enumerate(procs):
+                    if rcs[i] is None:
+                        p.terminate()
+                deadline = time.time() + 10
+                for i, p in enumerate(procs):
+                    if rcs[i] is None:
+                        try:
+                            rcs[i] = p.wait(timeout=max(0.1, deadline - time.time()))
+                        except subprocess.TimeoutExpired:
+                            p.kill()
+                            rcs[i] = p.wait()
+                break
+            time.sleep(0.1)
+    except KeyboardInterrupt:
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGINT)
+        for p in procs:
+            p.wait()
+        return 130
+    bad = [rc for rc in rcs if rc != 0]
+    if not bad:
+        return 0
+    rc = bad[0]
+    return 128 - rc if rc < 0 else rc
 
 
 def _red_dev(device):
@@ -90,6 +196,20 @@ def _rccl_version():
         return None
 
 
+def _rank_devices(device, ws):
+    """Every rank's device (index and PCI bus id): proves N distinct GPUs took part."""
+    mine = {"device": str(device)}
+    if device.type == "cuda":
+        p = torch.cuda.get_device_properties(device)
+        mine["pci_bus_id"] = getattr(p, "pci_bus_id", None)
+        mine["name"] = p.name
+    if ws > 1 and dist.is_initialized() and dist.get_backend() != "fake":
+        out = [None] * ws
+        dist.all_gather_object(out, mine)
+        return out
+    return [mine]
+
+
 def train_args(a):
     from distributed_pytorch_training_amd.config import parse_args
 
@@ -97,6 +217,7 @@ def train_args(a):
             "--image-size", str(a.image_size), "--num-classes", str(a.num_classes),
             "--impl", a.impl, "--amp-dtype", a.amp_dtype, "--optimizer", a.optimizer,
             "--bucket-cap-mb", str(a.bucket_cap_mb), "--first-bucket-mb", str(a.first_bucket_mb),
+            "--last-bucket-mb", str(a.last_bucket_mb),
             "--grad-dtype", a.grad_dtype, "--lr", "0.1", "--momentum", "0.9", "--weight-decay", "5e-4",
             "--comm", a.comm, "--rccl-channels", str(a.rccl_channels)]
     if not a.no_amp:
@@ -104,8 +225,9 @@ def train_args(a):
     argv.append("--no-channels-last" if a.no_channels_last else "--channels-last")
     if a.no_fused_bn:
         argv.append("--no-fused-bn")
-    if a.cuda_graph:
-        argv.append("--cuda-graph")
+    # the headline bench keeps hipGraph replay opt-in (the framework default turns it on for
+    # launch-bound steps only; the profiled window needs eager steps)
+    argv.append("--cuda-graph" if a.cuda_graph else "--no-cuda-graph")
     if a.no_weight_shadow:
         argv.append("--no-weight-shadow")
     if a.no_native_conv:
@@ -114,7 +236,19 @@ def train_args(a):
 
 
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = parse(argv)
+    env_ws = os.environ.get("WORLD_SIZE")
+    if a.fake_pg:
+        pass
+    elif env_ws is None:
+        if a.gpus > 1:
+            return launch_ranks(a, argv)
+    elif int(env_ws) != a.gpus:
+        print(f"error: --gpus {a.gpus} but the launcher started WORLD_SIZE={env_ws} ranks", file=sys.stderr)
+        return 2
+    launcher = ("fake" if a.fake_pg else os.environ.get(CHILD_MARK) or
+                ("torchrun" if env_ws is not None else "none"))
     from distributed_pytorch_training_amd.data import SyntheticLoader
     from distributed_pytorch_training_amd.engine.trainer import Trainer
     from distributed_pytorch_training_amd.models import build_model
@@ -138,11 +272,19 @@ def main(argv=None) -> int:
         dist.init_process_group("fake", store=FakeStore(), rank=0, world_size=a.gpus)
         info = DistInfo(0, a.gpus, 0, "fake", torch.device("cpu"))
     else:
+        if (env_ws is not None and int(env_ws) > 1 and _visible_gpus() > 0
+                and _visible_gpus() < int(os.environ.get("LOCAL_WORLD_SIZE", env_ws))):
+            print(f"error: {os.environ.get('LOCAL_WORLD_SIZE', env_ws)} local ranks but only "
+                  f"{_visible_gpus()} GPU(s) visible", file=sys.stderr)
+            return 2
         info = init_distributed("auto")
     gemm_db = setup_tunableop() if (a.impl == "native" and info.device.type == "cuda") else False
     rank, ws, device = info.rank, info.world_size, info.device
-    if ws != a.gpus and rank == 0:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={ws}; reporting WORLD_SIZE", file=sys.stderr)
+    if ws != a.gpus:
+        print(f"error: --gpus {a.gpus} but the process group has {ws} rank(s)", file=sys.stderr)
+        return 2
+    if a.fail_rank == rank:
+        os._exit(17)
     set_seed(0, rank)
     torch.backends.cudnn.benchmark = bool(a.find)
 
@@ -238,13 +380,24 @@ def main(argv=None) -> int:
     if prof:
         rec["sync_profile"] = {k: round(v, 4) if isinstance(v, float) else v for k, v in prof.items()}
     ddp = trainer.ddp
-    rec["comm"] = {"kind": (ddp.comm.kind if ddp is not None and ddp.comm is not None else
+    comm = ddp.comm if ddp is not None else None
+    rec["comm"] = {"kind": (comm.kind if comm is not None else
                             ("gloo" if ws > 1 and a.impl == "native" else
                              ("torch-ddp" if ws > 1 else "none"))),
+                   # rank count of the framework communicator itself (the process group's when
+                   # there is none: gloo / torch DDP)
+                   "world_size": int(comm.world_size) if comm is not None else ws,
+                   "pg_backend": dist.get_backend() if dist.is_initialized() else None,
+                   "rank_devices": _rank_devices(device, ws),
                    "buckets_mib": [round(v, 3) for v in ddp.bucket_sizes_mib()] if ddp is not None else None,
                    "bucket_cap_mb": a.bucket_cap_mb, "first_bucket_mb": a.first_bucket_mb,
-                   "grad_dtype": a.grad_dtype, "rccl_channels": a.rccl_channels or None,
+                   "last_bucket_mb": a.last_bucket_mb,
+                   "grad_dtype": a.grad_dtype,
+                   "rccl_channels": (int(comm.max_ctas) or None) if comm is not None and hasattr(comm, "max_ctas")
+                                    else None,
                    "rccl_version": _rccl_version()}
+    rec["config"]["launcher"] = launcher
+    rec["config"]["env"] = env_in_effect()
     if rank == 0:
         line = json.dumps(rec)
         print(line, flush=True)

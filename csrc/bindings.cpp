@@ -1236,11 +1236,25 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("sequence_hash", &dpt::Collective::sequence_hash)
       .def_property_readonly("rank", &dpt::Collective::rank)
       .def_property_readonly("world_size", &dpt::Collective::world_size)
-      .def_property_readonly("device", &dpt::Collective::device);
+      .def_property_readonly("device", &dpt::Collective::device)
+      .def("track", [](dpt::Collective& c) {
+             c10::hip::HIPGuard guard(c.device());
+             c.track(c10::hip::getCurrentHIPStream(c.device()).stream());
+           }, "hand the watchdog a completion marker for the work enqueued on the current stream")
+      .def("_test_spin", [](dpt::Collective& c, double ms, bool on_current_stream) {
+             TORCH_CHECK(ms >= 0 && ms <= 20000, "spin: 0..20000 ms");
+             c10::hip::HIPGuard guard(c.device());
+             dpt::launch_spin(ms, on_current_stream ? c10::hip::getCurrentHIPStream(c.device()).stream()
+                                                    : c.stream());
+           }, py::arg("ms"), py::arg("on_current_stream") = false,
+           "test hook: enqueue a wall-clock busy-wait on the communicator (or current) stream");
 
   py::class_<dpt::RcclComm, dpt::Collective, std::shared_ptr<dpt::RcclComm>>(m, "RcclComm")
-      .def(py::init<const std::string&, int, int, int>(), py::arg("unique_id"), py::arg("rank"),
-           py::arg("world_size"), py::arg("device"))
+      .def(py::init<const std::string&, int, int, int, int, int>(), py::arg("unique_id"), py::arg("rank"),
+           py::arg("world_size"), py::arg("device"), py::arg("min_ctas") = 0, py::arg("max_ctas") = 0)
+      .def_property_readonly("min_ctas", &dpt::RcclComm::min_ctas)
+      .def_property_readonly("max_ctas", &dpt::RcclComm::max_ctas)
+      .def("inject_async_error", &dpt::RcclComm::inject_async_error, py::arg("message"))
       .def_static("new_unique_id", []() { return py::bytes(dpt::RcclComm::new_unique_id()); })
       .def("enable_watchdog", &dpt::RcclComm::enable_watchdog, py::arg("timeout_s"), py::arg("poll_s") = 0.5,
            py::arg("exit_grace_s") = 30.0)
@@ -1287,6 +1301,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("backward_count", &dpt::Reducer::backward_count)
       .def("bucket_times_ms", &dpt::Reducer::bucket_times_ms, py::arg("slot") = -1)
       .def("step_times_ms", &dpt::Reducer::step_times_ms, py::arg("slot") = -1)
+      .def("bucket_start_ms", &dpt::Reducer::bucket_start_ms, py::arg("slot") = -1)
       .def("set_profile_slots", &dpt::Reducer::set_profile_slots, py::arg("n"))
       .def_property_readonly("profile_slots", &dpt::Reducer::profile_slots)
       .def_property_readonly("last_slot", &dpt::Reducer::last_slot)

@@ -18,7 +18,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstddef>
+#include <cstdint>
 #include <string>
 
 namespace dpt {
@@ -55,18 +57,24 @@ class Collective {
   // Host touch point: throws if the watchdog (or the backend) recorded an error.
   virtual void check() const {}
   virtual std::string kind() const = 0;
+  // Hand the watchdog (if any) a completion marker for the work enqueued on `stream` so far:
+  // collectives replayed from a captured hipGraph are not seen by all_reduce()/broadcast(),
+  // so the graph engine calls this after every replay.  No-op for backends without one.
+  virtual void track(hipStream_t /*stream*/) {}
   // Collectives issued so far and a running hash of their (kind, count, dtype, root)
-  // sequence: compared across ranks by the debug sequence check (parallel/ddp.py).
-  uint64_t ops() const { return ops_; }
-  uint64_t sequence_hash() const { return seq_hash_; }
+  // sequence: compared across ranks by the debug sequence check (parallel/ddp.py).  Written
+  // by the autograd thread (reducer, under its mutex), read by the main thread: atomics.
+  uint64_t ops() const { return ops_.load(std::memory_order_acquire); }
+  uint64_t sequence_hash() const { return seq_hash_.load(std::memory_order_acquire); }
 
  protected:
   void note_op(int kind, size_t count, WireType t, int root) {
-    ++ops_;
     uint64_t v = ((uint64_t)kind << 56) ^ ((uint64_t)(int)t << 48) ^ ((uint64_t)(root & 0xff) << 40) ^ (uint64_t)count;
-    seq_hash_ = (seq_hash_ ^ v) * 0x100000001b3ull;  // FNV-1a style
+    // single writer at a time (callers are serialised); FNV-1a style running hash
+    seq_hash_.store((seq_hash_.load(std::memory_order_relaxed) ^ v) * 0x100000001b3ull, std::memory_order_release);
+    ops_.fetch_add(1, std::memory_order_release);
   }
-  uint64_t ops_ = 0, seq_hash_ = 0xcbf29ce484222325ull;
+  std::atomic<uint64_t> ops_{0}, seq_hash_{0xcbf29ce484222325ull};
 };
 
 }  // namespace dpt

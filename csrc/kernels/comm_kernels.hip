@@ -69,4 +69,26 @@ void launch_unpack_bf16(const uint16_t* src, float* dst, int64_t n, const float*
                      host_factor, found_inf);
 }
 
+// Test-only: one wave busy-waits `ticks` of the constant-rate wall clock, then exits.  The
+// watchdog GPU tests enqueue it on the communicator stream ahead of a collective to model a
+// peer that never arrives.  Bounded twice: by the clock and by an iteration cap, so every
+// wave exits even if the clock read misbehaved.
+__global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks, uint64_t max_iters) {
+  const uint64_t t0 = wall_clock64();
+  for (uint64_t it = 0; it < max_iters; ++it) {
+    if (wall_clock64() - t0 >= ticks) break;
+    __builtin_amdgcn_s_sleep(100);
+  }
+}
+
+void launch_spin(double ms, hipStream_t s) {
+  int dev = 0, khz = 0;
+  hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+  const uint64_t ticks = (uint64_t)(ms * (double)khz);
+  // s_sleep 100 ~ 6400 cycles >= ~2 us at any shader clock: 4x the needed count is plenty
+  const uint64_t max_iters = (uint64_t)(ms * 1000.0) * 4 + 1000;
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, s, ticks, max_iters);
+}
+
 }  // namespace dpt

@@ -33,6 +33,8 @@ void launch_optim_tail(float* scale, int* growth_tracker, float* found_inf, floa
 void launch_pack_bf16(const float* src, uint16_t* dst, int64_t n, hipStream_t s);
 void launch_unpack_bf16(const uint16_t* src, float* dst, int64_t n, const float* scale,
                         float host_factor, float* found_inf, hipStream_t s);
+// test-only: a 1-wave kernel that busy-waits `ms` milliseconds of wall clock
+void launch_spin(double ms, hipStream_t s);
 
 // metrics_kernels.hip  (dtype: 0 f32, 1 bf16, 2 f16)
 void launch_metrics(const void* logits, int dtype, int64_t rows, int64_t cols, int64_t ld,

@@ -38,8 +38,9 @@ std::string RcclComm::new_unique_id() {
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
-RcclComm::RcclComm(const std::string& unique_id, int rank, int world_size, int device)
-    : rank_(rank), world_size_(world_size), device_(device) {
+RcclComm::RcclComm(const std::string& unique_id, int rank, int world_size, int device, int min_ctas,
+                   int max_ctas)
+    : rank_(rank), world_size_(world_size), device_(device), min_ctas_(min_ctas), max_ctas_(max_ctas) {
   if (unique_id.size() != sizeof(ncclUniqueId))
     throw std::invalid_argument("RcclComm: unique id must be " + std::to_string(sizeof(ncclUniqueId)) + " bytes");
   ncclUniqueId id;
@@ -49,7 +50,17 @@ RcclComm::RcclComm(const std::string& unique_id, int rank, int world_size, int d
   int lo = 0, hi = 0;
   DPT_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   DPT_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
-  DPT_RCCL_CHECK(ncclCommInitRank(&comm_, world_size, id, rank));
+  if (min_ctas > 0 || max_ctas > 0) {
+    // Only fields every config version since 2.14 carries are set; size/magic/version come
+    // from the header's initializer and the library copies what it knows.
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    if (min_ctas > 0) cfg.minCTAs = min_ctas;
+    if (max_ctas > 0) cfg.maxCTAs = max_ctas;
+    cfg.blocking = 1;
+    DPT_RCCL_CHECK(ncclCommInitRankConfig(&comm_, world_size, id, rank, &cfg));
+  } else {
+    DPT_RCCL_CHECK(ncclCommInitRank(&comm_, world_size, id, rank));
+  }
 }
 
 RcclComm::~RcclComm() { destroy(); }
@@ -61,7 +72,20 @@ void RcclComm::enable_watchdog(double timeout_s, double poll_s, double exit_grac
       [this] { return this->async_error(); });
 }
 
+void RcclComm::inject_async_error(const std::string& msg) {
+  std::lock_guard<std::mutex> lk(inject_mu_);
+  injected_error_ = msg;
+}
+
+void RcclComm::track(hipStream_t stream) {
+  if (watchdog_ && !aborted_.load()) watchdog_->track(stream ? stream : stream_);
+}
+
 std::string RcclComm::async_error() const {
+  {
+    std::lock_guard<std::mutex> lk(inject_mu_);
+    if (!injected_error_.empty()) return injected_error_;
+  }
   if (comm_ == nullptr || aborted_.load()) return "";
   ncclResult_t r = ncclSuccess;
   if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return "";

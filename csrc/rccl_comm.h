@@ -18,6 +18,7 @@
 
 #include <atomic>
 #include <memory>
+#include <mutex>
 #include <string>
 
 #include "comm.h"
@@ -27,7 +28,12 @@ namespace dpt {
 
 class RcclComm : public Collective {
  public:
-  RcclComm(const std::string& unique_id, int rank, int world_size, int device);
+  // `min_ctas` / `max_ctas` > 0: per-communicator RCCL channel (CTA) bounds through
+  // ncclCommInitRankConfig (ncclConfig_t.minCTAs / maxCTAs) - only this communicator is
+  // affected, unlike the process-wide NCCL_MIN/MAX_NCHANNELS environment, which RCCL reads
+  // once per process (torch's own communicator may already have read it).  0 = RCCL default.
+  RcclComm(const std::string& unique_id, int rank, int world_size, int device, int min_ctas = 0,
+           int max_ctas = 0);
   ~RcclComm() override;
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
@@ -45,6 +51,9 @@ class RcclComm : public Collective {
   void destroy() override;
   void check() const override;
   std::string kind() const override { return "rccl"; }
+  void track(hipStream_t stream) override;
+  int min_ctas() const { return min_ctas_; }
+  int max_ctas() const { return max_ctas_; }
 
   // Start the watchdog: a collective older than `timeout_s` (or an RCCL async error) aborts
   // the communicator; `exit_grace_s` < 0 disables the last-resort process exit.
@@ -52,8 +61,14 @@ class RcclComm : public Collective {
   bool watchdog_tripped() const { return watchdog_ && watchdog_->tripped(); }
   size_t watchdog_outstanding() const { return watchdog_ ? watchdog_->outstanding() : 0; }
   std::string async_error() const;
+  // Test hook: make async_error() report `msg` (exercises the watchdog's async-error branch
+  // without a broken peer).  Empty string clears it.
+  void inject_async_error(const std::string& msg);
 
  private:
+  int min_ctas_ = 0, max_ctas_ = 0;
+  std::string injected_error_;
+  mutable std::mutex inject_mu_;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   int rank_, world_size_, device_;

@@ -195,6 +195,10 @@ void Reducer::mark_ready(int64_t index) {
   }
   if (steal_) stolen_[index] = params_[index].grad();
   const int64_t b = param_bucket_[index];
+  if (debug_ && launched_[b] == 2)
+    throw std::runtime_error("Reducer(debug): gradient of parameter " + std::to_string(index) +
+                             " arrived after its bucket " + std::to_string(b) +
+                             " was already all-reduced (it would be missing from the sum)");
   if (--pending_[b] == 0) {
     if (gpu_) {
       // The gradient was produced on this thread's current stream.
@@ -248,8 +252,6 @@ void Reducer::gather_bucket(int64_t b, hipStream_t s) {
 }
 
 void Reducer::launch_bucket(int64_t b) {
-  if (debug_ && launched_[b] == 2)
-    throw std::runtime_error("Reducer(debug): bucket " + std::to_string(b) + " launched twice in one backward");
   const int64_t off = bucket_offsets_[b], n = bucket_numels_[b];
   if (!gpu_) {
     py::gil_scoped_acquire g;
@@ -346,6 +348,21 @@ std::vector<double> Reducer::bucket_times_ms(int64_t slot) {
     if (hipEventElapsedTime(&ms, ev_start_[pe], ev_end_[pe]) != hipSuccess) ms = -1.f;
     out.push_back(ms);
   }
+  (void)hipGetLastError();  // a not-yet-complete event leaves hipErrorNotReady pending: clear it
+  return out;
+}
+
+std::vector<double> Reducer::bucket_start_ms(int64_t slot) {
+  std::vector<double> out;
+  if (!gpu_ || !profile_ || !comm_ || backward_count_ == 0) return out;
+  if (slot < 0) slot = last_slot();
+  const size_t s = (size_t)(slot % slots_), B = bucket_offsets_.size();
+  for (size_t b = 0; b < B; ++b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ev_first_[s], ev_start_[s * B + b]) != hipSuccess) ms = -1.f;
+    out.push_back(ms);
+  }
+  (void)hipGetLastError();
   return out;
 }
 
@@ -357,9 +374,11 @@ std::vector<double> Reducer::step_times_ms(int64_t slot) {
   if (slot < 0) slot = last_slot();
   const size_t s = (size_t)(slot % slots_), B = bucket_offsets_.size();
   float a = 0.f, b = 0.f, c = 0.f;
-  hipEventElapsedTime(&a, ev_first_[s], ev_bwd_end_[s]);
-  hipEventElapsedTime(&b, ev_bwd_end_[s], ev_done_[s]);
-  hipEventElapsedTime(&c, ev_start_[s * B], ev_done_[s]);
+  // -1 marks a pair that is not complete yet (the caller read the slot too early)
+  if (hipEventElapsedTime(&a, ev_first_[s], ev_bwd_end_[s]) != hipSuccess) a = -1.f;
+  if (hipEventElapsedTime(&b, ev_bwd_end_[s], ev_done_[s]) != hipSuccess) b = -1.f;
+  if (hipEventElapsedTime(&c, ev_start_[s * B], ev_done_[s]) != hipSuccess) c = -1.f;
+  (void)hipGetLastError();
   out = {a, b, c};
   return out;
 }

@@ -71,6 +71,9 @@ class Reducer {
   int64_t last_slot() const { return backward_count_ > 0 ? (backward_count_ - 1) % slots_ : -1; }
   std::vector<double> bucket_times_ms(int64_t slot = -1);
   std::vector<double> step_times_ms(int64_t slot = -1);
+  // Per bucket: first gradient ready -> the bucket's collective starts on the comm stream (its
+  // ready time when the comm stream is idle, e.g. a 1-rank communicator).  -1 = not complete.
+  std::vector<double> bucket_start_ms(int64_t slot = -1);
   void remove_hooks();
 
  private:

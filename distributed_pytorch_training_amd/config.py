@@ -70,6 +70,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="gradient bucket size cap in MiB")
     g.add_argument("--first-bucket-mb", default=1.0, type=float,
                    help="first (last-layer) bucket cap in MiB")
+    g.add_argument("--last-bucket-mb", default=1.0, type=float,
+                   help="native impl: cap of the bucket that becomes ready last (its all-reduce can not "
+                        "overlap backward); 0 = torch DDP's plan, where it is whatever is left over")
     g.add_argument("--no-broadcast-buffers", dest="broadcast_buffers", action="store_false",
                    help="do not broadcast BN buffers from rank 0 before each forward")
     g.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
@@ -113,10 +116,12 @@ def build_parser() -> argparse.ArgumentParser:
                    help="device collective of the native reducer: rccl (RCCL over xGMI) or host (gloo "
                         "through pinned host staging - lets several ranks share one GPU; debug only)")
     g.add_argument("--rccl-channels", default=0, type=int,
-                   help="export NCCL_MIN/MAX_NCHANNELS before the RCCL communicator is created "
-                        "(0 = RCCL's topology default; >= 7 spans all xGMI links of an MI355X)")
+                   help="RCCL channels (CTAs) of the framework's gradient communicator, set per "
+                        "communicator through ncclConfig_t minCTAs/maxCTAs (0 = RCCL's topology default; "
+                        ">= 7 spans all xGMI links of an MI355X)")
     g.add_argument("--ddp-debug", action="store_true",
-                   help="debug: reducer assertions (double ready-mark, double bucket launch) and a "
+                   help="debug: reducer assertions (double ready-mark, a gradient arriving after its "
+                        "bucket was already all-reduced) and a "
                         "cross-rank collective-sequence check at every consistency check")
     g.add_argument("--amp-val", action="store_true",
                    help="run validation under autocast too (the reference validates in fp32)")
@@ -126,8 +131,12 @@ def build_parser() -> argparse.ArgumentParser:
                         "default sync-to-sync window, which has no per-step host sync")
     g.add_argument("--fault-inject", default=None, type=str, metavar="RANK:STEP",
                    help="testing: rank RANK exits abruptly (os._exit(17)) before global step STEP")
-    g.add_argument("--cuda-graph", action="store_true",
-                   help="capture the training step in a hipGraph (static shapes, native impl)")
+    g.add_argument("--cuda-graph", dest="cuda_graph", action="store_true", default=None,
+                   help="capture the training step in a hipGraph (static shapes, native impl); "
+                        "default: on when the step is launch-bound (per-GPU batch x pixels <= 2^18, "
+                        "e.g. the reference's ResNet-18 / CIFAR), off otherwise")
+    g.add_argument("--no-cuda-graph", dest="cuda_graph", action="store_false",
+                   help="never replay the step as a hipGraph")
     return p
 
 

@@ -114,9 +114,13 @@ class Trainer:
             shadow = torch.bfloat16 if self.amp_dtype == "bf16" else torch.float16
         self.ddp = NativeDDP(model, rank=self.rank, world_size=self.world_size, device=self.device,
                              bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb,
+                             last_bucket_mb=getattr(args, "last_bucket_mb", 0.0),
                              broadcast_buffers=args.broadcast_buffers, grad_dtype=args.grad_dtype,
                              found_inf=self.scaler.found_inf, scale=self.scaler.scale_tensor,
-                             check_inf=self.amp, profile=self.timeline.enabled, comm=comm,
+                             check_inf=self.amp, profile=self.timeline.enabled,
+                             # a step's comm events are read max_pending steps later: they must
+                             # still be that step's (one event slot per unresolved step + 1)
+                             profile_slots=self.timeline.max_pending + 1, comm=comm,
                              weight_shadow=shadow, comm_kind=getattr(args, "comm", "rccl"),
                              timeout_s=getattr(args, "dist_timeout", None),
                              rccl_channels=getattr(args, "rccl_channels", 0),
@@ -126,8 +130,11 @@ class Trainer:
         self.optimizer = build_optimizer(args.optimizer, self.ddp.arena, args, params_in_order)
         self.metrics = torch.zeros(3, dtype=torch.float64, device=self.device)
         self.graphed = None
-        if getattr(args, "cuda_graph", False) and self.device.type == "cuda":
-            from .graph import GraphedStep
+        from .graph import GraphedStep, auto_enabled
+        cg = getattr(args, "cuda_graph", False)
+        if cg is None:      # default: replay launch-bound steps (engine/graph.py)
+            cg = auto_enabled(args, self.device)
+        if cg and self.device.type == "cuda":
             self.graphed = GraphedStep(self)
 
     def _init_torch(self, model: nn.Module) -> None:

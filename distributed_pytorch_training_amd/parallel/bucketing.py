@@ -10,6 +10,14 @@ backward, then the regular cap (25 MiB).  ``assign_buckets`` reproduces
 Bucket caps are a first-class tuning knob on MI355X: an all-reduce over 8 GPUs on 7
 point-to-point xGMI links wants per-channel chunks past the latency knee, so the bench
 sweeps caps rather than assuming NVSwitch-era defaults.
+
+Tail cap (``last_bucket_mb``, not in torch DDP): the bucket that becomes ready LAST can not
+overlap any backward compute - its all-reduce is exposed by construction.  With the plain
+policy it is whatever is left over (ResNet-50: the stem + layer1, 9.3 MiB; ViT-B/16: the
+patch embedding, class token and position embedding), so the plan closes the longest
+suffix of the ready order that fits the tail cap (at least one tensor) as its own bucket:
+the tensors before it are reduced while the last layers' backward still runs, and only a
+small, latency-bound collective is left after backward (docs/DESIGN.md §3.3).
 """
 from __future__ import annotations
 
@@ -52,12 +60,36 @@ class BucketPlan:
         return [n * elem_bytes / MiB for n in self.numels]
 
 
-def plan_for_arena(arena, bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0) -> BucketPlan:
+def tail_split(sizes_bytes: Sequence[int], last_cap_bytes: int) -> int:
+    """Index where the tail bucket starts: the longest suffix whose bytes fit ``last_cap_bytes``
+    (at least the last tensor).  ``len(sizes)`` when there is no tail cap."""
+    n = len(sizes_bytes)
+    if last_cap_bytes <= 0 or n < 2:
+        return n
+    start, total = n - 1, sizes_bytes[-1]
+    while start > 0 and total + sizes_bytes[start - 1] <= last_cap_bytes:
+        start -= 1
+        total += sizes_bytes[start]
+    return start
+
+
+def assign_buckets_with_tail(sizes_bytes: Sequence[int], caps_bytes: Sequence[int],
+                             last_cap_bytes: int = 0) -> List[List[int]]:
+    """``assign_buckets`` over the prefix, then the tail (``tail_split``) as the last bucket."""
+    cut = tail_split(sizes_bytes, last_cap_bytes)
+    if cut <= 0 or cut >= len(sizes_bytes):
+        return assign_buckets(sizes_bytes, caps_bytes)
+    head = assign_buckets(sizes_bytes[:cut], caps_bytes)
+    return head + [list(range(cut, len(sizes_bytes)))]
+
+
+def plan_for_arena(arena, bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0,
+                   last_bucket_mb: float = 0.0) -> BucketPlan:
     """Partition ``arena`` (already laid out in ready order) into contiguous buckets."""
     elem = arena.param_flat.element_size()
     sizes = [p.numel() * elem for p in arena.params]
     caps = [max(1, int(first_bucket_mb * MiB)), max(1, int(bucket_cap_mb * MiB))]
-    groups = assign_buckets(sizes, caps)
+    groups = assign_buckets_with_tail(sizes, caps, int(max(0.0, last_bucket_mb) * MiB))
     offsets, numels, param_bucket = [], [], [0] * len(arena.params)
     for b, members in enumerate(groups):
         start = arena.offsets[members[0]]

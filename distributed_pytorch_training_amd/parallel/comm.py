@@ -16,15 +16,20 @@ on, one of
 On CPU (gloo) there is no device collective; ``make_comm`` returns ``None`` and the reducer
 drives ``torch.distributed`` through a Python callback instead.
 
-RCCL channel count: ``rccl_channels`` > 0 exports ``NCCL_MIN_NCHANNELS`` /
-``NCCL_MAX_NCHANNELS`` before ``ncclCommInitRank`` (read once at communicator creation).  On
-an 8x MI355X node every GPU has 7 point-to-point xGMI links; a ring uses one outgoing link
-per channel, so a bucket only reaches the aggregate link bandwidth with >= 7 channels
-(SURVEY.md §5.8).  0 keeps RCCL's own topology-derived choice.
+RCCL channel count: ``rccl_channels`` > 0 creates the framework communicator with
+``ncclCommInitRankConfig`` and ``ncclConfig_t.minCTAs = maxCTAs = rccl_channels`` - a
+per-communicator setting, so it applies no matter what torch's own process-group
+communicator (created earlier, eagerly, by ``init_process_group(device_id=...)``) read from
+the process-wide ``NCCL_MIN/MAX_NCHANNELS`` environment.  The environment is not touched.
+On an 8x MI355X node every GPU has 7 point-to-point xGMI links and a ring uses one outgoing
+link per channel, so a bucket reaches the aggregate link bandwidth only with >= 7 channels
+(SURVEY.md §5.8).  0 keeps RCCL's topology-derived choice, which already opens more than 7
+channels on a fully connected xGMI node; the knob exists to bound the CUs RCCL's kernels
+take from the overlapped backward (docs/DESIGN.md §3.2).  tests/test_comm_gpu.py parses
+RCCL's init log to check the communicator got what was asked.
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -52,12 +57,6 @@ def _host_broadcast(t: torch.Tensor, root: int) -> None:
     dist.broadcast(t, root, group=_host_group())
 
 
-def apply_rccl_channels(n: int) -> None:
-    if n and n > 0:
-        os.environ.setdefault("NCCL_MIN_NCHANNELS", str(int(n)))
-        os.environ.setdefault("NCCL_MAX_NCHANNELS", str(int(n)))
-
-
 def make_comm(device: torch.device, rank: int, world_size: int, kind: str = "rccl",
               timeout_s: Optional[float] = None, rccl_channels: int = 0,
               exit_grace_s: float = 30.0):
@@ -74,7 +73,7 @@ def make_comm(device: torch.device, rank: int, world_size: int, kind: str = "rcc
         if world_size > 1:
             _host_group()   # collective group creation: every rank, same point
         return C.HostBridgeComm(_host_all_reduce, _host_broadcast, rank, world_size, dev)
-    apply_rccl_channels(rccl_channels)
+    n_ch = max(0, int(rccl_channels or 0))
     if world_size > 1:
         if not dist.is_initialized():
             raise RuntimeError("make_comm needs an initialised torch.distributed process group")
@@ -83,7 +82,7 @@ def make_comm(device: torch.device, rank: int, world_size: int, kind: str = "rcc
         uid = box[0]
     else:
         uid = C.RcclComm.new_unique_id()
-    comm = C.RcclComm(uid, rank, world_size, dev)
+    comm = C.RcclComm(uid, rank, world_size, dev, n_ch, n_ch)
     if timeout_s and timeout_s > 0 and world_size > 1:
         comm.enable_watchdog(float(timeout_s), 0.5, float(exit_grace_s))
     return comm

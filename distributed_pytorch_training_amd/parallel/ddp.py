@@ -40,10 +40,10 @@ from .flat import BufferArena, FlatArena
 class NativeDDP(nn.Module):
     def __init__(self, module: nn.Module, *, rank: int = 0, world_size: int = 1,
                  device: Optional[torch.device] = None, bucket_cap_mb: float = 25.0,
-                 first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
+                 first_bucket_mb: float = 1.0, last_bucket_mb: float = 0.0, broadcast_buffers: bool = True,
                  grad_dtype: str = "fp32", found_inf: Optional[torch.Tensor] = None,
                  scale: Optional[torch.Tensor] = None, check_inf: bool = False,
-                 profile: bool = False, rebuild_buckets: bool = True, comm=None,
+                 profile: bool = False, profile_slots: int = 1, rebuild_buckets: bool = True, comm=None,
                  weight_shadow: Optional[torch.dtype] = None, comm_kind: str = "rccl",
                  timeout_s: Optional[float] = None, rccl_channels: int = 0,
                  debug: bool = False) -> None:
@@ -52,10 +52,11 @@ class NativeDDP(nn.Module):
         self.rank, self.world_size = rank, world_size
         self.device = device or next(module.parameters()).device
         self.bucket_cap_mb, self.first_bucket_mb = bucket_cap_mb, first_bucket_mb
+        self.last_bucket_mb = last_bucket_mb
         self.broadcast_buffers = broadcast_buffers
         self.grad_dtype = grad_dtype
         self.profile = profile
-        self._profile_slots = 1
+        self._profile_slots = max(1, int(profile_slots))
         self.rebuild_buckets = rebuild_buckets and world_size > 1
         self.require_backward_grad_sync = True
         self._sync_buffers_next = True
@@ -112,7 +113,7 @@ class NativeDDP(nn.Module):
             raise RuntimeError(f"NativeDDP: parameter shapes differ across ranks: {gathered}")
 
     def _build_reducer(self) -> None:
-        self.plan = plan_for_arena(self.arena, self.bucket_cap_mb, self.first_bucket_mb)
+        self.plan = plan_for_arena(self.arena, self.bucket_cap_mb, self.first_bucket_mb, self.last_bucket_mb)
         if self.reducer is not None:
             self.reducer.remove_hooks()
             self.reducer = None
@@ -315,7 +316,8 @@ class NativeDDP(nn.Module):
         if self.reducer is None or self.comm is None:
             return None
         return {"bucket_ms": list(self.reducer.bucket_times_ms(slot)),
-                "step_ms": list(self.reducer.step_times_ms(slot))}
+                "step_ms": list(self.reducer.step_times_ms(slot)),
+                "bucket_start_ms": list(self.reducer.bucket_start_ms(slot))}
 
     def comm_profile_ref(self):
         """A deferred reader of the backward that just finished (valid for ``slots`` steps)."""

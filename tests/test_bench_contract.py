@@ -69,6 +69,62 @@ def test_bench_torchrun_gloo_two_ranks(tmp_path):
     _check(lines[0], 2)
 
 
+def test_bench_self_launches_ranks_without_torchrun(tmp_path):
+    """``python bench.py --gpus 2`` with no launcher environment spawns its own 2 ranks (the
+    driver's whole-node invocation): the record says 2 GPUs, and the communicator itself saw a
+    world of 2 on 2 rank processes."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *TINY],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    rec = lines[0]
+    _check(rec, 2)
+    assert rec["comm"]["world_size"] == 2 and rec["comm"]["pg_backend"] == "gloo"
+    assert len(rec["comm"]["rank_devices"]) == 2
+    assert rec["config"]["launcher"] == "self" and isinstance(rec["config"]["env"], dict)
+
+
+def test_bench_dead_rank_fails_the_job(tmp_path):
+    """A rank that dies makes the self-launched job exit non-zero (never a partial record)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--fail-rank", "1", *TINY],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode != 0
+    assert not _json_lines(r.stdout)
+    assert "rank 1 exited with status 17" in r.stderr
+
+
+def test_bench_launcher_world_size_mismatch_fails(tmp_path):
+    """Under a launcher, ``--gpus`` must equal WORLD_SIZE: a 2-rank launch of ``--gpus 4`` is an
+    error, not a silently smaller run."""
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT="29533")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", *TINY],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+    assert not _json_lines(r.stdout)
+
+
+@pytest.mark.gpu
+def test_bench_self_launch_two_ranks_on_one_gpu(tmp_path):
+    """The self-launch path on a real GPU: ``bench.py --gpus 2 --rehearse-shared-gpu`` without
+    torchrun runs 2 rank processes on cuda:0 (gloo control plane, host-bridge collective)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch-size", "32",
+           "--image-size", "64", "--steps", "2", "--warmup", "1", "--profile-steps", "2",
+           "--rehearse-shared-gpu"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = lines[0]
+    assert rec["n_gpus"] == 2 and rec["comm"]["world_size"] == 2 and rec["comm"]["kind"] == "host"
+    assert rec["config"]["launcher"] == "self"
+    assert [d["device"] for d in rec["comm"]["rank_devices"]] == ["cuda:0", "cuda:0"]
+
+
 @pytest.mark.gpu
 def test_bench_two_ranks_sharing_one_gpu(tmp_path):
     """bench.py's N > 1 path on a real GPU step (2 torchrun ranks on cuda:0, gloo control plane,

@@ -40,3 +40,41 @@ def test_plan_is_contiguous_partition():
     for i, b in enumerate(plan.param_bucket):
         s = arena.region(i)
         assert plan.offsets[b] <= s.start and s.stop <= plan.offsets[b] + plan.numels[b]
+
+
+@pytest.mark.parametrize("name,classes", [("resnet50", 1000), ("vit_b_16", 1000), ("resnet18", 10)])
+@pytest.mark.parametrize("cap", [0.5, 1.0, 4.0])
+def test_last_bucket_cap(name, classes, cap):
+    """--last-bucket-mb: the bucket that becomes ready last fits the cap (or is one tensor that
+    alone exceeds it), the buckets before it are the reference's plan of the prefix, and the
+    partition stays contiguous and complete."""
+    from distributed_pytorch_training_amd.parallel.bucketing import tail_split
+
+    model = build_model(name, classes)
+    arena = FlatArena(list(reversed(list(model.parameters()))))
+    plan = plan_for_arena(arena, 25.0, 1.0, last_bucket_mb=cap)
+    last = plan.members[-1]
+    last_bytes = sum(arena.params[i].numel() * 4 for i in last)
+    assert last_bytes <= cap * MiB or len(last) == 1, (last_bytes, len(last))
+    # maximal: the tensor just before the tail would not have fit
+    first = last[0]
+    if first > 0:
+        assert last_bytes + arena.params[first - 1].numel() * 4 > cap * MiB
+    assert plan.offsets[-1] + plan.numels[-1] == arena.numel
+    assert sorted(i for m in plan.members for i in m) == list(range(len(arena.params)))
+    sizes = [p.numel() * 4 for p in arena.params]
+    assert assign_buckets(sizes[:tail_split(sizes, int(cap * MiB))], [MiB, 25 * MiB]) == plan.members[:-1]
+    full = plan_for_arena(arena, 25.0, 1.0)
+    assert plan.sizes_mib()[-1] <= full.sizes_mib()[-1]
+
+
+def test_last_bucket_cap_resnet50_defaults():
+    """The ResNet-50 plan with the default 1 MiB tail: the stem/layer1 leftover (9.27 MiB with
+    torch DDP's plan) becomes a ~1 MiB tail bucket plus the rest of layer1 reduced earlier."""
+    model = build_model("resnet50", 1000)
+    arena = FlatArena(list(reversed(list(model.parameters()))))
+    ref = plan_for_arena(arena, 25.0, 1.0).sizes_mib()
+    got = plan_for_arena(arena, 25.0, 1.0, last_bucket_mb=1.0).sizes_mib()
+    assert ref[-1] == pytest.approx(9.27, abs=0.02)
+    assert got[-1] <= 1.0 and sum(got) == pytest.approx(sum(ref))
+    assert got[:len(ref) - 1] == ref[:-1]

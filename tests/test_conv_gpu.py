@@ -155,7 +155,7 @@ def test_resnet50_native_conv_matches_miopen(cuda):
 
     torch.manual_seed(0)
     base = build_model("resnet50", 100, cuda, image_size=64, channels_last=True)
-    common = ["--model", "resnet50", "--dataset", "synthetic", "--channels-last", "--num-classes", "100",
+    common = ["--model", "resnet50", "--dataset", "synthetic", "--channels-last", "--no-cuda-graph", "--num-classes", "100",
               "--lr", "0.05"]
     amp = ["--amp", "--amp-dtype", "bf16"]
     runs = {
@@ -490,7 +490,7 @@ def test_resnet50_fp16_native_step(cuda):
 
     torch.manual_seed(0)
     base = build_model("resnet50", 100, cuda, image_size=64, channels_last=True)
-    common = ["--model", "resnet50", "--dataset", "synthetic", "--channels-last", "--num-classes", "100",
+    common = ["--model", "resnet50", "--dataset", "synthetic", "--channels-last", "--no-cuda-graph", "--num-classes", "100",
               "--lr", "0.05"]
     amp = ["--amp", "--amp-dtype", "fp16"]
     runs = {

@@ -17,7 +17,7 @@ def _pair(cuda, model_name, extra, image=32, classes=10):
     base = build_model(model_name, classes, cuda, image_size=image)
     # engine parity (reducer, optimizer, scaler): both in the reference's NCHW layout, so the
     # comparison is not confounded by NHWC-vs-NCHW conv algorithm differences
-    a = parse_args(["--model", model_name, "--dataset", "synthetic", "--no-channels-last", *extra])
+    a = parse_args(["--model", model_name, "--dataset", "synthetic", "--no-channels-last", "--no-cuda-graph", *extra])
     b = parse_args(["--model", model_name, "--dataset", "synthetic", "--impl", "torch", *extra])
     return (Trainer(copy.deepcopy(base), a, 0, 1, cuda, log=lambda s: None),
             Trainer(copy.deepcopy(base), b, 0, 1, cuda, log=lambda s: None))
@@ -205,7 +205,7 @@ def test_cuda_graph_step_matches_eager(cuda):
 
     torch.manual_seed(0)
     base = build_model("resnet18", 10, cuda, image_size=32, channels_last=True)
-    ea = parse_args(["--dataset", "synthetic", "--amp", "--amp-dtype", "bf16", "--channels-last"])
+    ea = parse_args(["--dataset", "synthetic", "--amp", "--amp-dtype", "bf16", "--channels-last", "--no-cuda-graph"])
     ga = parse_args(["--dataset", "synthetic", "--amp", "--amp-dtype", "bf16", "--channels-last", "--cuda-graph"])
     eager = Trainer(copy.deepcopy(base), ea, 0, 1, cuda, log=lambda s: None)
     graph = Trainer(copy.deepcopy(base), ga, 0, 1, cuda, log=lambda s: None)
@@ -244,7 +244,7 @@ def test_weight_shadow_matches_autocast_casts(cuda, model_name, opt):
     base = build_model(model_name, 10, cuda, image_size=32, channels_last=cl)
     # the shadow path is what is under test: keep both runs on MIOpen convolutions (the MFMA
     # convs have their own end-to-end test in test_conv_gpu.py)
-    common = ["--model", model_name, "--dataset", "synthetic", "--amp", "--amp-dtype", "bf16", "--no-native-conv",
+    common = ["--model", model_name, "--dataset", "synthetic", "--no-cuda-graph", "--amp", "--amp-dtype", "bf16", "--no-native-conv",
               "--optimizer", opt, "--lr", "0.1" if opt == "sgd" else "1e-3"] + (["--channels-last"] if cl else [])
     sh = Trainer(copy.deepcopy(base), parse_args(common), 0, 1, cuda, log=lambda s: None)
     no = Trainer(copy.deepcopy(base), parse_args(common + ["--no-weight-shadow"]), 0, 1, cuda, log=lambda s: None)
@@ -289,7 +289,7 @@ def test_validation_lines_identical_across_engines_under_amp(cuda):
     torch.manual_seed(0)
     base = build_model("resnet50", 100, cuda, image_size=64, channels_last=True)
     loader = SyntheticLoader(256, 64, 64, 100, cuda, channels_last=True, seed=9)
-    common = ["--model", "resnet50", "--dataset", "synthetic", "--image-size", "64", "--num-classes", "100",
+    common = ["--model", "resnet50", "--dataset", "synthetic", "--no-cuda-graph", "--image-size", "64", "--num-classes", "100",
               "--channels-last"]
     lines = {}
     for name, extra in [("native_amp", ["--amp", "--amp-dtype", "bf16"]),

@@ -67,7 +67,7 @@ def _run_native(rank, ws, device, extra, amp, steps, inf_step):
     from distributed_pytorch_training_amd.engine.trainer import Trainer
     from distributed_pytorch_training_amd.models import build_model
 
-    argv = ["--model", "resnet18", "--dataset", "synthetic", "--image-size", "32", "--num-classes", "10",
+    argv = ["--model", "resnet18", "--dataset", "synthetic", "--no-cuda-graph", "--image-size", "32", "--num-classes", "10",
             "--batch-size", str(B), "--channels-last", "--lr", str(LR), "--comm", "host", "--ddp-debug", *extra]
     if amp:
         argv += ["--amp", "--amp-dtype", "bf16"]
@@ -157,6 +157,11 @@ def _worker(rank, ws, port, out_dir, extra, amp, steps, inf_step, mode):
         torch.cuda.set_device(dev)
         dist.init_process_group("gloo", rank=rank, world_size=ws)
         torch.backends.cudnn.deterministic = True     # MIOpen: deterministic algorithms
+        if mode == "emulate":
+            # the semantics check must not depend on which MIOpen solver immediate mode picks for
+            # each of the two runs (round 2 saw 5e-3 fp32 gradient drift from that alone): both
+            # the engine under test and the emulation run ATen's own conv/BN kernels
+            torch.backends.cudnn.enabled = False
         native = _run_native(rank, ws, dev, extra, amp, steps, inf_step)
         if mode == "emulate":
             ref = _emulate(ws, rank, dev, amp, steps, inf_step)
@@ -209,7 +214,7 @@ MIOPEN = ["--no-fused-bn", "--no-native-conv"]   # plain torch layers: the emula
 @pytest.mark.parametrize("amp", [False, True], ids=["fp32", "amp"])
 def test_world_size_2_matches_ddp_semantics(cuda, tmp_path, amp):
     """3 steps (AMP: rank 1's step-2 batch carries an inf) against the one-process emulation of
-    the reference's DDP; both run the same MIOpen kernels, so the match is near-exact."""
+    the reference's DDP; both run the same ATen kernels, so the match is near-exact."""
     res = _spawn(tmp_path, MIOPEN, amp=amp, inf_step=INF_STEP if amp else -1, mode="emulate")
     for r in range(2):
         nat, ref = res[r]["native"], res[r]["ref"]
@@ -220,9 +225,8 @@ def test_world_size_2_matches_ddp_semantics(cuda, tmp_path, amp):
                         {n: v for n, v in ref["buffers"].items() if v.numel() > 1})
         print(f"{'amp' if amp else 'fp32'} rank {r}: rel-L2 dparam {d_err:.2e} grad {g_err:.2e} "
               f"buffers {b_err:.2e} scale {nat['scale']}/{ref['scale']} tracker {nat['tracker']}/{ref['tracker']}")
-        # same kernels -> ~1e-6 alone; MIOpen may pick a different fp32 algorithm (e.g. Winograd)
-        # when the shared user find-db has been written by earlier tests, hence the bound
-        assert d_err < 1e-2 and g_err < 2e-2 and b_err < 1e-4, (d_err, g_err, b_err)
+        # identical kernels on both sides (MIOpen off): only the fused optimizer's rounding differs
+        assert d_err < 1e-4 and g_err < 1e-4 and b_err < 1e-4, (d_err, g_err, b_err)
         if amp:
             # the inf on rank 1 at step 2 skipped that step on both ranks: scale backed off once
             assert nat["scale"] == ref["scale"] == 32768.0, (nat["scale"], ref["scale"])

@@ -139,7 +139,7 @@ def test_vit_trainer_fused_step(cuda):
 
     torch.manual_seed(0)
     m = build_model("vit_b_16", 10, cuda, image_size=32)
-    args = parse_args(["--model", "vit_b_16", "--dataset", "synthetic", "--amp", "--amp-dtype", "bf16",
+    args = parse_args(["--model", "vit_b_16", "--dataset", "synthetic", "--no-cuda-graph", "--amp", "--amp-dtype", "bf16",
                        "--optimizer", "adamw", "--lr", "1e-3"])
     tr = Trainer(m, args, 0, 1, cuda, log=lambda s: None)
     before = tr.ddp.arena.param_flat.clone()
