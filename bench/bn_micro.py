@@ -1,8 +1,8 @@
 """Microbenchmark of the fused BN kernels at ResNet-50's block-tail shapes (batch 256).
 
 Reports achieved HBM-equivalent bandwidth per pass (bytes the kernel chain must move / time).
-Knobs are environment variables read by the extension at load (DPT_BN_*), so run one
-configuration per process:  DPT_BN_MAX_CHUNKS=2048 python bench/bn_micro.py
+The geometry constants it was used to pick (kBnMaxChunks etc., bn_kernels.hip) are compile-time
+constants now: edit and rebuild to re-sweep.  Per-layer roofline table: bench/bn_roofline.py.
 """
 import os
 import sys
@@ -31,7 +31,6 @@ def t_ms(fn, iters=20):
 def main():
     C_ = ops.native()
     dev = torch.device("cuda")
-    knobs = {k: v for k, v in os.environ.items() if k.startswith("DPT_BN")}
     tot_f = tot_b = 0.0
     for shape in SHAPES:
         n, c, h, w = shape
@@ -51,7 +50,7 @@ def main():
         tot_b += tb
         print(f"{shape}: fwd {tf:.3f} ms = {4 * bytes_pass / tf / 1e9:.2f} TB/s | "
               f"bwd {tb:.3f} ms = {8 * bytes_pass / tb / 1e9:.2f} TB/s", flush=True)
-    print(f"knobs {knobs}: total fwd {tot_f:.3f} ms, bwd {tot_b:.3f} ms", flush=True)
+    print(f"total fwd {tot_f:.3f} ms, bwd {tot_b:.3f} ms", flush=True)
 
 
 if __name__ == "__main__":

@@ -21,13 +21,17 @@ def main(argv=None):
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--variants", type=int, nargs="+", default=[0, 9, 10, 11])
     ap.add_argument("--stats", action="store_true", help="with the BN-statistics epilogue")
+    ap.add_argument("--dgrad", action="store_true",
+                    help="time the stride-1 backward-data instead (the forward kernel on dy with the "
+                         "flipped weight, as the training step runs it)")
     a = ap.parse_args(argv)
     from distributed_pytorch_training_amd import ops
 
     C_ = ops.native()
     dev = torch.device("cuda")
     cl = torch.channels_last
-    print(f"# forward conv variants, ResNet-50, batch {a.batch}, bf16 NHWC, stats={a.stats}\n")
+    print(f"# {'backward-data' if a.dgrad else 'forward'} conv variants, ResNet-50, batch {a.batch}, bf16 NHWC, "
+          f"stats={a.stats}\n")
     print("| conv | x | " + " | ".join(f"v{v} ms (TF/s)" for v in a.variants) + " | best | max diff |")
     print("|---|---|" + "---|" * len(a.variants) + "---|---|")
     tot = {v: 0.0 for v in a.variants}
@@ -36,6 +40,12 @@ def main(argv=None):
         cin, h, w = cin_hw
         if cin % 64 or cout % 64:
             continue
+        if a.dgrad:
+            if s[0] != 1:
+                continue
+            # dx = conv(dy, flip(w)^T, pad' = R-1-pad): a forward conv cout -> cin on the output grid
+            ho = (h + 2 * p[0] - k[0]) // s[0] + 1
+            cin, cout, h, w, p = cout, cin, ho, ho, (k[0] - 1 - p[0], k[1] - 1 - p[1])
         x = torch.randn(a.batch, cin, h, w, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
         wt = (torch.randn(cout, cin, *k, device=dev, dtype=torch.bfloat16) * 0.05).contiguous(memory_format=cl)
         cells, times, ref, diff = [], {}, None, 0.0

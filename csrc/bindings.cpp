@@ -511,7 +511,7 @@ std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad, PendingRed
 // dw = conv2d backward-weight (fp32 or bf16 output, KRSC = channels_last [Cout, C, R, S]).
 // pending != nullptr: a split-K reduce is left for a backward-data launch (conv_wgrad_deferred).
 Tensor conv_wgrad_impl(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stride, int64_t pad, bool fp32_out,
-                       PendingReduce* pending, const dpt::BnBwdFinArgs* fin = nullptr) {
+                       PendingReduce* pending) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(x, "x");
   same_16(dy, x, "conv_wgrad");
@@ -534,7 +534,7 @@ Tensor conv_wgrad_impl(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t
   c10::hip::HIPGuard guard(x.device().index());
   dpt::launch_conv_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
                          part.data_ptr<float>(), dw.data_ptr(), fp32_out ? 0 : (is_f16(x) ? 2 : 1), N, H, W, C, Cout, R,
-                         S, (int)stride, (int)pad, pl, cur_stream(x), is_f16(x), pending ? &pending->r : nullptr, fin);
+                         S, (int)stride, (int)pad, pl, cur_stream(x), is_f16(x), pending ? &pending->r : nullptr);
   if (pending) {
     pending->part = part;
     pending->dw = dw;
@@ -554,47 +554,6 @@ py::tuple conv_wgrad_deferred(Tensor dy, Tensor x, std::vector<int64_t> wshape, 
   Tensor dw = conv_wgrad_impl(dy, x, wshape, stride, pad, false, p.get());
   if (p->r.consumed) return py::make_tuple(dw, py::none());
   return py::make_tuple(dw, p);
-}
-
-// conv_wgrad_deferred that also carries the backward finalize of the BatchNorm whose output
-// was this conv's input (partials p1/p2 [C, chunks] from the conv's backward-data epilogue;
-// x is that BN's output for BN+ReLU and the BN rows M = x rows).  Returns (dw, pending,
-// kbuf [3C] = [k1 | k2 | k3], dgamma, dbeta) for bn_bwd_apply_pre.
-py::tuple conv_wgrad_bnfin(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stride, int64_t pad, Tensor p1,
-                           Tensor p2, c10::optional<Tensor> weight, Tensor invstd, int64_t bn_rows) {
-  const int64_t C = p1.size(0);
-  TORCH_CHECK(p1.is_cuda() && p1.scalar_type() == at::kFloat && p1.dim() == 2 && p1.is_contiguous() &&
-                  p2.sizes() == p1.sizes() && p2.is_contiguous(),
-              "conv_wgrad_bnfin: partials must be contiguous fp32 [C, chunks]");
-  auto fopt = p1.options();
-  auto kbuf = at::empty({3 * C}, fopt);
-  auto dg = at::empty({C}, fopt);
-  auto db = at::empty({C}, fopt);
-  dpt::BnBwdFinArgs fin{p1.data_ptr<float>(), p2.data_ptr<float>(), (int)p1.size(1), (int)C, bn_rows,
-                        f32_param(weight, C, "weight"), f32_param(invstd, C, "invstd"), dg.data_ptr<float>(),
-                        db.data_ptr<float>(), kbuf.data_ptr<float>()};
-  auto p = std::make_shared<PendingReduce>();
-  Tensor dw = conv_wgrad_impl(dy, x, wshape, stride, pad, false, p.get(), &fin);
-  if (p->r.consumed) return py::make_tuple(dw, py::none(), kbuf, dg, db);
-  return py::make_tuple(dw, p, kbuf, dg, db);
-}
-
-// BatchNorm(+ReLU) backward apply from precomputed coefficients (conv_wgrad_bnfin): dx =
-// k1*dz + k2*(x - mean) + k3, dz = dy * mask(fma(x, a, b) > 0) from coef = [a | b], or dz = dy
-// (from_dz: the block-tail gradient already masked).  wgrad_reduce: carried in the grid's tail.
-Tensor bn_bwd_apply_pre(Tensor dy, Tensor x, Tensor mean, c10::optional<Tensor> coef, Tensor kbuf, bool from_dz,
-                        PendingReducePtr wgrad_reduce) {
-  auto [M, C] = bn_rows(x, "x");
-  auto [Md, Cd] = bn_rows(dy, "grad_output");
-  TORCH_CHECK(M == Md && C == Cd && dy.scalar_type() == x.scalar_type(), "grad_output mismatch");
-  TORCH_CHECK(from_dz || (coef.has_value() && coef->defined()), "bn_bwd_apply_pre: coef needed unless from_dz");
-  auto dx = at::empty_like(x);
-  c10::hip::HIPGuard guard(x.device().index());
-  MaybeAttach att(wgrad_reduce, cur_stream(x));
-  dpt::launch_bn_bwd_apply_pre(bn_dtype(x), dy.data_ptr(), x.data_ptr(), M, C, f32_param(mean, C, "mean"),
-                               f32_param(coef, 2 * C, "coef"), f32_param(kbuf, 3 * C, "kbuf"), dx.data_ptr(),
-                               cur_stream(x), from_dz);
-  return dx;
 }
 
 void conv_reduce_flush(PendingReducePtr p) {
@@ -1181,7 +1140,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_set_big", &dpt::conv_set_big, py::arg("on"));
   m.def("conv_set_halo", &dpt::conv_set_halo, py::arg("on"));
   m.def("conv_set_wgrad_halo", &dpt::conv_set_wgrad_halo, py::arg("mode"));
-  m.def("conv_set_wgrad_wide", &dpt::conv_set_wgrad_wide, py::arg("on"));
   m.def("conv_fwd_splits", [](int64_t M, int Cout, int64_t K, bool graph) {
           return dpt::conv_fwd_splits_for(M, Cout, K, graph);
         }, py::arg("M"), py::arg("Cout"), py::arg("K"), py::arg("graph") = false);
@@ -1208,11 +1166,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad_deferred", &conv_wgrad_deferred, py::arg("grad_output"), py::arg("x"), py::arg("weight_shape"),
         py::arg("stride"), py::arg("pad"));
   m.def("conv_reduce_flush", &conv_reduce_flush, py::arg("pending"));
-  m.def("conv_wgrad_bnfin", &conv_wgrad_bnfin, py::arg("grad_output"), py::arg("x"), py::arg("weight_shape"),
-        py::arg("stride"), py::arg("pad"), py::arg("p1"), py::arg("p2"), py::arg("weight"), py::arg("invstd"),
-        py::arg("bn_rows"));
-  m.def("bn_bwd_apply_pre", &bn_bwd_apply_pre, py::arg("grad_output"), py::arg("x"), py::arg("mean"), py::arg("coef"),
-        py::arg("kbuf"), py::arg("from_dz"), py::arg("wgrad_reduce") = nullptr);
   m.def("rccl_version", []() { return std::string(dpt::rccl_version_string()); });
 
   // Collective seam (comm.h): RcclComm (production) and HostBridgeComm (ranks sharing a GPU)

@@ -400,19 +400,6 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(BnBwdFin f) {
   bn_bwd_finalize_block<NT>(f, (int)blockIdx.x, red);
 }
 
-// Threads per block of the standalone WIDE finalizes (one block per channel, thousands of
-// partials each): a latency chain of chunks / (NT * 8) dependent load rounds (DPT_BN_FIN_THREADS,
-// 256 / 512 / 1024).
-static int g_fin_threads = -1;
-static int fin_threads() {
-  if (g_fin_threads < 0) {
-    const char* e = std::getenv("DPT_BN_FIN_THREADS");
-    const int v = e ? std::atoi(e) : 256;
-    g_fin_threads = (v == 512 || v == 1024) ? v : 256;
-  }
-  return g_fin_threads;
-}
-
 // Two BatchNorms' finalizes in one launch (a block tail with its downsample BN folded in)
 __global__ __launch_bounds__(kBlock) void bn_bwd_finalize2_kernel(BnBwdFin f, BnBwdFin h) {
   __shared__ double red[2 * (kBlock / 64)];
@@ -431,17 +418,10 @@ BnBwdFin make_bn_bwd_fin(const float* p1, const float* p2, int chunks, int C, in
   return f;
 }
 
+// Wide finalizes (one block per channel, thousands of partials) run 256-thread blocks too: 512
+// and 1024 measured 0.3-0.5 % slower in the step (docs/DESIGN.md §9).
 static void launch_bn_bwd_fin(const BnBwdFin& f, hipStream_t s) {
-  const int nt = f.wide ? fin_threads() : kBlock;
-  if (nt == 1024) hipLaunchKernelGGL(bn_bwd_finalize_kernel<1024>, dim3((unsigned)f.blocks), dim3(1024), 0, s, f);
-  else if (nt == 512) hipLaunchKernelGGL(bn_bwd_finalize_kernel<512>, dim3((unsigned)f.blocks), dim3(512), 0, s, f);
-  else hipLaunchKernelGGL(bn_bwd_finalize_kernel<kBlock>, dim3((unsigned)f.blocks), dim3(kBlock), 0, s, f);
-}
-
-void launch_bn_bwd_finalize(const BnBwdFinArgs& a, hipStream_t s) {
-  launch_bn_bwd_fin(make_bn_bwd_fin(a.p1, a.p2, a.chunks, a.C, a.M, a.gamma, a.invstd, a.dgamma, a.dbeta, a.kbuf,
-                                    a.kbuf + a.C, a.kbuf + 2 * a.C, -1),
-                    s);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<kBlock>, dim3((unsigned)f.blocks), dim3(kBlock), 0, s, f);
 }
 
 // dx = k1*dz + k2*(x - mean) + k3, dz = dy*(y>0) recomputed (RELU; mask from x if MX) or
@@ -542,20 +522,16 @@ bool bn_supported(int64_t C) {
   return C >= 8 && C % 8 == 0 && C <= 8 * kBlock && kBlock % (C / 8) == 0;
 }
 
-// Tuning knobs (read once; defaults from bench/bn_micro.py on MI355X, ResNet-50 tail shapes):
-// DPT_BN_MAX_CHUNKS (stats blocks, default 512), DPT_BN_BWD_UNROLL (rows in flight in the
-// backward stats pass: 2 or 4, default 2), DPT_BN_APPLY_MAX (forward-apply grid cap, default
-// 32768: one 2-row iteration per thread), DPT_BN_BWD_APPLY_MAX (backward-apply grid cap,
-// default 8192).
-static int env_int(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
-static const int kBnMaxChunks = env_int("DPT_BN_MAX_CHUNKS", 512);
-static const int kBnBwdUnroll = env_int("DPT_BN_BWD_UNROLL", 2);
-static const int kBnApplyMax = env_int("DPT_BN_APPLY_MAX", 32768);
-static const int kBnBwdApplyMax = env_int("DPT_BN_BWD_APPLY_MAX", 4 * kMaxBlocks);
-static const int kBnReverse = env_int("DPT_BN_REVERSE", 1);  // apply passes walk rows last-to-first
+// Geometry constants, measured on MI355X at the ResNet-50 shapes (bench/bn_micro.py,
+// profiles/bn_kernel_knob_sweep.txt): statistics blocks per channel group, rows in flight in
+// the backward statistics pass, forward / backward apply grid caps (one 2-row iteration per
+// thread forward), and apply passes walking rows last-to-first (the rows the producing kernel
+// wrote last are still in the caches).
+constexpr int kBnMaxChunks = 512;
+constexpr int kBnBwdUnroll = 2;
+constexpr int kBnApplyMax = 32768;
+constexpr int kBnBwdApplyMax = 4 * kMaxBlocks;
+constexpr int kBnReverse = 1;
 
 BnGeometry bn_geometry(int64_t M, int64_t C) {
   BnGeometry g;
@@ -624,10 +600,7 @@ void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void
 #define DPT_FWD_FIN(NT)                                                                                        \
   hipLaunchKernelGGL(bn_fwd_finalize_wide_kernel<NT>, dim3((unsigned)C), dim3(NT), 0, s, psum, psq, chunks, (int)C, \
                      M, gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd, ca, cb)
-    const int nt = fin_threads();
-    if (nt == 1024) DPT_FWD_FIN(1024);
-    else if (nt == 512) DPT_FWD_FIN(512);
-    else DPT_FWD_FIN(kBlock);
+    DPT_FWD_FIN(kBlock);
 #undef DPT_FWD_FIN
   } else
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), dim3(kBlock), 0, s, psum, psq, chunks,
@@ -679,11 +652,7 @@ static void bwd_dispatch(bool relu, const void* dy, const void* dy2, const void*
                          float* p2, const float* gamma, const float* invstd, float* dgamma, float* dbeta,
                          float* k1, float* k2, float* k3, void* dx, void* dz, hipStream_t s) {
   dim3 bl(kBlock);
-  if (kBnBwdUnroll == 4) {
-    bwd_stats_dispatch<IO, 4>(relu, dy, dy2, y, x, mean, coef, M, C, g, p1, p2, dz, s);
-  } else {
-    bwd_stats_dispatch<IO, 2>(relu, dy, dy2, y, x, mean, coef, M, C, g, p1, p2, dz, s);
-  }
+  bwd_stats_dispatch<IO, kBnBwdUnroll>(relu, dy, dy2, y, x, mean, coef, M, C, g, p1, p2, dz, s);
   launch_bn_bwd_fin(make_bn_bwd_fin(p1, p2, g.chunks, C, M, gamma, invstd, dgamma, dbeta, k1, k2, k3, 0), s);
   dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
   if (dz != nullptr) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, true, false>), ga, bl, 0, s, dz, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse, ReduceCarry{});

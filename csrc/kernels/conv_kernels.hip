@@ -134,6 +134,11 @@ struct ConvFwdArgs {
 };
 
 
+template <int N>
+__device__ __forceinline__ void vmcnt_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // K-major operands (rows of the LDS image = k) use the transposing reads and the swizzle of
 // mfma.h: wg_frag is its natural-k-order tr_frag.
 template <int RB>
@@ -447,6 +452,37 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
         }
       }
     }
+  } else if constexpr (STAGES >= 3) {
+    // Deep pipeline (cdna_hip_programming.md §5 "Pipelining across barriers"): STAGES-1 K-tiles
+    // stay in flight across ONE raw s_barrier per K-step.  Iteration i waits (counted vmcnt)
+    // until this wave's loads of tile i have landed, the barrier makes every wave's tile-i
+    // loads visible AND proves every wave finished reading tile i-1, whose buffer then receives
+    // tile i+STAGES-1 while tile i is multiplied.  No vmcnt(0) / __syncthreads inside the loop
+    // (its fence would drain the in-flight tiles); all LDS lives in the one `lds` array.
+    constexpr int PER = A_PER_T + B_PER_T;  // glds per wave per K-tile
+    static_assert(STAGES <= 4, "pipeline depth");
+    const int nk = ks1 - ks0;
+#pragma unroll
+    for (int t = 0; t < STAGES - 1; ++t)
+      if (t < nk) stage(ks0 + t, t);
+    int buf = 0;
+    for (int i = 0; i < nk; ++i) {
+      const int ahead = min(STAGES - 2, nk - 1 - i);  // later tiles already issued
+      if (ahead >= 2) vmcnt_wait<2 * PER>();
+      else if (ahead == 1) vmcnt_wait<PER>();
+      else vmcnt_wait<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (i + STAGES - 1 < nk) {
+        const int nb = buf == 0 ? STAGES - 1 : buf - 1;  // buffer of tile i-1 == (i+STAGES-1) % STAGES
+        stage(ks0 + i + STAGES - 1, nb);
+      }
+      mma(buf);
+      buf = buf + 1 == STAGES ? 0 : buf + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // the epilogue reuses the LDS
   } else if (STAGES == 2) {
     stage(ks0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -895,11 +931,6 @@ __global__ __launch_bounds__(256) void conv_split_epilogue_kernel(ConvFwdArgs p)
 // ds_read_b128 quarter-wave touches (4 per 256-B bank row) land on distinct banks.
 // Epilogue: pairs of accumulators are rounded with v_cvt_pk_bf16_f32 and written to a padded
 // LDS image, then stored as 16-byte rows; BN statistics (STATS) from the rounded values.
-template <int N>
-__device__ __forceinline__ void vmcnt_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 template <int BN, int NS, bool STATS>
 __global__ __launch_bounds__(conv::kThreads, 2) void conv_fwd_pipe_kernel(ConvFwdArgs p) {
   using namespace conv;
@@ -1122,8 +1153,6 @@ struct ConvWgradArgs {
   int dw_step, wwrap, dh_step, hwrap;
   int dp_w, dp_wwrap, dp_h, dp_hwrap;
   int f16;             // fp16 operands (bf16 otherwise)
-  // carried BatchNorm backward finalize (carry.h): the grid's last fin.blocks blocks
-  BnBwdFin fin;
   // conv_wgrad_halo_kernel: padded pixel count N*H*(W+2) and divisors by W+2 and H
   int Mp = 0;
   FastDiv div_wp{}, div_h{};
@@ -1147,15 +1176,6 @@ __global__ __launch_bounds__(NT, (NT == conv::kThreads && BNW <= 128) ? DPT_WGRA
   constexpr int MI = WTM / 32, NI = WTN / 32;
   static_assert(MI >= 1 && NI >= 1 && A_INSTR >= 1 && B_INSTR >= 1, "conv_wgrad_kernel: bad tiling");
   __shared__ __attribute__((aligned(16))) unsigned char lds[STAGES * STAGE];
-  if constexpr (NT == conv::kThreads) {
-    if (p.fin.blocks) {  // carried BatchNorm backward finalize blocks (ConvWgradArgs::fin)
-      const int nw = (int)gridDim.x - p.fin.blocks;
-      if ((int)blockIdx.x >= nw) {
-        bn_bwd_finalize_block(p.fin, (int)blockIdx.x - nw, lds);
-        return;
-      }
-    }
-  }
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WNW, wn = wid % WNW;
@@ -1366,13 +1386,6 @@ __global__ __launch_bounds__(conv::kThreads, BNW == 64 ? 4 : 2) void conv_wgrad_
   constexpr int B_GI = B_BYTES / 1024;                              // 17 or 9 per block
   constexpr int B_PW = (B_GI + NW - 1) / NW;
   __shared__ __attribute__((aligned(16))) unsigned char lds[STAGES * STAGE];
-  if (p.fin.blocks) {  // carried BatchNorm backward finalize blocks (ConvWgradArgs::fin)
-    const int nw = (int)gridDim.x - p.fin.blocks;
-    if ((int)blockIdx.x >= nw) {
-      bn_bwd_finalize_block(p.fin, (int)blockIdx.x - nw, lds);
-      return;
-    }
-  }
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles = p.co_tiles * p.n_tiles;
@@ -1787,15 +1800,9 @@ int conv_split_cols(int64_t M) { return (int)((M + 15) / 16); }
 // epilogue), 1 = 2-stage + LDS epilogue, 2 = 2-stage +
 // register epilogue, 3 = 1-stage + register epilogue, 4 = 1-stage + LDS epilogue.
 // The backward-weight kernel takes 1-2 -> 2 stages, 0/3-4 -> 1 stage.
-// DPT_CONV_VARIANT overrides; conv_set_variant switches at run time (A/B tests, benchmarks).
-static int g_conv_variant = -1;
-static int conv_variant() {
-  if (g_conv_variant < 0) {
-    const char* e = std::getenv("DPT_CONV_VARIANT");
-    g_conv_variant = e ? std::atoi(e) : 0;
-  }
-  return g_conv_variant;
-}
+// conv_set_variant switches at run time (A/B tests, benchmarks; the bindings' conv_set_variant).
+static int g_conv_variant = 0;
+static int conv_variant() { return g_conv_variant; }
 void conv_set_variant(int v) { g_conv_variant = v; }
 
 // Production choice of the 8-wave 256-row tiles (variant 0): deep reductions onto narrow
@@ -1805,13 +1812,9 @@ void conv_set_variant(int v) { g_conv_variant = v; }
 //   N = 512, K >= 2048, M <= 16384          -> 10 (256 x 128): 3x3 512->512 @7x7 714 -> 802 TF
 // Off by default: in the ResNet-50 training step (stats / BNB / BNR epilogues, L2 shared with
 // the neighbouring kernels) the per-shape wins did not show (11680/11521 vs 11659/11534 img/s,
-// same-box A/B).  DPT_CONV_BIG=1 / conv_set_big(1) turns it on.
-static int g_conv_big = -1;
+// same-box A/B).  conv_set_big(1) turns it on.
+static int g_conv_big = 0;
 static int conv_big_auto(int64_t M, int N, int64_t K) {
-  if (g_conv_big < 0) {
-    const char* e = std::getenv("DPT_CONV_BIG");
-    g_conv_big = e ? std::atoi(e) : 0;
-  }
   if (!g_conv_big) return 0;
   if (N == 256 && K >= 1024 && M >= 32768) return 9;
   if (N == 512 && K >= 2048 && M <= 16384) return 10;
@@ -1876,25 +1879,18 @@ int take_attached_reduce(ReduceCarry& rc) {
 static int take_attached_reduce(ConvFwdArgs& a) { return take_attached_reduce(a.red); }
 
 // 3x3 / stride 1 / pad 1 convs (and their backward-data) take the HALO K loop (conv_fwd_kernel).
-// DPT_CONV_HALO: 0 = per-tap loop (A/B), 1 = auto (default): all three B taps per load phase
-// (HB = 3) when the tile grid is at most two blocks per CU - there the grid, not LDS, limits the
-// resident blocks and one wait per three K-steps wins (3x3 512->512 @7x7: 0.075 -> 0.064 ms) -
-// else one B tap per phase (HB = 1; HB = 3 everywhere lost 1.2 % in the step), 2 / 3 = force HB
-static int g_conv_halo = -1;
+// conv_set_halo: 0 = per-tap loop (A/B), 1 = auto (default): all three B taps per load phase
+// (HB = 3) when the tile grid is at most 512 tiles (two blocks per CU) - there the grid, not LDS,
+// limits the resident blocks and one wait per three K-steps wins (3x3 512->512 @7x7: 0.075 ->
+// 0.064 ms; a 1024-tile cut-off measured slower) - else one B tap per phase (HB = 1; HB = 3
+// everywhere lost 1.2 % in the step), 2 / 3 = force HB
+static int g_conv_halo = 1;
 static int halo_hb(const ConvFwdArgs& a, int bn) {
   if (g_conv_halo == 2) return 1;
   if (g_conv_halo == 3) return 3;
-  static const int hb3_tiles = [] {  // DPT_CONV_HALO_HB3_TILES: the grid-size cut-off (A/B knob)
-    const char* e = std::getenv("DPT_CONV_HALO_HB3_TILES");
-    return e ? std::atoi(e) : 512;
-  }();
-  return (int64_t)a.m_tiles * (a.Cout / bn) <= hb3_tiles ? 3 : 1;
+  return (int64_t)a.m_tiles * (a.Cout / bn) <= 512 ? 3 : 1;
 }
 static bool halo_ok(const ConvFwdArgs& a) {
-  if (g_conv_halo < 0) {
-    const char* e = std::getenv("DPT_CONV_HALO");
-    g_conv_halo = e ? std::atoi(e) : 1;
-  }
   return g_conv_halo && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 64 == 0 && a.Ho == a.H &&
          a.Wo == a.W;
 }
@@ -1944,17 +1940,11 @@ static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdAr
 // A conv whose 128 x BN tile grid is far below one block per CU (ResNet-18 on 32x32 images:
 // layer4 is 4 tiles at batch 128, each a 72-step K loop) is latency-bound on the K loop: split
 // the K-steps over blocks (fp32 partials, summed by conv_split_epilogue_kernel).  Target ~2
-// blocks per CU, at least 2 K-steps per split.  DPT_CONV_SPLITK=0 disables it (A/B).
+// blocks per CU, at least 2 K-steps per split.  conv_set_splitk(0) disables it (A/B).
 // 0 = never split, 1 = auto (the policy below), 2 = the in-graph policy everywhere (tests that
-// compare eager with replayed steps)
-static int g_splitk = -1;
-static int splitk_mode() {
-  if (g_splitk < 0) {
-    const char* e = std::getenv("DPT_CONV_SPLITK");
-    g_splitk = e == nullptr ? 1 : std::atoi(e);
-  }
-  return g_splitk;
-}
+// compare eager with replayed steps); conv_set_splitk
+static int g_splitk = 1;
+static int splitk_mode() { return g_splitk; }
 void conv_set_splitk(int mode) { g_splitk = mode; }
 
 int conv_fwd_splits(int64_t M, int Cout, int64_t K, int* kps_out, hipStream_t s) {
@@ -1964,18 +1954,12 @@ int conv_fwd_splits(int64_t M, int Cout, int64_t K, int* kps_out, hipStream_t s)
   return conv_fwd_splits_for(M, Cout, K, capturing, kps_out);
 }
 
-// Thresholds of the policy below (DPT_CONV_SPLIT_TILES / _EAGER_TILES / _TARGET override them
-// for A/B runs): split grids of fewer than kSplitTiles tiles (eagerly: at most kSplitEager
-// tiles with >= 24 K-steps) to about kSplitTarget blocks.
-static int split_knob(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
+// Thresholds of the policy below: split grids of fewer than kSplitTiles tiles (eagerly: at most
+// kSplitEager tiles with >= 24 K-steps) to about kSplitTarget blocks (512 / 1024 targets
+// measured -1 % / -5 %, docs/DESIGN.md §7.2).
+constexpr int kSplitTiles = 160, kSplitEager = 32, kSplitTarget = 512;
 
 int conv_fwd_splits_for(int64_t M, int Cout, int64_t K, bool graph, int* kps_out) {
-  static const int kSplitTiles = split_knob("DPT_CONV_SPLIT_TILES", 160);
-  static const int kSplitEager = split_knob("DPT_CONV_SPLIT_EAGER_TILES", 32);
-  static const int kSplitTarget = split_knob("DPT_CONV_SPLIT_TARGET", 512);
   const int n_tiles = Cout % 128 == 0 ? Cout / 128 : Cout / 64;
   const int64_t tiles = (int64_t)conv_m_tiles(M) * n_tiles;
   const int nk = (int)(K / conv::BK);
@@ -2107,17 +2091,26 @@ static void conv_fwd_dispatch(int variant, bool bkn, ConvFwdArgs a, hipStream_t 
   }
 }
 
-// 8-wave (512-thread), 2-stage variants: 9 = 256x256 tile, 10 = 256x128, 11 = 128x256.
-// Returns false when the shape does not fit the variant's N tile.
+// 8-wave (512-thread) variants: 9 = 256x256 tile, 10 = 256x128, 11 = 128x256 (2 stages);
+// 12 = 256x128, 13 = 128x256 with the 3-stage pipelined K loop (two K-tiles in flight across
+// one raw barrier per step).  Returns false when the shape does not fit the variant's N tile.
+static int big_bn(int v) { return (v == 10 || v == 12) ? 128 : 256; }
+static int big_bm(int v) { return (v == 11 || v == 13) ? 128 : 256; }
 static bool conv_fwd_big(int v, ConvFwdArgs& a, hipStream_t s) {
-  const int bn = v == 10 ? 128 : 256, bm = v == 11 ? 128 : 256;
+  const int bn = big_bn(v), bm = big_bm(v);
   if (a.Cout % bn) return false;
   a.n_tiles = a.Cout / bn;
   a.mt256 = (int)((a.M + 255) / 256);
   const int mt = bm == 256 ? a.mt256 : a.m_tiles;
   const dim3 grid((unsigned)(mt * a.n_tiles)), block(512);
   const bool st = a.psum != nullptr;
-  if (v == 9) {
+  if (v == 12) {
+    if (st) fwd_launch<256, 128, 3, true, false, true, false, false, false, false, false, 512>(grid, block, s, a);
+    else fwd_launch<256, 128, 3, true, false, false, false, false, false, false, false, 512>(grid, block, s, a);
+  } else if (v == 13) {
+    if (st) fwd_launch<128, 256, 3, true, false, true, false, false, false, false, false, 512>(grid, block, s, a);
+    else fwd_launch<128, 256, 3, true, false, false, false, false, false, false, false, 512>(grid, block, s, a);
+  } else if (v == 9) {
     if (st) fwd_launch<256, 256, 2, true, false, true, false, false, false, false, false, 512>(grid, block, s, a);
     else fwd_launch<256, 256, 2, true, false, false, false, false, false, false, false, 512>(grid, block, s, a);
   } else if (v == 10) {
@@ -2150,7 +2143,7 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
   const int v = conv_variant();
   if (!bkn && maybe_split(a, ws, psum != nullptr, false, false, false, s)) return;
   if (!bkn && !a.f16) {
-    const int vb = (v >= 9 && v <= 11) ? v : v == 0 ? conv_big_auto(a.M, Cout, (int64_t)R * S * C) : 0;
+    const int vb = (v >= 9 && v <= 13) ? v : v == 0 ? conv_big_auto(a.M, Cout, (int64_t)R * S * C) : 0;
     if (vb && conv_fwd_big(vb, a, s)) return;
   }
   if (wide) conv_fwd_dispatch<128>(v, bkn, a, s);
@@ -2188,24 +2181,35 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
     a.bp_ld = keep_ld;
   }
   const bool two = res && bnx2 != nullptr;
-  if (!f16 && conv_variant() == 0) {
-    // 8-wave 256-row tiles (conv_big_auto): N = C, K = Cout*R*S
-    const int vb = conv_big_auto(a.M, C, (int64_t)Cout * R * S);
-    if (vb) {
-      const int bn = vb == 10 ? 128 : 256;
+  const int cv = conv_variant();
+  if (!f16 && (cv == 0 || (cv >= 9 && cv <= 13))) {
+    // 8-wave tiles (conv_big_auto, or a forced variant): N = C, K = Cout*R*S
+    const int vb = cv ? cv : conv_big_auto(a.M, C, (int64_t)Cout * R * S);
+    if (vb && C % big_bn(vb) == 0) {
+      const int bn = big_bn(vb), bm = big_bm(vb);
       a.n_tiles = C / bn;
       a.mt256 = (int)((a.M + 255) / 256);
-      const dim3 g((unsigned)(a.mt256 * a.n_tiles));
-      if (vb == 9) {
+      const dim3 g((unsigned)((bm == 256 ? a.mt256 : a.m_tiles) * a.n_tiles));
+      if (vb == 12) {
+        if (two) fwd_launch<256, 128, 3, true, false, false, true, true, false, false, true, 512>(g, block, s, a);
+        else if (res) fwd_launch<256, 128, 3, true, false, false, true, true, false, false, false, 512>(g, block, s, a);
+        else fwd_launch<256, 128, 3, true, false, false, true, false, false, false, false, 512>(g, block, s, a);
+      } else if (vb == 13) {
+        if (two) fwd_launch<128, 256, 3, true, false, false, true, true, false, false, true, 512>(g, block, s, a);
+        else if (res) fwd_launch<128, 256, 3, true, false, false, true, true, false, false, false, 512>(g, block, s, a);
+        else fwd_launch<128, 256, 3, true, false, false, true, false, false, false, false, 512>(g, block, s, a);
+      } else if (vb == 9) {
         if (two) fwd_launch<256, 256, 2, true, false, false, true, true, false, false, true, 512>(g, block, s, a);
         else if (res) fwd_launch<256, 256, 2, true, false, false, true, true, false, false, false, 512>(g, block, s, a);
         else fwd_launch<256, 256, 2, true, false, false, true, false, false, false, false, 512>(g, block, s, a);
-      } else {
+      } else if (vb == 10) {
         if (two) fwd_launch<256, 128, 2, true, false, false, true, true, false, false, true, 512>(g, block, s, a);
         else if (res) fwd_launch<256, 128, 2, true, false, false, true, true, false, false, false, 512>(g, block, s, a);
         else fwd_launch<256, 128, 2, true, false, false, true, false, false, false, false, 512>(g, block, s, a);
+      } else {
+        a.n_tiles = 0;  // unsupported forced variant for this pass: fall through to the default
       }
-      return;
+      if (a.n_tiles) return;
     }
   }
   a.n_tiles = C % 128 == 0 ? C / 128 : C / 64;
@@ -2349,31 +2353,17 @@ void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, i
 }
 
 // conv_wgrad_halo_kernel modes: 0 off, 1 / 2: 128-channel strips, 3 / 4: 64-channel strips
-// (even: double-buffered), 5 auto (default, DPT_WGRAD_HALO): mode 3 for 64-channel inputs,
+// (even: double-buffered), 5 auto (default; conv_set_wgrad_halo for A/B): mode 3 for 64-channel inputs,
 // where the per-tap kernel's two-tap tiles waste 1/9 of their MFMA work on a ragged last tile
 // (64x56x56 -> 64: 0.118 -> 0.085-0.095 ms); the per-tap kernel elsewhere (the halo's W+2
 // padding costs 7-29 % more MFMA work and measured level or slower at 128-512 channels,
 // profiles/wgrad_halo_r2.md)
-static int g_wgrad_halo = -1;
+static int g_wgrad_halo = 5;
 static int wgrad_halo_mode(int C = 0) {
-  if (g_wgrad_halo < 0) {
-    const char* e = std::getenv("DPT_WGRAD_HALO");
-    g_wgrad_halo = e ? std::atoi(e) : 5;
-  }
   if (g_wgrad_halo == 5) return C == 64 ? 3 : 0;
   return g_wgrad_halo;
 }
 void conv_set_wgrad_halo(int on) { g_wgrad_halo = on; }
-
-static int g_wgrad_wide = -1;
-static int wgrad_wide_mode() {
-  if (g_wgrad_wide < 0) {
-    const char* e = std::getenv("DPT_WGRAD_WIDE");
-    g_wgrad_wide = e ? std::atoi(e) : 0;
-  }
-  return g_wgrad_wide;
-}
-void conv_set_wgrad_wide(int on) { g_wgrad_wide = on; }
 
 static FastDiv make_fastdiv(uint32_t d) {
   FastDiv f;
@@ -2404,11 +2394,7 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
     pl.bnw = pl.halo >= 3 ? 64 : 128;
     const int tiles = (Cout / 64) * 3 * (C / pl.bnw);
     const int steps = (int)(((int64_t)N * H * (W + 2) + 63) / 64);
-    static const int env_target = [] {
-      const char* e = std::getenv("DPT_WGRAD_HALO_TARGET");
-      return e ? std::atoi(e) : 0;
-    }();
-    const int target = env_target > 0 ? env_target : pl.bnw == 128 ? 512 : 768;
+    const int target = pl.bnw == 128 ? 512 : 768;
     int splits = (target + tiles - 1) / tiles;
     const int min_steps = (int64_t)tiles * (steps / 32) >= 512 ? 32 : 2;
     splits = std::max(1, std::min(splits, steps / min_steps));
@@ -2425,14 +2411,6 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
   pl.bnw = C % 128 == 0 ? 128 : (C == 64 && R * S > 1) ? 128 : (C == 16 && R * S * C >= 256 && pl.bmw == 64) ? 256 : 64;
   // variant 12 (A/B): 8-wave 256 x 256 tiles where both channel counts allow them
   if (conv_variant() == 12 && Cout % 256 == 0 && C % 256 == 0) pl.bmw = pl.bnw = 256;
-  // 1x1 with a 64-channel side (DPT_WGRAD_WIDE, A/B knob): one tile spans all 256 channels of
-  // the other side, so neither operand is streamed twice (64->256: x read once instead of per
-  // 128-channel output tile; 256->64: dy likewise)
-  const int wide = wgrad_wide_mode();
-  if (wide && R == 1 && S == 1 && conv_variant() == 0) {
-    if (C == 64 && Cout == 256) { pl.bmw = 256; pl.bnw = 64; }
-    else if (Cout == 64 && C == 256) { pl.bmw = 64; pl.bnw = 256; }
-  }
   const int tiles = (Cout / pl.bmw) * ((R * S * C + pl.bnw - 1) / pl.bnw);
   const int steps = (int)((M + 63) / 64);
   // ~768 blocks (3 per CU) and at least 32 K-steps per split: a split's fp32 partial tile
@@ -2450,7 +2428,7 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
 
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void* dw, int dw_kind, int N, int H,
                        int W, int C, int Cout, int R, int S, int stride, int pad, const ConvWgradPlan& pl,
-                       hipStream_t st, bool f16, WgradReduce* defer, const BnBwdFinArgs* fin) {
+                       hipStream_t st, bool f16, WgradReduce* defer) {
   ConvWgradArgs a;
   a.f16 = f16 ? 1 : 0;
   const bool direct_out = pl.splits == 1 && dw_kind == 0;  // fp32 result written in place
@@ -2492,16 +2470,6 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
   }
   dim3 grid((unsigned)(a.co_tiles * a.n_tiles * a.splits)), block(conv::kThreads);
   const int v = a.f16 ? 0 : conv_variant();
-  if (fin != nullptr) {
-    a.fin = make_bn_bwd_fin(fin->p1, fin->p2, fin->chunks, fin->C, fin->M, fin->gamma, fin->invstd, fin->dgamma,
-                            fin->dbeta, fin->kbuf, fin->kbuf + fin->C, fin->kbuf + 2 * fin->C, -1);
-    if (pl.bmw == 256 && pl.bnw == 256) {  // the 512-thread variant carries nothing: finalize on its own
-      launch_bn_bwd_finalize(*fin, st);
-      a.fin = BnBwdFin{};
-    } else {
-      grid.x += (unsigned)a.fin.blocks;
-    }
-  }
   if (pl.halo) {
 #define DPT_WH(BNW, ST)                                                                      \
   do {                                                                                       \

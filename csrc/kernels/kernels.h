@@ -169,7 +169,6 @@ struct ConvWgradPlan {
   int64_t part_floats;
   int halo = 0;  // 3x3 / stride-1: the three taps of a tap row share one x strip (conv_wgrad_halo_kernel)
 };
-void conv_set_wgrad_wide(int on);   // 1x1 64<->256-channel wgrad in one 256-wide tile (DPT_WGRAD_WIDE)
 void conv_set_wgrad_halo(int mode);  // 0 off, 1-4 forced, 5 auto (default, DPT_WGRAD_HALO)
 ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad, int Ho = 0,
                               int Wo = 0);
@@ -182,29 +181,12 @@ struct WgradReduce {
   bool consumed;
 };
 void launch_wgrad_reduce(const WgradReduce& r, hipStream_t s);
-// A BatchNorm backward finalize (carry.h BnBwdFin): [C][chunks] partials p1 = sum dz,
-// p2 = sum dz*(x - mean) -> dgamma, dbeta (optional) and kbuf = [k1 | k2 | k3] (3C floats).
-struct BnBwdFinArgs {
-  const float* p1;
-  const float* p2;
-  int chunks, C;
-  int64_t M;
-  const float* gamma;  // nullptr: 1
-  const float* invstd;
-  float* dgamma;
-  float* dbeta;
-  float* kbuf;
-};
 // defer != nullptr: the reduce is not launched but described in *defer (consumed = false) when
 // the plan needs one, for a conv backward-data launch to run in its tail (AttachWgradReduce).
-// fin != nullptr: the backward-weight grid also carries that BatchNorm finalize (its blocks
-// run in the backward-weight's tail; standalone for the 8-wave variant).
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void* dw, int dw_kind, int N, int H,
                        int W, int C, int Cout, int R, int S, int stride, int pad, const ConvWgradPlan& plan,
-                       hipStream_t s, bool f16 = false, WgradReduce* defer = nullptr,
-                       const BnBwdFinArgs* fin = nullptr);
-void launch_bn_bwd_finalize(const BnBwdFinArgs& f, hipStream_t s);
-// BatchNorm backward apply with precomputed kbuf (launch_bn_bwd_finalize / a carried one):
+                       hipStream_t s, bool f16 = false, WgradReduce* defer = nullptr);
+// BatchNorm backward apply with precomputed kbuf (a finalize run before it):
 // dx = k1*dz + k2*(x - mean) + k3, dz = dy * relu-mask(fma(x, coef_a, coef_b) > 0), or dz = dy
 // when from_dz.  Takes an attached backward-weight reduce into its grid (AttachWgradReduce).
 void launch_bn_bwd_apply_pre(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* mean,

@@ -24,14 +24,6 @@ typedef float pf32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 pbf16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 pf16x2 __attribute__((ext_vector_type(2)));
 
-// DPT_POOL_BLOCK2=0: the per-output 3x3/s2 forward kernel (A/B of the 2x2-block one)
-static bool pool_block2() {
-  static const bool on = [] {
-    const char* e = std::getenv("DPT_POOL_BLOCK2");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return on;
-}
 
 namespace dpt {
 
@@ -515,7 +507,7 @@ void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t
   if (total == 0) return;
   const dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
   const int64_t total2 = B * ((Ho + 1) / 2) * ((Wo + 1) / 2) * (C / 8);
-  if (K == 3 && S == 2 && P == 1 && total2 + kBlock < (int64_t(1) << 32) && pool_block2()) {
+  if (K == 3 && S == 2 && P == 1 && total2 + kBlock < (int64_t(1) << 32)) {  // 2x2-block kernel
     const dim3 grid2((unsigned)((total2 + kBlock - 1) / kBlock)), block(kBlock);
     const uint32_t t2 = (uint32_t)total2;
     if (coef != nullptr) {
@@ -560,17 +552,11 @@ void launch_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int64_t
 // finalize reads them all - ResNet-50's stem at batch 256 had 25,088 blocks (DPT_POOL_BN_BLOCKS;
 // in-step rocprofv3: uncapped 268 us, 4096 blocks 241, 2048 237, 1024 234, and the stem's BN
 // finalize drops from ~21 us to a few, profiles/pool_bn_blocks_r2.txt).
-static int pool_bn_blocks() {
-  static const int v = [] {
-    const char* e = std::getenv("DPT_POOL_BN_BLOCKS");
-    return e ? std::max(1, std::atoi(e)) : 1024;
-  }();
-  return v;
-}
+constexpr int kPoolBnBlocks = 1024;
 
 int maxpool_bwd_bn_chunks(int64_t B, int H, int W, int C) {
   const int64_t total2 = B * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
-  return (int)std::min<int64_t>((total2 + kBlock - 1) / kBlock, pool_bn_blocks());
+  return (int)std::min<int64_t>((total2 + kBlock - 1) / kBlock, kPoolBnBlocks);
 }
 
 void launch_maxpool_bwd(int dtype, const void* dy, const void* dy2, const uint8_t* idx, void* dx, int64_t B, int H,
@@ -675,14 +661,11 @@ __global__ __launch_bounds__(kBlock) void gap_bwd_bnr_kernel(const void* __restr
 
 int gap_bwd_bnr_chunks(int64_t M, int64_t C) {
   const int rpp = kBlock / (int)(C / 8);
-  // ~one block per CU (DPT_GAP_BNR_BLOCKS): each block ends with C scattered stores per partial
-  // array into the [C][blocks] layout the finalize reads, which at C = 2048 costs more than the
-  // extra rows per block - ResNet-50's tail, 7x7x2048 x 256 images: 1024 blocks 62 us, 256
-  // blocks 42 us, 128 blocks 62 us
-  static const int target = [] {
-    const char* e = std::getenv("DPT_GAP_BNR_BLOCKS");
-    return e ? std::max(1, std::atoi(e)) : 256;
-  }();
+  // ~one block per CU: each block ends with C scattered stores per partial array into the
+  // [C][blocks] layout the finalize reads, which at C = 2048 costs more than the extra rows per
+  // block - ResNet-50's tail, 7x7x2048 x 256 images: 1024 blocks 62 us, 256 blocks 42 us, 128
+  // blocks 62 us (profiles/gap_bwd_bnr_blocks_r2.txt)
+  constexpr int target = 256;
   int64_t rpb = (M + target - 1) / target;
   rpb = (rpb + rpp - 1) / rpp * rpp;
   return (int)((M + rpb - 1) / rpb);

@@ -80,14 +80,12 @@ def _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches,
     if mask_from_x:
         # a native conv consuming y sums this BN's backward statistics in its dgrad epilogue
         y._dpt_bn_src = (x, mean, coef)
-        y._dpt_bn_fin = (weight, invstd)  # ... and may run this BN's whole backward (ops/conv.py)
     own_slot, res_slot = links
     ctx.res_slot = res_slot  # our residual input is the identity alias of an earlier block tail
     if own_slot is not None:
         # block tail: the conv consuming y sums the statistics (and folds in the identity-path
         # gradient the next block's tail leaves in own_slot, see _bwd) in its dgrad epilogue
         y._dpt_bn_src = (x, mean, own_slot)
-        y._dpt_bn_fin = (weight, invstd)
     return y
 
 
@@ -101,9 +99,6 @@ def _bwd(ctx, dy, dy2):
     want_dz = ctx.has_res and ctx.needs_input_grad[1]
     if coef is not None and dy2 is None:
         part = take_bnb_partials(dy)
-        if part is not None and part[4] is not None:  # the consuming conv ran this whole backward
-            dx, dg, db = part[4]
-            return (dx, None, dg if want_params else None, db if want_params else None)
         if part is not None:  # statistics already summed by the consuming conv's dgrad epilogue
             dx, dg, db = native().bn_bwd_partials(dy, x, weight, mean, invstd, coef, part[0], part[1],
                                                   bool(want_params))
@@ -118,11 +113,8 @@ def _bwd(ctx, dy, dy2):
             if part[2] != dy2.data_ptr():
                 raise RuntimeError("fused block-tail backward: the identity-path gradient folded into the "
                                    "conv's dgrad is not the one autograd delivered (alias used twice?)")
-            if part[4] is not None:  # the consuming conv ran this whole backward (ops/conv.py)
-                dx, dg, db = part[4]
-            else:
-                dx, dg, db = native().bn_bwd_partials(dy, x, weight, mean, invstd, None, part[0], part[1],
-                                                      bool(want_params), True)
+            dx, dg, db = native().bn_bwd_partials(dy, x, weight, mean, invstd, None, part[0], part[1],
+                                                  bool(want_params), True)
             if ctx.res_slot is not None:
                 ctx.res_slot["dres"] = dy
             return (dx, dy if want_dz else None, dg if want_params else None, db if want_params else None)

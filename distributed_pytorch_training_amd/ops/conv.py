@@ -43,14 +43,6 @@ S2_DGRAD = os.environ.get("DPT_S2_DGRAD", "1") != "0"
 # Backward-weight before backward-data, its split-K reduce run by extra blocks in the
 # backward-data launch's tail (conv_wgrad_deferred / wgrad_reduce=): no reduce launch of its own
 WGRAD_REDUCE_FUSE = os.environ.get("DPT_WGRAD_REDUCE_FUSE", "1") != "0"
-# A conv whose input is a fused BN(+ReLU) output, or a block tail's, also runs that BN's backward:
-# backward-data (BN statistics in its epilogue) -> backward-weight carrying the BN finalize ->
-# BN apply carrying the backward-weight reduce (csrc/kernels/carry.h), one launch less per BN
-# than conv backward + BN backward; the BN's own backward then returns the precomputed result.
-# Opt-in (DPT_BN_FIN_CARRY=1): bit-identical, but the BN apply then reads the backward-data
-# output after the backward-weight has streamed its operands through the caches, and the
-# ResNet-50 step lost 0.4 % (same-box A/B 12060/12085 vs 12126/12118 img/s)
-BN_FIN_CARRY = os.environ.get("DPT_BN_FIN_CARRY", "0") == "1"
 # The im2col stem path is correct but measured slower than MIOpen on ResNet-50's 7x7/2 stem at
 # batch 256 (the [3.2M x 192] bf16 patch matrix is 1.2 GB written and read twice): opt-in only.
 STEM_ENABLED = os.environ.get("DPT_NATIVE_STEM", "0") == "1"
@@ -82,53 +74,10 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous(memory_format=_CL) else t.contiguous(memory_format=_CL)
 
 
-def _backward_with_bn(ctx, dy, x, w):
-    """This conv's backward (both gradients) plus the backward of the fused BN whose
-    output was x: three launches, the two small kernels carried (see BN_FIN_CARRY).  Returns
-    (dx, dw) or None when the case is not covered (the caller runs the unfused order)."""
-    src, fin = ctx.bn_src, ctx.bn_fin
-    s, p = ctx.stride, ctx.pad
-    if not isinstance(src[2], dict) and s == 2:  # BN+ReLU into a strided conv: parity classes
-        bn_x, bn_mean, bn_coef = src
-        dx, p1, p2 = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3], bn_x, bn_mean, bn_coef)
-        dres_ptr, from_dz = None, False
-    elif not isinstance(src[2], dict):  # BN+ReLU: (x, mean, coef)
-        bn_x, bn_mean, bn_coef = src
-        wt = _flipped(w)
-        dx, p1, p2, _ = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, bn_coef, w_flipped=wt)
-        dres_ptr, from_dz = None, False
-    elif len(src) == 3 and s == 1:  # block tail without a downsample BN: (x, mean, slot)
-        bn_x, bn_mean, bn_coef = src[0], src[1], None
-        dres = src[2].get("dres")
-        if not _dres_ok(dres, x):
-            return None
-        src[2].pop("dres")
-        wt = _flipped(w)
-        dx, p1, p2, _ = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, None, x, dres, wt)
-        dres_ptr, from_dz = dres.data_ptr(), True
-    else:
-        return None
-    rows = bn_x.numel() // bn_x.shape[1]
-    dw, red, kbuf, dg, db = native().conv_wgrad_bnfin(dy, x, list(w.shape), s, p, p1, p2, fin[0], fin[1], rows)
-    dx_bn = native().bn_bwd_apply_pre(dx, bn_x, bn_mean, bn_coef, kbuf, from_dz, wgrad_reduce=red)
-    if red is not None and not red.done:
-        native().conv_reduce_flush(red)
-    _put_bnb(dx, p1, p2, dres_ptr, None, pre=(dx_bn, dg, db))
-    return dx, dw
-
-
 def _backward(ctx, dy):
     x, w = ctx.saved_tensors
     dy = _cl(dy.to(x.dtype))
     s, p = ctx.stride, ctx.pad
-    if (BN_FIN_CARRY and BN_BWD_FUSE and ctx.bn_src is not None and ctx.bn_fin is not None
-            and ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and x.dim() == 4
-            and (s == 1 or (s == 2 and S2_DGRAD and not isinstance(ctx.bn_src[2], dict) and w.shape[2] > 1))):
-        done = _backward_with_bn(ctx, dy, x, w)
-        if done is not None:
-            if ctx.res_slot is not None:
-                ctx.res_slot["dres"] = done[0]
-            return done
     dx = dw = red = None
     if ctx.needs_input_grad[1]:
         if ctx.needs_input_grad[0] and WGRAD_REDUCE_FUSE:
@@ -192,8 +141,8 @@ def reset_side_channels() -> None:
     _BNB_PARTIALS.clear()
 
 
-def _put_bnb(dx, p1, p2, dres_ptr, p3, pre=None) -> None:
-    _BNB_PARTIALS[dx.data_ptr()] = (_GEN[0], dx._version, p1, p2, tuple(dx.shape), dres_ptr, p3, pre)
+def _put_bnb(dx, p1, p2, dres_ptr, p3) -> None:
+    _BNB_PARTIALS[dx.data_ptr()] = (_GEN[0], dx._version, p1, p2, tuple(dx.shape), dres_ptr, p3)
 
 
 def begin_step() -> None:
@@ -232,30 +181,30 @@ def _dres_ok(dres, x) -> bool:
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride: int, pad: int, out_hw, bn_src, res_slot, bn_fin):
+    def forward(ctx, x, w, stride: int, pad: int, out_hw, bn_src, res_slot):
         y = native().conv_fwd(x, w, stride, pad, False, *out_hw)[0]
         ctx.save_for_backward(x, w)
-        ctx.stride, ctx.pad, ctx.bn_src, ctx.res_slot, ctx.bn_fin = stride, pad, bn_src, res_slot, bn_fin
+        ctx.stride, ctx.pad, ctx.bn_src, ctx.res_slot = stride, pad, bn_src, res_slot
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        return _backward(ctx, dy) + (None,) * 6
+        return _backward(ctx, dy) + (None,) * 5
 
 
 class _ConvStats(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride: int, pad: int, out_hw, bn_src, res_slot, bn_fin):
+    def forward(ctx, x, w, stride: int, pad: int, out_hw, bn_src, res_slot):
         y, ps, pq = native().conv_fwd(x, w, stride, pad, True, *out_hw)
         ctx.save_for_backward(x, w)
-        ctx.stride, ctx.pad, ctx.bn_src, ctx.res_slot, ctx.bn_fin = stride, pad, bn_src, res_slot, bn_fin
+        ctx.stride, ctx.pad, ctx.bn_src, ctx.res_slot = stride, pad, bn_src, res_slot
         ctx.mark_non_differentiable(ps, pq)
         ctx.set_materialize_grads(False)  # no zero-filled gradients for the statistics outputs
         return y, ps, pq
 
     @staticmethod
     def backward(ctx, dy, _dps, _dpq):
-        return _backward(ctx, dy) + (None,) * 6
+        return _backward(ctx, dy) + (None,) * 5
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bool = False,
@@ -270,11 +219,9 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bo
     bn_src = x.__dict__.get("_dpt_bn_src")
     # x is the identity alias of a fused block tail (this conv is a downsample)
     res_slot = x.__dict__.get("_dpt_res_slot")
-    # (weight, invstd) of that BN: lets this conv's backward run the BN's backward too
-    bn_fin = x.__dict__.get("_dpt_bn_fin")
     if not bn_stats:
-        return _Conv.apply(x, w, int(stride), int(pad), tuple(out_hw), bn_src, res_slot, bn_fin)
-    y, ps, pq = _ConvStats.apply(x, w, int(stride), int(pad), tuple(out_hw), bn_src, res_slot, bn_fin)
+        return _Conv.apply(x, w, int(stride), int(pad), tuple(out_hw), bn_src, res_slot)
+    y, ps, pq = _ConvStats.apply(x, w, int(stride), int(pad), tuple(out_hw), bn_src, res_slot)
     y._dpt_bn_partials = (ps, pq)
     return y
 
@@ -292,20 +239,19 @@ def register_bnb_partials(dx: torch.Tensor, p1: torch.Tensor, p2: torch.Tensor, 
 
 
 def take_bnb_partials(dy: torch.Tensor):
-    """(p1, p2, dres_ptr, p3, pre) the backward of the conv that consumed a BN output summed for
+    """(p1, p2, dres_ptr, p3) the backward of the conv that consumed a BN output summed for
     ``dy``, once; dres_ptr is None for BN+ReLU, else the data pointer of the identity-path
     gradient that was folded into ``dy`` (block tails); p3: the folded downsample BN's statistic
-    (tails with a downsample branch), else None; pre: (dx, dgamma, dbeta) when that conv's
-    backward already ran this BN's whole backward (BN_FIN_CARRY), else None."""
+    (tails with a downsample branch), else None."""
     if not _BNB_PARTIALS:
         return None
     ent = _BNB_PARTIALS.pop(dy.data_ptr(), None)
     if ent is None:
         return None
-    gen, ver, p1, p2, shape, dres_ptr, p3, pre = ent
+    gen, ver, p1, p2, shape, dres_ptr, p3 = ent
     if gen != _GEN[0] or ver != dy._version or shape != tuple(dy.shape):
         return None
-    return p1, p2, dres_ptr, p3, pre
+    return p1, p2, dres_ptr, p3
 
 
 def take_bn_partials(x: torch.Tensor):

@@ -62,7 +62,11 @@ class BucketPlan:
 
 def tail_split(sizes_bytes: Sequence[int], last_cap_bytes: int) -> int:
     """Index where the tail bucket starts: the longest suffix whose bytes fit ``last_cap_bytes``
-    (at least the last tensor).  ``len(sizes)`` when there is no tail cap."""
+    (at least the last tensor).  ``len(sizes)`` (no split) when there is no tail cap, or when
+    that suffix holds less than half the cap: then the tensors just before it are big ones
+    whose gradients arrive at the very end too (ViT-B/16: the 2.25 MiB patch embedding ahead
+    of the 3 KiB class token), splitting would only add a collective (measured:
+    profiles/comm_model_r3.md)."""
     n = len(sizes_bytes)
     if last_cap_bytes <= 0 or n < 2:
         return n
@@ -70,6 +74,8 @@ def tail_split(sizes_bytes: Sequence[int], last_cap_bytes: int) -> int:
     while start > 0 and total + sizes_bytes[start - 1] <= last_cap_bytes:
         start -= 1
         total += sizes_bytes[start]
+    if total > last_cap_bytes or 2 * total < last_cap_bytes:
+        return n
     return start
 
 

@@ -4,7 +4,7 @@ import torch
 import torch.distributed as dist
 
 from distributed_pytorch_training_amd.models import build_model
-from distributed_pytorch_training_amd.parallel.bucketing import MiB, assign_buckets, plan_for_arena
+from distributed_pytorch_training_amd.parallel.bucketing import MiB, assign_buckets, plan_for_arena, tail_split
 from distributed_pytorch_training_amd.parallel.flat import FlatArena
 
 
@@ -48,24 +48,34 @@ def test_last_bucket_cap(name, classes, cap):
     """--last-bucket-mb: the bucket that becomes ready last fits the cap (or is one tensor that
     alone exceeds it), the buckets before it are the reference's plan of the prefix, and the
     partition stays contiguous and complete."""
-    from distributed_pytorch_training_amd.parallel.bucketing import tail_split
-
     model = build_model(name, classes)
     arena = FlatArena(list(reversed(list(model.parameters()))))
     plan = plan_for_arena(arena, 25.0, 1.0, last_bucket_mb=cap)
+    full = plan_for_arena(arena, 25.0, 1.0)
+    sizes = [p.numel() * 4 for p in arena.params]
+    if tail_split(sizes, int(cap * MiB)) == len(sizes):
+        # no split: the fitting suffix was under half the cap (or the plain tail already fits)
+        assert plan.members == full.members
+        return
     last = plan.members[-1]
     last_bytes = sum(arena.params[i].numel() * 4 for i in last)
-    assert last_bytes <= cap * MiB or len(last) == 1, (last_bytes, len(last))
+    assert cap * MiB / 2 <= last_bytes <= cap * MiB, (last_bytes, len(last))
     # maximal: the tensor just before the tail would not have fit
     first = last[0]
     if first > 0:
         assert last_bytes + arena.params[first - 1].numel() * 4 > cap * MiB
     assert plan.offsets[-1] + plan.numels[-1] == arena.numel
     assert sorted(i for m in plan.members for i in m) == list(range(len(arena.params)))
-    sizes = [p.numel() * 4 for p in arena.params]
     assert assign_buckets(sizes[:tail_split(sizes, int(cap * MiB))], [MiB, 25 * MiB]) == plan.members[:-1]
-    full = plan_for_arena(arena, 25.0, 1.0)
     assert plan.sizes_mib()[-1] <= full.sizes_mib()[-1]
+
+
+def test_last_bucket_cap_skips_a_useless_split():
+    """ViT-B/16: the suffix that fits a 1 MiB tail is the 3 KiB class token alone (the 2.25 MiB
+    patch embedding before it is ready at the same moment): no split, the plan is torch's."""
+    model = build_model("vit_b_16", 1000)
+    arena = FlatArena(list(reversed(list(model.parameters()))))
+    assert plan_for_arena(arena, 25.0, 1.0, 1.0).members == plan_for_arena(arena, 25.0, 1.0).members
 
 
 def test_last_bucket_cap_resnet50_defaults():

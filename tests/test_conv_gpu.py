@@ -752,66 +752,6 @@ def test_wgrad_reduce_piggybacked_on_dgrad(cuda, case):
     assert red2.done and torch.equal(dw2.view(torch.int16), dw_ref.view(torch.int16))
 
 
-@pytest.mark.parametrize("ds", [False, True], ids=["identity", "downsample"])
-def test_bn_backward_run_by_consuming_conv_is_bitwise(cuda, monkeypatch, ds):
-    """BN_FIN_CARRY (ops/conv.py): the conv consuming a fused BN(+ReLU) / block-tail output runs
-    that BN's backward itself (backward-data -> backward-weight carrying the BN finalize -> BN
-    apply carrying the backward-weight reduce).  Same kernels, same math as conv backward + BN
-    backward: every gradient must be bit-identical with the path off, and the BN backward must
-    have found the precomputed result (no side-channel entry left)."""
-    from distributed_pytorch_training_amd.ops import bn as fbn
-    from distributed_pytorch_training_amd.ops import conv as nc
-
-    g = torch.Generator(device=cuda).manual_seed(11)
-    N, C4, C, HW = 4, 256, 64, 14
-
-    def t(*s, scale=1.0):
-        return torch.randn(*s, device=cuda, generator=g) * scale
-
-    x0 = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
-    r0 = t(N, C4, HW, HW).to(torch.bfloat16).contiguous(memory_format=CL)
-    ws = [t(*sh, scale=sc).to(torch.bfloat16).contiguous(memory_format=CL) for sh, sc in
-          (((C4, C4, 1, 1), 0.06), ((C, C4, 1, 1), 0.06), ((C, C, 3, 3), 0.04), ((C4, C, 1, 1), 0.12),
-           ((C4, C4, 1, 1), 0.06))]
-    bn = [(torch.rand(c, device=cuda, generator=g) + 0.5, t(c, scale=0.1)) for c in (C4, C, C, C4, C4)]
-    ho = HW // 2 if ds else HW
-    gy = t(N, C4, ho, ho).to(torch.bfloat16).contiguous(memory_format=CL)
-    gy2 = t(N, C4, ho, ho).to(torch.bfloat16).contiguous(memory_format=CL)
-    calls = []
-    real = nc._backward_with_bn
-    monkeypatch.setattr(nc, "_backward_with_bn", lambda *a: calls.append(1) or real(*a))
-    grads = []
-    for carry in (True, False):
-        monkeypatch.setattr(nc, "BN_FIN_CARRY", carry)
-        nc.reset_side_channels()
-        xi, ri = (v.detach().clone().requires_grad_(True) for v in (x0, r0))
-        ps = [v.detach().clone().requires_grad_(True) for v in ws]
-        bp = [(a.clone().requires_grad_(True), b.clone().requires_grad_(True)) for a, b in bn]
-
-        def bnt(h, i, res=None, relu=True, pair=False):
-            c = h.shape[1]
-            rm, rv = torch.zeros(c, device=cuda), torch.ones(c, device=cuda)
-            nb = torch.zeros((), dtype=torch.long, device=cuda)
-            return fbn.bn_act_train(h, res, bp[i][0], bp[i][1], rm, rv, nb, 0.1, 1e-5, relu, pair)
-
-        yc, yi = bnt(nc.conv2d(xi, ps[0], 1, 0, bn_stats=True), 0, res=ri, pair=True)
-        u = bnt(nc.conv2d(yc, ps[1], 1, 0, bn_stats=True), 1)          # tail -> conv1 (BNR)
-        ident = yi
-        if ds:
-            ident = bnt(nc.conv2d(yi, ps[4], 2, 0, bn_stats=True), 4, relu=False)
-        u = bnt(nc.conv2d(u, ps[2], 2 if ds else 1, 1, bn_stats=True), 2)  # BN+ReLU -> conv2
-        oc, oi = bnt(nc.conv2d(u, ps[3], 1, 0, bn_stats=True), 3, res=ident, pair=True)  # -> conv3
-        torch.autograd.backward([oc, oi], [gy, gy2])
-        torch.cuda.synchronize()
-        grads.append([xi.grad, ri.grad] + [p.grad for p in ps if p.grad is not None]
-                     + [v.grad for ab in bp for v in ab if v.grad is not None])
-        assert not nc._BNB_PARTIALS
-    # conv3 (BN+ReLU input), conv2 (BN+ReLU input, stride 1 or 2), conv1 (tail input)
-    assert len(calls) == 3
-    for a, b in zip(*grads):
-        assert torch.equal(a, b), (a.float() - b.float()).abs().max()
-
-
 @pytest.mark.parametrize("C,hw", [(2048, 7), (512, 4)])
 def test_last_tail_statistics_from_avgpool_backward(cuda, monkeypatch, C, hw):
     """The network's last block tail feeds the global average pool: its backward forms the
@@ -940,26 +880,3 @@ def test_wgrad_halo_matches_reference(cuda, shape, mode, dtype):
     torch.testing.assert_close(dw, ref, rtol=1e-3, atol=1e-4 * scale + 1e-3)
     torch.testing.assert_close(dw, base, rtol=1e-4, atol=1e-5 * scale + 1e-4)
     torch.testing.assert_close(dw16.float(), ref, rtol=1e-2, atol=1e-2 * scale)
-
-
-@pytest.mark.parametrize("shape", [(2, 64, 14, 14, 256), (3, 256, 9, 7, 64), (1, 64, 5, 5, 256)])
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_wgrad_wide_1x1_tiles(cuda, shape, dtype):
-    """1x1 backward-weight with one 256-wide tile over the 256-channel side (conv_set_wgrad_wide:
-    256x64 / 64x256 tiles) vs an fp32 reference and the default 128-wide tiles."""
-    N, C, H, W, Cout = shape
-    C_ = ops.native()
-    g = torch.Generator(device=cuda).manual_seed(9)
-    x = torch.randn(N, C, H, W, device=cuda, generator=g).to(dtype).contiguous(memory_format=CL)
-    gy = torch.randn(N, Cout, H, W, device=cuda, generator=g).to(dtype).contiguous(memory_format=CL)
-    ref = torch.nn.grad.conv2d_weight(x.float(), (Cout, C, 1, 1), gy.float())
-    scale = ref.abs().max().item()
-    try:
-        C_.conv_set_wgrad_wide(0)
-        base = C_.conv_wgrad(gy, x, [Cout, C, 1, 1], 1, 0, True)
-        C_.conv_set_wgrad_wide(1)
-        dw = C_.conv_wgrad(gy, x, [Cout, C, 1, 1], 1, 0, True)
-    finally:
-        C_.conv_set_wgrad_wide(0)
-    torch.testing.assert_close(dw, ref, rtol=1e-3, atol=1e-4 * scale + 1e-3)
-    torch.testing.assert_close(dw, base, rtol=1e-4, atol=1e-5 * scale + 1e-4)
