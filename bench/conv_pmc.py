@@ -21,6 +21,8 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--wvariant", type=int, default=0)
+    ap.add_argument("--fvariants", type=int, nargs="+", default=[0],
+                    help="forward / backward-data kernel variants to run, in order (conv_set_variant)")
     a = ap.parse_args(argv)
     shapes = a.shape or [(256, 14, 256, 3, 1, 1), (64, 56, 64, 3, 1, 1)]
     C_ = ops.native()
@@ -31,15 +33,20 @@ def main(argv=None):
         w = (torch.randn(cout, cin, k, k, device=dev, dtype=torch.bfloat16) * 0.05).contiguous(memory_format=cl)
         y = C_.conv_fwd(x, w, s, p, True)[0]
         gy = torch.randn_like(y)
+        wt = C_.conv_dgrad_flip(gy, w, p)[1] if ("dgrad" in a.ops and s == 1) else None
+        for fv in a.fvariants:
+            for _ in range(a.reps):
+                C_.conv_set_variant(fv)
+                if "fwd" in a.ops:
+                    C_.conv_fwd(x, w, s, p, True)
+                if "dgrad" in a.ops and s == 1:
+                    C_.conv_dgrad_preflipped(gy, wt, p)
+                C_.conv_set_variant(0)
         for _ in range(a.reps):
-            if "fwd" in a.ops:
-                C_.conv_fwd(x, w, s, p, True)
             if "wgrad" in a.ops:
                 C_.conv_set_variant(a.wvariant)
                 C_.conv_wgrad(gy, x, list(w.shape), s, p, True)
                 C_.conv_set_variant(0)
-            if "dgrad" in a.ops and s == 1:
-                C_.conv_dgrad_flip(gy, w, p)
     torch.cuda.synchronize()
     print("ok")
 

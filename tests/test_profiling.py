@@ -33,3 +33,17 @@ def test_disabled_on_cpu_and_roctx_is_harmless():
     assert tl.summary() == {}
     with roctx_range("x", enabled=True):
         pass
+
+
+def test_trainer_gives_the_reducer_one_event_slot_per_unresolved_step():
+    """--profile-sync: a step's per-bucket comm events are read max_pending steps
+    later, so the reducer must keep at least max_pending + 1 event slots or the deferred reader
+    sees the NEXT step's (incomplete) events."""
+    from distributed_pytorch_training_amd.config import parse_args
+    from distributed_pytorch_training_amd.engine.trainer import Trainer
+    from distributed_pytorch_training_amd.models import build_model
+
+    args = parse_args(["--model", "resnet18", "--dataset", "synthetic", "--image-size", "32", "--num-classes", "10",
+                       "--profile-sync"])
+    tr = Trainer(build_model("resnet18", 10), args, 0, 1, torch.device("cpu"), log=lambda s: None)
+    assert tr.ddp._profile_slots >= tr.timeline.max_pending + 1
