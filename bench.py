@@ -77,14 +77,15 @@ def parse(argv=None):
                          "per-bucket hipEvents on the comm stream (one event slot per step, read after "
                          "the window: no host sync inside it) -> BASELINE's second metric, %% of step "
                          "in all-reduce, plus exposed comm; 0 = off")
-    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
-                    help="native reducer collective (host = gloo staging, debug only)")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host", "host-async"],
+                    help="native reducer collective (host / host-async = gloo staging, debug only)")
     ap.add_argument("--rccl-channels", type=int, default=0,
                     help="NCCL_MIN/MAX_NCHANNELS for the framework's RCCL communicator (0 = RCCL default)")
     ap.add_argument("--rehearse-shared-gpu", action="store_true",
-                    help="testing: the torchrun ranks share cuda:0 over a gloo process group and the "
-                         "host-bridge collective (--comm host) - the N > 1 path of this script on a "
-                         "1-GPU box (RCCL itself is not exercised; timings are not representative)")
+                    help="testing: the ranks share cuda:0 over a gloo process group and the asynchronous "
+                         "host-bridge collective (--comm host-async: enqueued like RCCL, so backward "
+                         "overlaps it) - the N > 1 path of this script on a 1-GPU box (RCCL itself is not "
+                         "exercised; timings are gloo's, not xGMI's)")
     ap.add_argument("--fake-pg", action="store_true",
                     help="testing: run as rank 0 of a --gpus-rank job on torch's fake process group (CPU)")
     ap.add_argument("--fail-rank", type=int, default=-1,
@@ -255,8 +256,8 @@ def main(argv=None) -> int:
     from distributed_pytorch_training_amd.utils.dist import init_distributed, set_seed
     from distributed_pytorch_training_amd.utils.env import setup_miopen_env, setup_tunableop
 
-    if a.rehearse_shared_gpu:
-        a.comm = "host"
+    if a.rehearse_shared_gpu and a.comm == "rccl":
+        a.comm = "host-async"   # RCCL needs one device per rank
     setup_miopen_env()
     args = train_args(a)
     if a.rehearse_shared_gpu:

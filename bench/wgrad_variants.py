@@ -1,5 +1,5 @@
 """Backward-weight conv kernel variants per ResNet-50 conv shape: default tiles vs the 8-wave
-256 x 256 tile (conv_set_variant(12)), time, TFLOP/s and max relative difference.
+256 x 256 tile (conv_set_variant(20)), time, TFLOP/s and max relative difference.
 
     python bench/wgrad_variants.py [--batch 256] > gpurun_out/wv.md
 """
@@ -19,7 +19,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--image", type=int, default=224)
-    ap.add_argument("--variants", type=int, nargs="+", default=[0, 12])
+    ap.add_argument("--variants", type=int, nargs="+", default=[0, 20])
     a = ap.parse_args(argv)
     from distributed_pytorch_training_amd import ops
 

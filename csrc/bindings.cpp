@@ -1216,8 +1216,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("async_error", &dpt::RcclComm::async_error);
 
   py::class_<dpt::HostBridgeComm, dpt::Collective, std::shared_ptr<dpt::HostBridgeComm>>(m, "HostBridgeComm")
-      .def(py::init<py::object, py::object, int, int, int>(), py::arg("all_reduce_fn"), py::arg("broadcast_fn"),
-           py::arg("rank"), py::arg("world_size"), py::arg("device"));
+      .def(py::init([](py::object ar, py::object bc, int rank, int ws, int dev, bool async_mode, py::object pg) {
+             c10::intrusive_ptr<c10d::ProcessGroup> p;
+             if (!pg.is_none()) p = pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>();
+             return std::make_shared<dpt::HostBridgeComm>(std::move(ar), std::move(bc), rank, ws, dev, async_mode,
+                                                          std::move(p));
+           }),
+           py::arg("all_reduce_fn"), py::arg("broadcast_fn"), py::arg("rank"), py::arg("world_size"),
+           py::arg("device"), py::arg("async_mode") = false, py::arg("process_group") = py::none())
+      // the async bridge drives a torch.distributed group from C++: check the Python object casts
+      .def_static("_process_group_size", [](py::object pg) {
+             return pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>()->getSize();
+           })
+      .def_property_readonly("async_mode", &dpt::HostBridgeComm::async_mode)
+      .def_property_readonly("completed", &dpt::HostBridgeComm::completed);
 
   // Watchdog decision logic with an explicit clock (unit-tested with a fake clock)
   py::class_<dpt::WatchdogCore>(m, "WatchdogCore")

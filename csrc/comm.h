@@ -42,6 +42,8 @@ class Collective {
   virtual ~Collective() = default;
   // In-place SUM all-reduce of `count` elements at device pointer `ptr`, ordered after the
   // work already enqueued on `stream` (and, for asynchronous backends, enqueued on it).
+  // `stream` is used as given: nullptr is the null stream (torch's default current stream on
+  // ROCm), never a request for the comm stream - substituting stream() would race the caller.
   virtual void all_reduce(void* ptr, size_t count, WireType t, hipStream_t stream) = 0;
   virtual void broadcast(void* ptr, size_t count, WireType t, int root, hipStream_t stream) = 0;
   // The stream bucket collectives are issued on (the reducer orders it behind the producer

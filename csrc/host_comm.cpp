@@ -28,12 +28,16 @@ static at::ScalarType to_scalar(WireType t) {
 }
 
 HostBridgeComm::HostBridgeComm(py::object all_reduce_fn, py::object broadcast_fn, int rank, int world_size,
-                               int device)
+                               int device, bool async_mode, c10::intrusive_ptr<c10d::ProcessGroup> process_group)
     : all_reduce_fn_(std::move(all_reduce_fn)),
       broadcast_fn_(std::move(broadcast_fn)),
       rank_(rank),
       world_size_(world_size),
-      device_(device) {
+      device_(device),
+      async_(async_mode),
+      pg_(std::move(process_group)) {
+  if (async_ && world_size > 1 && !pg_)
+    throw std::invalid_argument("HostBridgeComm: async mode needs a (gloo) process group for world_size > 1");
   DPT_HIP_THROW(hipSetDevice(device));
   int lo = 0, hi = 0;
   DPT_HIP_THROW(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -49,7 +53,15 @@ HostBridgeComm::~HostBridgeComm() {
 
 void HostBridgeComm::destroy() {
   if (stream_ != nullptr) {
-    hipStreamSynchronize(stream_);
+    {
+      // async mode: host functions may be pending on any stream the caller used, and they read
+      // the staging buffers freed below - drain the device (without the GIL: a gloo peer may
+      // still need this process's Python side to reach its own matching collective)
+      std::unique_ptr<py::gil_scoped_release> rel;
+      if (PyGILState_Check()) rel = std::make_unique<py::gil_scoped_release>();
+      if (async_) hipDeviceSynchronize();
+      else hipStreamSynchronize(stream_);
+    }
     hipStreamDestroy(stream_);
     stream_ = nullptr;
   }
@@ -58,14 +70,17 @@ void HostBridgeComm::destroy() {
     host_ = nullptr;
     host_bytes_ = 0;
   }
+  for (auto& kv : staging_) hipHostFree(kv.second);
+  staging_.clear();
 }
 
 void HostBridgeComm::check() const {
+  std::lock_guard<std::mutex> lk(err_mu_);
+  if (!error_.empty()) throw std::runtime_error("HostBridgeComm: host collective failed: " + error_);
   if (aborted_) throw std::runtime_error("HostBridgeComm: communicator was aborted");
 }
 
 at::Tensor HostBridgeComm::stage_in(void* ptr, size_t count, WireType t, hipStream_t stream) {
-  if (aborted_ || stream_ == nullptr) throw std::runtime_error("HostBridgeComm: aborted or destroyed");
   const size_t bytes = count * wire_bytes(t);
   if (bytes > host_bytes_) {
     if (host_ != nullptr) DPT_HIP_THROW(hipHostFree(host_));
@@ -73,38 +88,79 @@ at::Tensor HostBridgeComm::stage_in(void* ptr, size_t count, WireType t, hipStre
     DPT_HIP_THROW(hipHostMalloc(&host_, bytes, hipHostMallocDefault));
     host_bytes_ = bytes;
   }
-  hipStream_t s = stream ? stream : stream_;
-  DPT_HIP_THROW(hipMemcpyAsync(host_, ptr, bytes, hipMemcpyDeviceToHost, s));
-  DPT_HIP_THROW(hipStreamSynchronize(s));
+  DPT_HIP_THROW(hipMemcpyAsync(host_, ptr, bytes, hipMemcpyDeviceToHost, stream));
+  DPT_HIP_THROW(hipStreamSynchronize(stream));
   return at::from_blob(host_, {(int64_t)count}, at::TensorOptions().dtype(to_scalar(t)));
 }
 
 void HostBridgeComm::stage_out(void* ptr, size_t count, WireType t, hipStream_t stream) {
-  hipStream_t s = stream ? stream : stream_;
-  DPT_HIP_THROW(hipMemcpyAsync(ptr, host_, count * wire_bytes(t), hipMemcpyHostToDevice, s));
-  DPT_HIP_THROW(hipStreamSynchronize(s));  // the staging buffer is reused by the next call
+  DPT_HIP_THROW(hipMemcpyAsync(ptr, host_, count * wire_bytes(t), hipMemcpyHostToDevice, stream));
+  DPT_HIP_THROW(hipStreamSynchronize(stream));  // the staging buffer is reused by the next call
+}
+
+void HostBridgeComm::call(int op, const at::Tensor& h, int root) {
+  py::gil_scoped_acquire g;
+  if (op == 0) all_reduce_fn_(h);
+  else broadcast_fn_(h, root);
+}
+
+// Runs on HIP's host-function thread, between the D2H and the H2D copy of the stream.  No GIL,
+// no HIP call: a blocking c10d collective on the pinned staging buffer.
+void HostBridgeComm::host_fn(void* arg) {
+  std::unique_ptr<Job> j(static_cast<Job*>(arg));
+  HostBridgeComm* self = j->self;
+  try {
+    if (self->aborted_.load()) throw std::runtime_error("aborted before the collective ran");
+    std::vector<at::Tensor> v{
+        at::from_blob(j->host, {(int64_t)j->count}, at::TensorOptions().dtype(to_scalar(j->t)))};
+    if (j->op == 0) {
+      self->pg_->allreduce(v)->wait();
+    } else {
+      c10d::BroadcastOptions o;
+      o.rootRank = j->root;
+      self->pg_->broadcast(v, o)->wait();
+    }
+  } catch (const std::exception& e) {
+    std::lock_guard<std::mutex> lk(self->err_mu_);
+    if (self->error_.empty()) self->error_ = e.what();
+    self->aborted_ = true;
+  }
+  self->completed_.fetch_add(1);
+}
+
+void HostBridgeComm::run(int op, void* ptr, size_t count, WireType t, int root, hipStream_t stream) {
+  if (aborted_ || stream_ == nullptr) throw std::runtime_error("HostBridgeComm: aborted or destroyed");
+  if (count == 0) return;
+  note_op(op, count, t, root);
+  // nullptr is the null stream (torch's default current stream), a real stream to order behind,
+  // not "use the comm stream": substituting stream_ would race the caller's work.
+  hipStream_t s = stream;
+  if (!async_) {
+    at::Tensor h = stage_in(ptr, count, t, s);
+    call(op, h, root);
+    stage_out(ptr, count, t, s);
+    return;
+  }
+  if (world_size_ == 1) return;  // identity; stream order is all a caller can observe
+  const size_t bytes = count * wire_bytes(t);
+  void*& buf = staging_[{ptr, bytes}];  // one pinned buffer per (tensor, size): reuse is stream-ordered
+  if (buf == nullptr) DPT_HIP_THROW(hipHostMalloc(&buf, bytes, hipHostMallocDefault));
+  DPT_HIP_THROW(hipMemcpyAsync(buf, ptr, bytes, hipMemcpyDeviceToHost, s));
+  auto* job = new Job{this, op, root, buf, count, t};
+  hipError_t e = hipLaunchHostFunc(s, &HostBridgeComm::host_fn, job);
+  if (e != hipSuccess) {
+    delete job;
+    DPT_HIP_THROW(e);
+  }
+  DPT_HIP_THROW(hipMemcpyAsync(ptr, buf, bytes, hipMemcpyHostToDevice, s));
 }
 
 void HostBridgeComm::all_reduce(void* ptr, size_t count, WireType t, hipStream_t stream) {
-  if (count == 0) return;
-  note_op(0, count, t, 0);
-  at::Tensor h = stage_in(ptr, count, t, stream);
-  {
-    py::gil_scoped_acquire g;
-    all_reduce_fn_(h);
-  }
-  stage_out(ptr, count, t, stream);
+  run(0, ptr, count, t, 0, stream);
 }
 
 void HostBridgeComm::broadcast(void* ptr, size_t count, WireType t, int root, hipStream_t stream) {
-  if (count == 0) return;
-  note_op(1, count, t, root);
-  at::Tensor h = stage_in(ptr, count, t, stream);
-  {
-    py::gil_scoped_acquire g;
-    broadcast_fn_(h, root);
-  }
-  stage_out(ptr, count, t, stream);
+  run(1, ptr, count, t, root, stream);
 }
 
 }  // namespace dpt

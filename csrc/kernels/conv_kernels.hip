@@ -1803,6 +1803,8 @@ int conv_split_cols(int64_t M) { return (int)((M + 15) / 16); }
 // conv_set_variant switches at run time (A/B tests, benchmarks; the bindings' conv_set_variant).
 static int g_conv_variant = 0;
 static int conv_variant() { return g_conv_variant; }
+// forward / backward-data tile variant: codes >= 20 select backward-weight tiles only
+static int fwd_variant() { return g_conv_variant >= 20 ? 0 : g_conv_variant; }
 void conv_set_variant(int v) { g_conv_variant = v; }
 
 // Production choice of the 8-wave 256-row tiles (variant 0): deep reductions onto narrow
@@ -2140,7 +2142,7 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
   const bool wide = Cout % 128 == 0;
   a.n_tiles = Cout / (wide ? 128 : 64);
   a.mt256 = 0;
-  const int v = conv_variant();
+  const int v = fwd_variant();
   if (!bkn && maybe_split(a, ws, psum != nullptr, false, false, false, s)) return;
   if (!bkn && !a.f16) {
     const int vb = (v >= 9 && v <= 13) ? v : v == 0 ? conv_big_auto(a.M, Cout, (int64_t)R * S * C) : 0;
@@ -2181,7 +2183,7 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
     a.bp_ld = keep_ld;
   }
   const bool two = res && bnx2 != nullptr;
-  const int cv = conv_variant();
+  const int cv = fwd_variant();
   if (!f16 && (cv == 0 || (cv >= 9 && cv <= 13))) {
     // 8-wave tiles (conv_big_auto, or a forced variant): N = C, K = Cout*R*S
     const int vb = cv ? cv : conv_big_auto(a.M, C, (int64_t)Cout * R * S);
@@ -2409,8 +2411,9 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
   // the MFMA work per staged dy tile); the 16-channel space-to-depth stem takes all 16 taps of
   // its 4x4 window in one 256-column tile (dy staged once instead of four times)
   pl.bnw = C % 128 == 0 ? 128 : (C == 64 && R * S > 1) ? 128 : (C == 16 && R * S * C >= 256 && pl.bmw == 64) ? 256 : 64;
-  // variant 12 (A/B): 8-wave 256 x 256 tiles where both channel counts allow them
-  if (conv_variant() == 12 && Cout % 256 == 0 && C % 256 == 0) pl.bmw = pl.bnw = 256;
+  // variant 20 (A/B, bench/wgrad_variants.py): 8-wave 256 x 256 tiles where both channel counts
+  // allow them.  Its own code: 10-13 select forward/dgrad tile variants (conv_fwd_big).
+  if (conv_variant() == 20 && Cout % 256 == 0 && C % 256 == 0) pl.bmw = pl.bnw = 256;
   const int tiles = (Cout / pl.bmw) * ((R * S * C + pl.bnw - 1) / pl.bnw);
   const int steps = (int)((M + 63) / 64);
   // ~768 blocks (3 per CU) and at least 32 K-steps per split: a split's fp32 partial tile
@@ -2469,7 +2472,7 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
     a.div_h = make_fastdiv((uint32_t)H);
   }
   dim3 grid((unsigned)(a.co_tiles * a.n_tiles * a.splits)), block(conv::kThreads);
-  const int v = a.f16 ? 0 : conv_variant();
+  const int v = a.f16 ? 0 : fwd_variant();
   if (pl.halo) {
 #define DPT_WH(BNW, ST)                                                                      \
   do {                                                                                       \

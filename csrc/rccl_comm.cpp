@@ -78,7 +78,7 @@ void RcclComm::inject_async_error(const std::string& msg) {
 }
 
 void RcclComm::track(hipStream_t stream) {
-  if (watchdog_ && !aborted_.load()) watchdog_->track(stream ? stream : stream_);
+  if (watchdog_ && !aborted_.load()) watchdog_->track(stream);
 }
 
 std::string RcclComm::async_error() const {
@@ -114,7 +114,7 @@ void RcclComm::destroy() {
 void RcclComm::all_reduce(void* ptr, size_t count, WireType t, hipStream_t stream) {
   if (aborted_.load() || comm_ == nullptr) throw std::runtime_error("RcclComm: communicator was aborted or destroyed");
   if (count == 0) return;
-  hipStream_t s = stream ? stream : stream_;
+  hipStream_t s = stream;  // nullptr = the null stream, ordered like any other
   note_op(0, count, t, 0);
   DPT_RCCL_CHECK(ncclAllReduce(ptr, ptr, count, to_nccl(t), ncclSum, comm_, s));
   if (watchdog_) watchdog_->track(s);
@@ -123,7 +123,7 @@ void RcclComm::all_reduce(void* ptr, size_t count, WireType t, hipStream_t strea
 void RcclComm::broadcast(void* ptr, size_t count, WireType t, int root, hipStream_t stream) {
   if (aborted_.load() || comm_ == nullptr) throw std::runtime_error("RcclComm: communicator was aborted or destroyed");
   if (count == 0) return;
-  hipStream_t s = stream ? stream : stream_;
+  hipStream_t s = stream;  // nullptr = the null stream, ordered like any other
   note_op(1, count, t, root);
   DPT_RCCL_CHECK(ncclBroadcast(ptr, ptr, count, to_nccl(t), root, comm_, s));
   if (watchdog_) watchdog_->track(s);

@@ -12,6 +12,11 @@ on, one of
   served by ``torch.distributed`` over gloo through pinned host staging.  Several ranks can
   then share one GPU and still run the whole multi-rank GPU data path (tests/
   test_multirank_gpu.py); it is a verification / debug transport, not a fast one.
+* ``"host-async"`` - the same bridge enqueued like RCCL (D2H, a HIP host function running the
+  gloo collective, H2D on the caller's stream; the caller never blocks), so backward overlaps
+  the in-flight collective and the exposed-comm measurement means something on one GPU.  Its
+  collectives use a gloo group of their own, driven from C++ on HIP's host-function thread
+  without the GIL; they never interleave with the main thread's collectives on the default group.
 
 On CPU (gloo) there is no device collective; ``make_comm`` returns ``None`` and the reducer
 drives ``torch.distributed`` through a Python callback instead.
@@ -37,8 +42,9 @@ import torch.distributed as dist
 
 from .. import ops
 
-COMM_KINDS = ("rccl", "host")
+COMM_KINDS = ("rccl", "host", "host-async")
 _HOST_GROUP = None
+_ASYNC_GROUP = None
 
 
 def _host_group():
@@ -47,6 +53,15 @@ def _host_group():
     if _HOST_GROUP is None:
         _HOST_GROUP = dist.group.WORLD if dist.get_backend() == "gloo" else dist.new_group(backend="gloo")
     return _HOST_GROUP
+
+
+def _async_group():
+    """A gloo group of its own for the asynchronous bridge (its collectives run on another
+    thread, concurrently with the main thread's).  Collective creation: every rank, same point."""
+    global _ASYNC_GROUP
+    if _ASYNC_GROUP is None:
+        _ASYNC_GROUP = dist.new_group(backend="gloo")
+    return _ASYNC_GROUP
 
 
 def _host_all_reduce(t: torch.Tensor) -> None:
@@ -67,11 +82,16 @@ def make_comm(device: torch.device, rank: int, world_size: int, kind: str = "rcc
         raise ValueError(f"unknown communicator kind {kind!r}; expected one of {COMM_KINDS}")
     C = ops.native()
     dev = device.index if device.index is not None else 0
-    if kind == "host":
+    if kind in ("host", "host-async"):
         if world_size > 1 and not dist.is_initialized():
             raise RuntimeError("the host-bridge communicator needs an initialised process group")
+        if kind == "host-async":
+            # collective group creation: every rank, same point.  The bridge calls the group's
+            # C++ ProcessGroup from HIP's host-function thread, without the GIL.
+            pg = _async_group() if world_size > 1 else None
+            return C.HostBridgeComm(_host_all_reduce, _host_broadcast, rank, world_size, dev, True, pg)
         if world_size > 1:
-            _host_group()   # collective group creation: every rank, same point
+            _host_group()
         return C.HostBridgeComm(_host_all_reduce, _host_broadcast, rank, world_size, dev)
     n_ch = max(0, int(rccl_channels or 0))
     if world_size > 1:

@@ -120,7 +120,7 @@ def test_bench_self_launch_two_ranks_on_one_gpu(tmp_path):
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout[-2000:]
     rec = lines[0]
-    assert rec["n_gpus"] == 2 and rec["comm"]["world_size"] == 2 and rec["comm"]["kind"] == "host"
+    assert rec["n_gpus"] == 2 and rec["comm"]["world_size"] == 2 and rec["comm"]["kind"] == "host-async"
     assert rec["config"]["launcher"] == "self"
     assert [d["device"] for d in rec["comm"]["rank_devices"]] == ["cuda:0", "cuda:0"]
 
@@ -141,7 +141,7 @@ def test_bench_two_ranks_sharing_one_gpu(tmp_path):
     assert len(lines) == 1, r.stdout[-2000:]
     rec = lines[0]
     assert KEYS <= set(rec) and rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
-    assert rec["config"]["global_batch"] == 64 and rec["comm"]["kind"] == "host"
+    assert rec["config"]["global_batch"] == 64 and rec["comm"]["kind"] == "host-async"
     assert rec["value"] == pytest.approx(64 * 1e3 / rec["ms_per_step"], rel=0.02)
     # a real collective ran: the sync share is a measured number and buckets were formed
     assert isinstance(rec["pct_step_allreduce"], float) and rec["pct_step_allreduce"] > 0

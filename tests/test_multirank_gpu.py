@@ -81,7 +81,7 @@ def _run_native(rank, ws, device, extra, amp, steps, inf_step):
     torch.cuda.synchronize()
     ddp = tr.ddp
     if ws > 1:
-        assert ddp.comm is not None and ddp.comm.kind == "host"
+        assert ddp.comm is not None and ddp.comm.kind.startswith("host")
     res = {"params": {n: p.detach().float().cpu() for n, p in model.named_parameters()},
            "buffers": {n: b.detach().float().cpu() for n, b in model.named_buffers()},
            "comm_ops": int(ddp.comm.ops) if ddp.comm is not None else 0,
@@ -247,6 +247,9 @@ def _bf16(t):
 # (variant, flags): the FULL native engine (MFMA convs, fused BN, weight shadows, steal mode)
 LOCAL_CASES = [
     ("native_fp32_wire", []),
+    # the asynchronous bridge: collectives enqueued on the comm stream (HIP host functions), the
+    # autograd thread never blocks - same sums required
+    ("native_fp32_wire_async", ["--comm", "host-async"]),
     ("native_bf16_wire", ["--grad-dtype", "bf16"]),
     ("miopen_bf16_wire", MIOPEN + ["--grad-dtype", "bf16"]),
 ]
