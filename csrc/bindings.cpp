@@ -321,6 +321,15 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t pad) {
   return dx;
 }
 
+// Optional 1-bit ReLU mask output of a block tail's forward apply: uint8 [M, C/8] on x's device.
+static uint8_t* relu_mask_ptr(const c10::optional<Tensor>& m, int64_t M, int64_t C, const Tensor& x, const char* who) {
+  if (!m.has_value() || !m->defined()) return nullptr;
+  TORCH_CHECK(m->device() == x.device() && m->scalar_type() == at::kByte && m->is_contiguous() && m->dim() == 2 &&
+                  m->size(0) == M && m->size(1) == C / 8,
+              who, ": mask_out must be a contiguous uint8 [M, C/8] tensor on x's device");
+  return m->data_ptr<uint8_t>();
+}
+
 // Stride-1 backward-data whose epilogue also sums the backward statistics of the BatchNorm+ReLU
 // that produced the conv's input (bn_x: that BN's input, same shape as dx; coef = [a | b]).
 // Returns {dx, p1, p2} with p1/p2 [C, m_tiles] for bn_bwd_partials.
@@ -330,7 +339,8 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
                                        c10::optional<Tensor> bn_coef,
                                        c10::optional<Tensor> bn_y, c10::optional<Tensor> bn_res,
                                        c10::optional<Tensor> w_flipped, c10::optional<Tensor> bn_x2,
-                                       c10::optional<Tensor> bn_mean2, PendingReducePtr wgrad_reduce) {
+                                       c10::optional<Tensor> bn_mean2, PendingReducePtr wgrad_reduce,
+                                       c10::optional<Tensor> bn_mask) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(w, "w");
   check_cl_bf16(bn_x, "bn_x");
@@ -376,6 +386,12 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
     TORCH_CHECK(bn_x2->sizes() == bn_x.sizes(), "conv_dgrad_bnstats: bn_x2 must match bn_x");
   }
   auto p3 = at::empty({two ? C : 0, two ? mt : 0}, dy.options().dtype(at::kFloat));
+  // the tail's 1-bit ReLU mask (bn_fwd_train mask_out): read instead of bn_y
+  const uint8_t* mp = nullptr;
+  if (bn_mask.has_value() && bn_mask->defined()) {
+    TORCH_CHECK(res, "conv_dgrad_bnstats: bn_mask needs bn_y / bn_res");
+    mp = relu_mask_ptr(bn_mask, (int64_t)N * H * W, C, dy, "conv_dgrad_bnstats");
+  }
   auto st = cur_stream(dy);
   if (!pre)
     dpt::launch_conv_wt_flip(reinterpret_cast<const uint16_t*>(w.data_ptr()), reinterpret_cast<uint16_t*>(wt.data_ptr()),
@@ -391,7 +407,7 @@ std::vector<Tensor> conv_dgrad_bnstats(Tensor dy, Tensor w, int64_t pad, Tensor 
                                  two ? reinterpret_cast<const uint16_t*>(bn_x2->data_ptr()) : nullptr,
                                  two ? f32_param(bn_mean2, C, "bn_mean2") : nullptr,
                                  two ? p3.data_ptr<float>() : nullptr, is_f16(dy),
-                                 ws.defined() ? ws.data_ptr<float>() : nullptr);
+                                 ws.defined() ? ws.data_ptr<float>() : nullptr, mp);
   return {dx, p1, p2, p3};
 }
 
@@ -636,7 +652,7 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::
                                  c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
                                  c10::optional<Tensor> running_var, c10::optional<Tensor> num_batches,
                                  double momentum, double eps, bool relu, c10::optional<Tensor> psum,
-                                 c10::optional<Tensor> psq, bool apply) {
+                                 c10::optional<Tensor> psq, bool apply, c10::optional<Tensor> mask_out) {
   auto [M, C] = bn_rows(x, "x");
   TORCH_CHECK(dpt::bn_supported(C), "fused BN: unsupported channel count ", C);
   const void* rp = nullptr;
@@ -656,6 +672,8 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::
   auto fopt = x.options().dtype(at::kFloat);
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
   auto coef = at::empty({2 * C}, fopt);  // [a | b]: y = relu(x*a + b [+ r]); lets bn_bwd skip reading y
+  uint8_t* mp = relu_mask_ptr(mask_out, M, C, x, "bn_fwd_train");
+  TORCH_CHECK(mp == nullptr || (relu && rp != nullptr && apply), "bn_fwd_train: mask_out needs relu + residual");
   c10::hip::HIPGuard guard(x.device().index());
   if (psum.has_value() && psum->defined()) {
     // statistics summed by the producing conv's epilogue: [C][chunks] fp32 partials
@@ -668,7 +686,7 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::
                                      f32_param(bias, C, "bias"), (float)eps, (float)momentum,
                                      f32_param(running_mean, C, "running_mean"),
                                      f32_param(running_var, C, "running_var"), nb, mean.data_ptr<float>(),
-                                     invstd.data_ptr<float>(), coef.data_ptr<float>(), relu, cur_stream(x));
+                                     invstd.data_ptr<float>(), coef.data_ptr<float>(), relu, cur_stream(x), mp);
     return {y, mean, invstd, coef};
   }
   auto ws = at::empty({dpt::bn_workspace_floats(M, C)}, fopt);
@@ -676,12 +694,12 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::
                            f32_param(bias, C, "bias"), (float)eps, (float)momentum,
                            f32_param(running_mean, C, "running_mean"), f32_param(running_var, C, "running_var"), nb,
                            mean.data_ptr<float>(), invstd.data_ptr<float>(), coef.data_ptr<float>(),
-                           ws.data_ptr<float>(), relu, cur_stream(x));
+                           ws.data_ptr<float>(), relu, cur_stream(x), mp);
   return {y, mean, invstd, coef};
 }
 
 // y = relu(x*a + b + x2*a2 + b2), coef = [a | b], coef2 = [a2 | b2] (bn_fwd_train coefficients)
-Tensor bn_apply_aff(Tensor x, Tensor x2, Tensor coef, Tensor coef2) {
+Tensor bn_apply_aff(Tensor x, Tensor x2, Tensor coef, Tensor coef2, c10::optional<Tensor> mask_out) {
   auto [M, C] = bn_rows(x, "x");
   TORCH_CHECK(dpt::bn_supported(C), "fused BN: unsupported channel count ", C);
   TORCH_CHECK(x2.sizes() == x.sizes() && x2.scalar_type() == x.scalar_type(), "bn_apply_aff: x2 mismatch");
@@ -690,8 +708,9 @@ Tensor bn_apply_aff(Tensor x, Tensor x2, Tensor coef, Tensor coef2) {
   const float* a2 = f32_param(coef2, 2 * C, "coef2");
   auto y = at::empty_like(x);
   c10::hip::HIPGuard guard(x.device().index());
+  uint8_t* mp = relu_mask_ptr(mask_out, M, C, x, "bn_apply_aff");
   dpt::launch_bn_apply_aff(bn_dtype(x), x.data_ptr(), x2.data_ptr(), y.data_ptr(), M, C, a, a + C, a2, a2 + C,
-                           cur_stream(x));
+                           cur_stream(x), mp);
   return y;
 }
 
@@ -1101,9 +1120,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_supported", [](int64_t C) { return dpt::bn_supported(C); });
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("residual"), py::arg("weight"), py::arg("bias"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches"), py::arg("momentum"), py::arg("eps"),
-        py::arg("relu"), py::arg("psum") = py::none(), py::arg("psq") = py::none(), py::arg("apply") = true);
+        py::arg("relu"), py::arg("psum") = py::none(), py::arg("psq") = py::none(), py::arg("apply") = true,
+        py::arg("mask_out") = py::none());
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("residual"), py::arg("a"), py::arg("b"), py::arg("relu"));
-  m.def("bn_apply_aff", &bn_apply_aff, py::arg("x"), py::arg("x2"), py::arg("coef"), py::arg("coef2"));
+  m.def("bn_apply_aff", &bn_apply_aff, py::arg("x"), py::arg("x2"), py::arg("coef"), py::arg("coef2"),
+        py::arg("mask_out") = py::none());
   m.def("bn2_bwd_partials", &bn2_bwd_partials, py::arg("dz"), py::arg("x"), py::arg("x2"), py::arg("weight"),
         py::arg("weight2"), py::arg("mean"), py::arg("invstd"), py::arg("mean2"), py::arg("invstd2"), py::arg("p1"),
         py::arg("p2"), py::arg("p3"), py::arg("want_dparams"));
@@ -1148,7 +1169,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad_bnstats", &conv_dgrad_bnstats, py::arg("grad_output"), py::arg("w"), py::arg("pad"),
         py::arg("bn_x"), py::arg("bn_mean"), py::arg("bn_coef"), py::arg("bn_y") = py::none(),
         py::arg("bn_res") = py::none(), py::arg("w_flipped") = py::none(), py::arg("bn_x2") = py::none(),
-        py::arg("bn_mean2") = py::none(), py::arg("wgrad_reduce") = nullptr);
+        py::arg("bn_mean2") = py::none(), py::arg("wgrad_reduce") = nullptr, py::arg("bn_mask") = py::none());
   m.def("conv_wt_flip_multi", &conv_wt_flip_multi, py::arg("ws"));
   m.def("conv_dgrad_preflipped", &conv_dgrad_preflipped, py::arg("grad_output"), py::arg("w_flipped"), py::arg("pad"),
         py::arg("wgrad_reduce") = nullptr);

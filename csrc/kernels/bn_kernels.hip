@@ -51,7 +51,20 @@ struct BF16 {
     w.w = (uint32_t)f32_to_bf16(f[6]) | ((uint32_t)f32_to_bf16(f[7]) << 16);
     *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p) + i) = w;
   }
-  // y > 0 test straight on the bits (sign clear and not +0): no conversion needed.
+  // y > 0 test straight on the bits (sign clear, not +0, not NaN): no conversion needed.
+  __device__ static bool pos16(uint32_t h) { return !(h & 0x8000u) && (h & 0x7fffu) && (h & 0x7fffu) <= 0x7f80u; }
+  // store8 that also returns the ReLU mask of the STORED (rounded) values, bit k = channel k
+  __device__ static uint32_t store8m(void* p, int64_t i, const float f[8]) {
+    uint32_t h[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = f32_to_bf16(f[k]);
+    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p) + i) =
+        make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16));
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m |= (pos16(h[k]) ? 1u : 0u) << k;
+    return m;
+  }
   __device__ static void pos8(const void* p, int64_t i, bool m[8]) {
     uint4 w = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p) + i);
     uint32_t u[4] = {w.x, w.y, w.z, w.w};
@@ -83,6 +96,13 @@ struct F16 {
     w.w = (uint32_t)to16(f[6]) | ((uint32_t)to16(f[7]) << 16);
     *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p) + i) = w;
   }
+  __device__ static uint32_t store8m(void* p, int64_t i, const float f[8]) {
+    store8(p, i, f);
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m |= ((float)__builtin_bit_cast(_Float16, to16(f[k])) > 0.0f ? 1u : 0u) << k;
+    return m;
+  }
   __device__ static void pos8(const void* p, int64_t i, bool m[8]) {
     float f[8];
     load8(p, i, f);
@@ -101,6 +121,13 @@ struct F32 {
     float4* q = reinterpret_cast<float4*>(static_cast<float*>(p) + i);
     q[0] = make_float4(f[0], f[1], f[2], f[3]);
     q[1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+  __device__ static uint32_t store8m(void* p, int64_t i, const float f[8]) {
+    store8(p, i, f);
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m |= (f[k] > 0.0f ? 1u : 0u) << k;
+    return m;
   }
   __device__ static void pos8(const void* p, int64_t i, bool m[8]) {
     float f[8];
@@ -239,7 +266,8 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(const void* __rest
                                                               const float* __restrict__ coef_b,
                                                               int64_t M, int C, int rev,
                                                               const float* __restrict__ coef_a2 = nullptr,
-                                                              const float* __restrict__ coef_b2 = nullptr) {
+                                                              const float* __restrict__ coef_b2 = nullptr,
+                                                              uint8_t* __restrict__ mask = nullptr) {
   const int tpr = C >> 3, rpi = kBlock / tpr;
   const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
   float a[8], b[8], a2[8], b2[8];
@@ -282,8 +310,15 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(const void* __rest
       v0[k] = o0;
       v1[k] = o1;
     }
-    IO::store8(y, r * C + cg * 8, v0);
-    if (two) IO::store8(y, r2 * C + cg * 8, v1);
+    if (RELU && RES && mask != nullptr) {
+      // block tail: also the 1-bit ReLU mask [M][C/8] the consuming conv's backward-data
+      // epilogue reads instead of y (ops/bn.py) - 1/16 of y's bytes
+      mask[r * tpr + cg] = (uint8_t)IO::store8m(y, r * C + cg * 8, v0);
+      if (two) mask[r2 * tpr + cg] = (uint8_t)IO::store8m(y, r2 * C + cg * 8, v1);
+    } else {
+      IO::store8(y, r * C + cg * 8, v0);
+      if (two) IO::store8(y, r2 * C + cg * 8, v1);
+    }
   }
 }
 
@@ -552,10 +587,12 @@ BnGeometry bn_geometry(int64_t M, int64_t C) {
 
 template <typename IO>
 static void fwd_apply_dispatch(bool relu, bool res, const void* x, const void* r, void* y, const float* a,
-                               const float* b, int64_t M, int C, int blocks, hipStream_t s) {
+                               const float* b, int64_t M, int C, int blocks, hipStream_t s, uint8_t* mask = nullptr) {
   dim3 gr(blocks), bl(kBlock);
   const int rev = kBnReverse;
-  if (relu && res) hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, true, true>), gr, bl, 0, s, x, r, y, a, b, M, C, rev);
+  if (relu && res)
+    hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, true, true>), gr, bl, 0, s, x, r, y, a, b, M, C, rev, nullptr, nullptr,
+                       mask);
   else if (relu) hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, true, false>), gr, bl, 0, s, x, r, y, a, b, M, C, rev);
   else if (res) hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, false, true>), gr, bl, 0, s, x, r, y, a, b, M, C, rev);
   else hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, false, false>), gr, bl, 0, s, x, r, y, a, b, M, C, rev);
@@ -564,7 +601,7 @@ static void fwd_apply_dispatch(bool relu, bool res, const void* x, const void* r
 void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                          const float* gamma, const float* beta, float eps, float momentum, float* run_mean,
                          float* run_var, int64_t* num_batches, float* save_mean, float* save_invstd,
-                         float* save_coef, float* workspace, bool relu, hipStream_t s) {
+                         float* save_coef, float* workspace, bool relu, hipStream_t s, uint8_t* mask) {
   BnGeometry g = bn_geometry(M, C);
   float* psum = workspace;
   float* psq = psum + (int64_t)C * g.chunks;
@@ -580,9 +617,9 @@ void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int
                      gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd, ca, cb);
   if (y == nullptr) return;  // statistics only (the apply is fused elsewhere)
   switch (dtype) {
-    case 0: fwd_apply_dispatch<F32>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
-    case 1: fwd_apply_dispatch<BF16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
-    default: fwd_apply_dispatch<F16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
+    case 0: fwd_apply_dispatch<F32>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s, mask); break;
+    case 1: fwd_apply_dispatch<BF16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s, mask); break;
+    default: fwd_apply_dispatch<F16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s, mask); break;
   }
 }
 
@@ -592,7 +629,7 @@ void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void
                                  const float* psum, const float* psq, int chunks, const float* gamma,
                                  const float* beta, float eps, float momentum, float* run_mean, float* run_var,
                                  int64_t* num_batches, float* save_mean, float* save_invstd, float* save_coef,
-                                 bool relu, hipStream_t s) {
+                                 bool relu, hipStream_t s, uint8_t* mask) {
   BnGeometry g = bn_geometry(M, C);
   float* ca = save_coef;
   float* cb = ca + C;
@@ -608,9 +645,9 @@ void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void
                        ca, cb);
   if (y == nullptr) return;  // statistics only (the apply is fused elsewhere)
   switch (dtype) {
-    case 0: fwd_apply_dispatch<F32>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
-    case 1: fwd_apply_dispatch<BF16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
-    default: fwd_apply_dispatch<F16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s); break;
+    case 0: fwd_apply_dispatch<F32>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s, mask); break;
+    case 1: fwd_apply_dispatch<BF16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s, mask); break;
+    default: fwd_apply_dispatch<F16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s, mask); break;
   }
 }
 
@@ -725,13 +762,13 @@ void launch_bn_bwd_from_partials(int dtype, const void* dy, const void* x, int64
 }
 
 void launch_bn_apply_aff(int dtype, const void* x, const void* x2, void* y, int64_t M, int64_t C, const float* a,
-                         const float* b, const float* a2, const float* b2, hipStream_t s) {
+                         const float* b, const float* a2, const float* b2, hipStream_t s, uint8_t* mask) {
   BnGeometry g = bn_geometry(M, C);
   dim3 gr(g.apply_blocks), bl(kBlock);
   switch (dtype) {
-    case 0: hipLaunchKernelGGL((bn_fwd_apply_kernel<F32, true, true, true>), gr, bl, 0, s, x, x2, y, a, b, M, (int)C, kBnReverse, a2, b2); break;
-    case 1: hipLaunchKernelGGL((bn_fwd_apply_kernel<BF16, true, true, true>), gr, bl, 0, s, x, x2, y, a, b, M, (int)C, kBnReverse, a2, b2); break;
-    default: hipLaunchKernelGGL((bn_fwd_apply_kernel<F16, true, true, true>), gr, bl, 0, s, x, x2, y, a, b, M, (int)C, kBnReverse, a2, b2); break;
+    case 0: hipLaunchKernelGGL((bn_fwd_apply_kernel<F32, true, true, true>), gr, bl, 0, s, x, x2, y, a, b, M, (int)C, kBnReverse, a2, b2, mask); break;
+    case 1: hipLaunchKernelGGL((bn_fwd_apply_kernel<BF16, true, true, true>), gr, bl, 0, s, x, x2, y, a, b, M, (int)C, kBnReverse, a2, b2, mask); break;
+    default: hipLaunchKernelGGL((bn_fwd_apply_kernel<F16, true, true, true>), gr, bl, 0, s, x, x2, y, a, b, M, (int)C, kBnReverse, a2, b2, mask); break;
   }
 }
 

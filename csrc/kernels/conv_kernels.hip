@@ -108,6 +108,9 @@ struct ConvFwdArgs {
   // next block's identity path
   const uint16_t* bny;    // its output y (ReLU mask)
   const uint16_t* bnres;  // the identity-path gradient (added before the mask)
+  // the same ReLU mask as 1 bit per element, [M][Cout/8] bytes written by the tail's forward
+  // apply (bn_kernels.hip): read instead of bny when set - 1/16 of y's bytes
+  const uint8_t* bnmask = nullptr;
   // BNR with a downsample branch: the block's identity path was BN2(x2) (folded into the tail,
   // ops/bn.py _BN2AddReLUPair): also sum s3 = sum dz*(x2 - mean2) for that BatchNorm
   const uint16_t* bnx2;
@@ -646,6 +649,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
 #pragma unroll
     for (int g0 = 0; g0 < NPASS; g0 += GRP) {
       uint4 xv[GRP], yv[GRP], rv[GRP], x2v[GRP];
+      uint32_t mv[GRP];
       if (BNB) {
 #pragma unroll
         for (int q = 0; q < GRP; ++q) {
@@ -653,7 +657,13 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
           const int64_t off = grow(m < p.M ? m : 0) * p.Cout + n0 + oc * 8;
           xv[q] = *reinterpret_cast<const uint4*>(p.bnx + off);
           if (BNR) {
-            yv[q] = *reinterpret_cast<const uint4*>(p.bny + off);
+            if (p.bnmask != nullptr) {
+              mv[q] = p.bnmask[off >> 3];
+              yv[q] = make_uint4(0u, 0u, 0u, 0u);
+            } else {
+              mv[q] = 0u;
+              yv[q] = *reinterpret_cast<const uint4*>(p.bny + off);
+            }
             rv[q] = *reinterpret_cast<const uint4*>(p.bnres + off);
             if (two) x2v[q] = *reinterpret_cast<const uint4*>(p.bnx2 + off);
             else x2v[q] = make_uint4(0u, 0u, 0u, 0u);
@@ -683,9 +693,9 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
                 const float x = cunpack<F16>(xu[k2], h);
                 float dz;
                 if (BNR) {
-                  const float yy = cunpack<F16>(yu[k2], h);
+                  const bool pos = p.bnmask != nullptr ? ((mv[q] >> k) & 1u) != 0u : cunpack<F16>(yu[k2], h) > 0.0f;
                   const float rr = cunpack<F16>(ru[k2], h);
-                  dz = yy > 0.0f ? g + rr : 0.0f;
+                  dz = pos ? g + rr : 0.0f;
                 } else {
                   dz = __builtin_fmaf(x, ba[k], bb[k]) > 0.0f ? g : 0.0f;
                 }
@@ -834,8 +844,10 @@ __global__ __launch_bounds__(256) void conv_split_epilogue_kernel(ConvFwdArgs p)
     if (BNB) {
       const uint4 xv = *reinterpret_cast<const uint4*>(p.bnx + off);
       uint4 yv = make_uint4(0u, 0u, 0u, 0u), rv = yv, x2v = yv;
+      uint32_t mv = 0u;
       if (BNR) {
-        yv = *reinterpret_cast<const uint4*>(p.bny + off);
+        if (p.bnmask != nullptr) mv = p.bnmask[off >> 3];
+        else yv = *reinterpret_cast<const uint4*>(p.bny + off);
         rv = *reinterpret_cast<const uint4*>(p.bnres + off);
         if (two) x2v = *reinterpret_cast<const uint4*>(p.bnx2 + off);
       }
@@ -851,7 +863,8 @@ __global__ __launch_bounds__(256) void conv_split_epilogue_kernel(ConvFwdArgs p)
           const float x = cunpack<F16>(xu[k2], h);
           float dz;
           if (BNR) {
-            dz = cunpack<F16>(yu[k2], h) > 0.0f ? g + cunpack<F16>(ru[k2], h) : 0.0f;
+            const bool pos = p.bnmask != nullptr ? ((mv >> k) & 1u) != 0u : cunpack<F16>(yu[k2], h) > 0.0f;
+            dz = pos ? g + cunpack<F16>(ru[k2], h) : 0.0f;
           } else {
             dz = __builtin_fmaf(x, p.bn_coef[c], p.bn_coef[p.Cout + c]) > 0.0f ? g : 0.0f;
           }
@@ -2159,7 +2172,7 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
                                int C, int R, int S, int pad, const uint16_t* bnx, const float* bn_mean,
                                const float* bn_coef, float* bp1, float* bp2, hipStream_t s,
                                const uint16_t* bny, const uint16_t* bnres, const uint16_t* bnx2,
-                               const float* bn_mean2, float* bp3, bool f16, float* ws) {
+                               const float* bn_mean2, float* bp3, bool f16, float* ws, const uint8_t* bnmask) {
   ConvFwdArgs a;
   a.part = nullptr; a.splits = 1; a.kps = 0;
   a.f16 = f16 ? 1 : 0;
@@ -2171,7 +2184,7 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
   a.m_tiles = conv_m_tiles(a.M);
   a.mt256 = 0;
   a.bnx = bnx; a.bn_mean = bn_mean; a.bn_coef = bn_coef; a.bp1 = bp1; a.bp2 = bp2;
-  a.bny = bny; a.bnres = bnres;
+  a.bny = bny; a.bnres = bnres; a.bnmask = bnmask;
   a.bnx2 = bnx2; a.bn_mean2 = bn_mean2; a.bp3 = bp3;
   a.bp_ld = a.m_tiles; a.bp_off = 0;
   const bool res = bny != nullptr;

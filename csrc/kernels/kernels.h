@@ -57,19 +57,21 @@ int64_t bn_workspace_floats(int64_t M, int64_t C);
 void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                          const float* gamma, const float* beta, float eps, float momentum, float* run_mean,
                          float* run_var, int64_t* num_batches, float* save_mean, float* save_invstd,
-                         float* save_coef, float* workspace, bool relu, hipStream_t s);
+                         float* save_coef, float* workspace, bool relu, hipStream_t s, uint8_t* mask = nullptr);
+// mask (relu + residual only, else ignored): also write the 1-bit ReLU mask of y, [M][C/8] bytes,
+// bit k of byte (m, g) = y[m, 8g + k] > 0 after rounding to y's dtype
 void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                                  const float* psum, const float* psq, int chunks, const float* gamma,
                                  const float* beta, float eps, float momentum, float* run_mean, float* run_var,
                                  int64_t* num_batches, float* save_mean, float* save_invstd, float* save_coef,
-                                 bool relu, hipStream_t s);
+                                 bool relu, hipStream_t s, uint8_t* mask = nullptr);
 void launch_bn_bwd_from_partials(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* gamma,
                                  const float* mean, const float* invstd, const float* coef, const float* p1,
                                  const float* p2, int chunks, float* dgamma, float* dbeta, void* dx, float* kbuf,
                                  hipStream_t s, bool from_dz = false);
 // y = relu(x*a + b + x2*a2 + b2) (block tail with its downsample BatchNorm folded in)
 void launch_bn_apply_aff(int dtype, const void* x, const void* x2, void* y, int64_t M, int64_t C, const float* a,
-                         const float* b, const float* a2, const float* b2, hipStream_t s);
+                         const float* b, const float* a2, const float* b2, hipStream_t s, uint8_t* mask = nullptr);
 // backward of that: finalize both BNs from dgrad-epilogue partials (p1 shared), one apply pass
 // writing dx and dx2; kbuf: 6C floats
 void launch_bn2_bwd_from_partials(int dtype, const void* dz, const void* x, const void* x2, int64_t M, int64_t C,
@@ -218,7 +220,8 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
                                const float* bn_coef, float* bp1, float* bp2, hipStream_t s,
                                const uint16_t* bny = nullptr, const uint16_t* bnres = nullptr,
                                const uint16_t* bnx2 = nullptr, const float* bn_mean2 = nullptr,
-                               float* bp3 = nullptr, bool f16 = false, float* ws = nullptr);
+                               float* bp3 = nullptr, bool f16 = false, float* ws = nullptr,
+                               const uint8_t* bnmask = nullptr);
 // many weights flipped/transposed (wt[ci][R-1-r][S-1-s][co] = w[co][r][s][ci]) in one launch
 constexpr int kWtFlipMax = 64;
 struct WtFlipBatch {

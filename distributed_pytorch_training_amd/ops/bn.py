@@ -8,7 +8,9 @@ separate MIOpen/ATen kernels (BN, in-place add, in-place ReLU).
 
 Saved for backward: the BN input ``x`` and, for BN+add+ReLU, the output ``y`` - tensors the
 unfused graph keeps alive anyway (BN saves its input, ReLU its output, and ``y`` is the next
-convolution's saved input), so the fusion costs no extra activation memory.  For BN+ReLU
+convolution's saved input), so the fusion costs no extra activation memory.  A block tail whose
+output feeds a native conv also writes its ReLU mask as 1 bit per element (1/16 of ``y``), which
+that conv's backward-data epilogue reads instead of ``y``.  For BN+ReLU
 without a residual the ReLU mask is recomputed from ``x`` and the forward's per-channel
 coefficients (``fma(x, a, b) > 0``, bit-identical to the forward's decision), so the backward
 passes never read ``y``: 2 of 7 activation passes saved per such layer.
@@ -32,6 +34,12 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
     if t.dim() == 4 and not t.is_contiguous(memory_format=torch.channels_last):
         return t.contiguous(memory_format=torch.channels_last)
     return t
+
+
+def _relu_mask(x: torch.Tensor) -> torch.Tensor:
+    """uint8 [N*H*W, C/8]: bit k of byte (m, g) = (y[m, 8g + k] > 0), written by the forward apply."""
+    c = x.shape[1]
+    return torch.empty((x.numel() // c, c // 8), dtype=torch.uint8, device=x.device)
 
 
 class _BNActTrain(torch.autograd.Function):
@@ -70,8 +78,13 @@ class _BNActTrainPair(torch.autograd.Function):
 def _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches, momentum, eps, relu,
          pair=False, partials=None, links=(None, None)):
     ps, pq = partials if partials is not None else (None, None)
+    own_slot, res_slot = links
+    # block tail whose output feeds a native conv: the 1-bit ReLU mask that conv's dgrad epilogue
+    # reads instead of y (1/16 of y's bytes; ops/conv.py BNR)
+    mask = _relu_mask(x) if (own_slot is not None and relu and residual is not None) else None
     y, mean, invstd, coef = native().bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
-                                                  num_batches, float(momentum), float(eps), bool(relu), ps, pq)
+                                                  num_batches, float(momentum), float(eps), bool(relu), ps, pq,
+                                                  mask_out=mask)
     ctx.relu = bool(relu)
     ctx.has_res = residual is not None
     mask_from_x = ctx.relu and not ctx.has_res and not pair   # pair outputs always write dz
@@ -80,9 +93,10 @@ def _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches,
     if mask_from_x:
         # a native conv consuming y sums this BN's backward statistics in its dgrad epilogue
         y._dpt_bn_src = (x, mean, coef)
-    own_slot, res_slot = links
     ctx.res_slot = res_slot  # our residual input is the identity alias of an earlier block tail
     if own_slot is not None:
+        if mask is not None:
+            own_slot["mask"] = mask
         # block tail: the conv consuming y sums the statistics (and folds in the identity-path
         # gradient the next block's tail leaves in own_slot, see _bwd) in its dgrad epilogue
         y._dpt_bn_src = (x, mean, own_slot)
@@ -158,10 +172,12 @@ class _BN2AddReLUPair(torch.autograd.Function):
                                                ps, pq, False)
         _, mean2, invstd2, coef2 = C.bn_fwd_train(x2, None, w2, b2, rm2, rv2, nb2, float(momentum2), float(eps2),
                                                   False, ps2, pq2, False)
-        y = C.bn_apply_aff(x, x2, coef, coef2)
+        mask = _relu_mask(x) if own_slot is not None else None
+        y = C.bn_apply_aff(x, x2, coef, coef2, mask_out=mask)
         ctx.save_for_backward(x, x2, y, w, w2, mean, invstd, mean2, invstd2)
         ctx.set_materialize_grads(False)
         if own_slot is not None:
+            own_slot["mask"] = mask
             y._dpt_bn_src = (x, mean, own_slot, x2, mean2)
         return y, y.view_as(y)
 

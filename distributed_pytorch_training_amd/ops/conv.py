@@ -101,8 +101,9 @@ def _backward(ctx, dy):
             # (x, mean, slot, x2, mean2): the tail's identity path was a downsample BatchNorm
             # folded into it (ops/bn.py _BN2AddReLUPair) - also sum that BN's statistic
             x2, mean2 = (src[3], src[4]) if len(src) > 3 else (None, None)
+            # the tail's 1-bit ReLU mask (ops/bn.py) is read instead of its output x when present
             dx, p1, p2, p3 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, None, x, dres, wt, x2, mean2,
-                                                         wgrad_reduce=red)
+                                                         wgrad_reduce=red, bn_mask=src[2].get("mask"))
             _put_bnb(dx, p1, p2, dres.data_ptr(), p3 if x2 is not None else None)
         elif s == 1:
             dx = (native().conv_dgrad_flip(dy, w, p, wgrad_reduce=red)[0] if wt is None

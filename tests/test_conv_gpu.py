@@ -880,3 +880,34 @@ def test_wgrad_halo_matches_reference(cuda, shape, mode, dtype):
     torch.testing.assert_close(dw, ref, rtol=1e-3, atol=1e-4 * scale + 1e-3)
     torch.testing.assert_close(dw, base, rtol=1e-4, atol=1e-5 * scale + 1e-4)
     torch.testing.assert_close(dw16.float(), ref, rtol=1e-2, atol=1e-2 * scale)
+
+
+@pytest.mark.parametrize("shape", [(4, 28, 256, 64), (2, 7, 2048, 512)], ids=["grid", "splitk"])
+def test_tail_relu_bitmask_matches_output_mask(cuda, shape):
+    """Block tails write their ReLU mask as 1 bit per element (bn_fwd_train mask_out); the
+    consuming conv's backward-data epilogue (BNR, both the direct and the split-K epilogue)
+    reads it instead of the tail output y and must produce bit-identical dx / statistics."""
+    N, HW, C, Cout = shape
+    g = torch.Generator(device=cuda).manual_seed(77)
+
+    def t(*s, scale=1.0):
+        return (torch.randn(*s, device=cuda, generator=g) * scale).to(torch.bfloat16).contiguous(memory_format=CL)
+
+    x, res = t(N, C, HW, HW), t(N, C, HW, HW)
+    w = torch.rand(C, device=cuda, generator=g) + 0.5
+    b = torch.randn(C, device=cuda, generator=g) * 0.1
+    M = N * HW * HW
+    mask = torch.empty(M, C // 8, dtype=torch.uint8, device=cuda)
+    C_ = ops.native()
+    y, mean, _, _ = C_.bn_fwd_train(x, res, w, b, None, None, None, 0.1, 1e-5, True, mask_out=mask)
+    bits = (y.permute(0, 2, 3, 1).reshape(M, C // 8, 8) > 0).to(torch.int32)
+    ref = (bits << torch.arange(8, device=cuda, dtype=torch.int32)).sum(-1).to(torch.uint8)
+    assert torch.equal(mask, ref)
+    assert 0.2 < bits.float().mean().item() < 0.8
+    # backward-data of a 1x1 conv C -> Cout whose input is the tail output y
+    wc = t(Cout, C, 1, 1, scale=0.05)
+    dy, dres = t(N, Cout, HW, HW), t(N, C, HW, HW)
+    a = C_.conv_dgrad_bnstats(dy, wc, 0, x, mean, None, y, dres)
+    m = C_.conv_dgrad_bnstats(dy, wc, 0, x, mean, None, y, dres, bn_mask=mask)
+    for u, v in zip(a[:3], m[:3]):
+        assert torch.equal(u, v)
