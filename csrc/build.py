@@ -49,9 +49,15 @@ def _torch_paths():
     return tdir, incs, bool(torch._C._GLIBCXX_USE_CXX11_ABI)
 
 
-def output_path(asan: bool = False) -> Path:
+def output_path(asan: bool = False, variant: str = "") -> Path:
     name = "_C" + sysconfig.get_config_var("EXT_SUFFIX")
+    if variant:  # outside build/ (gpurun-ignored): the A/B library travels to the GPU box
+        return ROOT / "variants" / variant / name
     return (ROOT / "build" / "asan" / name) if asan else (PKG / name)
+
+
+def _variant_tag(defines) -> str:
+    return "_".join(d.replace("=", "-") for d in sorted(defines)) if defines else ""
 
 
 def _run(cmd):
@@ -71,8 +77,14 @@ def _stamp(src: Path, flags) -> str:
 
 
 def build(jobs: int = 4, force: bool = False, debug: bool = False, verbose: bool = False,
-          asan: bool = False) -> Path:
+          asan: bool = False, defines=()) -> Path:
+    """``defines`` (``NAME=VALUE`` strings): an A/B build of the kernel library with those
+    compile-time switches, written to variants/<tag>/ (never over the in-tree extension);
+    load it with ``DPT_NATIVE_LIB=<path>``."""
     tdir, tincs, cxx11 = _torch_paths()
+    variant = _variant_tag(defines)
+    kbuild = (ROOT / "build" / f"variant-{variant}" / "obj") if variant else BUILD
+    kbuild.mkdir(parents=True, exist_ok=True)
     BUILD.mkdir(parents=True, exist_ok=True)
     host_build = BUILD.parent / "native-asan" if asan else BUILD
     host_build.mkdir(parents=True, exist_ok=True)
@@ -82,7 +94,8 @@ def build(jobs: int = 4, force: bool = False, debug: bool = False, verbose: bool
     common_defs = ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DHIPBLAS_V2",
                    f"-D_GLIBCXX_USE_CXX11_ABI={int(cxx11)}"]
     hip_flags = [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-std=c++17", "-fPIC",
-                 *opt, "-Wall", "-Wno-unused-result", *common_defs, f"-I{CSRC}", f"-I{CSRC / 'kernels'}"]
+                 *opt, "-Wall", "-Wno-unused-result", *common_defs, *[f"-D{d}" for d in defines],
+                 f"-I{CSRC}", f"-I{CSRC / 'kernels'}"]
     cpp_flags = ["g++", "-std=c++17", "-fPIC", "-fvisibility=hidden", *host_opt, "-Wall", "-Wno-unused-variable", "-Wno-sign-compare",
                  *common_defs, "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C",
                  f"-I{CSRC}", *[f"-I{p}" for p in tincs], f"-I{ROCM / 'include'}", f"-I{py_inc}"]
@@ -95,8 +108,8 @@ def build(jobs: int = 4, force: bool = False, debug: bool = False, verbose: bool
 
     def compile_one(item):
         src, flags = item
-        obj = (BUILD if src.suffix == ".hip" else host_build) / (src.stem + (".hip.o" if src.suffix == ".hip" else ".o"))
-        stamp = BUILD / (obj.name + ".stamp")
+        obj = (kbuild if src.suffix == ".hip" else host_build) / (src.stem + (".hip.o" if src.suffix == ".hip" else ".o"))
+        stamp = obj.parent / (obj.name + ".stamp")
         key = _stamp(src, flags)
         if not force and obj.exists() and stamp.exists() and stamp.read_text() == key:
             return obj, False
@@ -110,7 +123,7 @@ def build(jobs: int = 4, force: bool = False, debug: bool = False, verbose: bool
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         results = list(ex.map(compile_one, jobs_list))
     objs = [o for o, _ in results]
-    out = output_path(asan)
+    out = output_path(asan, variant)
     out.parent.mkdir(parents=True, exist_ok=True)
     rebuilt = any(changed for _, changed in results)
     if rebuilt or force or not out.exists():
@@ -145,9 +158,12 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--asan", action="store_true", help="host code with AddressSanitizer -> build/asan/")
+    ap.add_argument("-D", "--define", action="append", default=[],
+                    help="NAME=VALUE kernel compile switch: an A/B build under variants/<tag>/")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args(argv)
-    out = build(jobs=min(a.jobs, 16), force=a.force, debug=a.debug, verbose=a.verbose, asan=a.asan)
+    out = build(jobs=min(a.jobs, 16), force=a.force, debug=a.debug, verbose=a.verbose, asan=a.asan,
+                defines=tuple(a.define))
     print(f"built {out}")
     return 0
 
