@@ -77,7 +77,7 @@ def parse(argv=None):
                          "per-bucket hipEvents on the comm stream (one event slot per step, read after "
                          "the window: no host sync inside it) -> BASELINE's second metric, %% of step "
                          "in all-reduce, plus exposed comm; 0 = off")
-    ap.add_argument("--comm", default="rccl", choices=["rccl", "host", "host-async"],
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "c10d", "host", "host-async"],
                     help="native reducer collective (host / host-async = gloo staging, debug only)")
     ap.add_argument("--rccl-channels", type=int, default=0,
                     help="NCCL_MIN/MAX_NCHANNELS for the framework's RCCL communicator (0 = RCCL default)")

@@ -7,6 +7,7 @@
 
 #include "kernels/kernels.h"
 #include "host_comm.h"
+#include "pg_comm.h"
 #include "rccl_comm.h"
 #include "watchdog.h"
 #include "reducer.h"
@@ -1251,6 +1252,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            })
       .def_property_readonly("async_mode", &dpt::HostBridgeComm::async_mode)
       .def_property_readonly("completed", &dpt::HostBridgeComm::completed);
+
+  // the Collective contract over a torch c10d group on device memory (RCCL through
+  // ProcessGroupNCCL): the framework communicator's fallback and A/B arm (csrc/pg_comm.h)
+  py::class_<dpt::ProcessGroupComm, dpt::Collective, std::shared_ptr<dpt::ProcessGroupComm>>(m, "ProcessGroupComm")
+      .def(py::init([](py::object pg, int dev) {
+             return std::make_shared<dpt::ProcessGroupComm>(pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>(), dev);
+           }),
+           py::arg("process_group"), py::arg("device"))
+      .def_property_readonly("backend", &dpt::ProcessGroupComm::backend);
 
   // Watchdog decision logic with an explicit clock (unit-tested with a fake clock)
   py::class_<dpt::WatchdogCore>(m, "WatchdogCore")

@@ -36,8 +36,8 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("DPT_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = sorted((CSRC / "kernels").glob("*.hip"))
-CPP_SOURCES = [CSRC / "watchdog.cpp", CSRC / "rccl_comm.cpp", CSRC / "host_comm.cpp", CSRC / "reducer.cpp",
-               CSRC / "bindings.cpp"]
+CPP_SOURCES = [CSRC / "watchdog.cpp", CSRC / "rccl_comm.cpp", CSRC / "host_comm.cpp", CSRC / "pg_comm.cpp",
+               CSRC / "reducer.cpp", CSRC / "bindings.cpp"]
 
 
 def _torch_paths():

@@ -112,11 +112,12 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--check-consistency", default=0, type=int,
                    help="debug: every N optimizer steps (and at every epoch end) verify that parameters "
                         "are identical across ranks")
-    g.add_argument("--comm", default="rccl", choices=["rccl", "host", "host-async"],
-                   help="device collective of the native reducer: rccl (RCCL over xGMI) or host (gloo "
-                        "through pinned host staging - lets several ranks share one GPU; debug only); "
-                        "host-async enqueues the host collective on the comm stream like RCCL, so "
-                        "backward overlaps it")
+    g.add_argument("--comm", default="rccl", choices=["rccl", "c10d", "host", "host-async"],
+                   help="device collective of the native reducer: rccl (the framework's own RCCL "
+                        "communicator over xGMI; falls back to c10d if it cannot be created), c10d "
+                        "(RCCL through torch's default process group), host (gloo through pinned host "
+                        "staging - lets several ranks share one GPU; debug only); host-async enqueues "
+                        "the host collective on the comm stream like RCCL, so backward overlaps it")
     g.add_argument("--rccl-channels", default=0, type=int,
                    help="RCCL channels (CTAs) of the framework's gradient communicator, set per "
                         "communicator through ncclConfig_t minCTAs/maxCTAs (0 = RCCL's topology default; "

@@ -8,6 +8,9 @@ on, one of
 * ``"rccl"`` - ``RcclComm`` (csrc/rccl_comm.cpp): RCCL over xGMI on a dedicated
   high-priority HIP stream, guarded by a watchdog thread (csrc/watchdog.cpp) that enforces
   ``--dist-timeout`` and polls ``ncclCommGetAsyncError`` (SURVEY.md §5.3);
+* ``"c10d"`` - ``ProcessGroupComm`` (csrc/pg_comm.cpp): the same contract served by torch's
+  default process group on device memory (RCCL through ProcessGroupNCCL, torch's watchdog).
+  The fallback when the framework communicator cannot be created, and its A/B arm;
 * ``"host"`` - ``HostBridgeComm`` (csrc/host_comm.cpp): the same device-pointer contract
   served by ``torch.distributed`` over gloo through pinned host staging.  Several ranks can
   then share one GPU and still run the whole multi-rank GPU data path (tests/
@@ -42,7 +45,7 @@ import torch.distributed as dist
 
 from .. import ops
 
-COMM_KINDS = ("rccl", "host", "host-async")
+COMM_KINDS = ("rccl", "c10d", "host", "host-async")
 _HOST_GROUP = None
 _ASYNC_GROUP = None
 
@@ -93,6 +96,8 @@ def make_comm(device: torch.device, rank: int, world_size: int, kind: str = "rcc
         if world_size > 1:
             _host_group()
         return C.HostBridgeComm(_host_all_reduce, _host_broadcast, rank, world_size, dev)
+    if kind == "c10d":
+        return _pg_comm(C, dev)
     n_ch = max(0, int(rccl_channels or 0))
     if world_size > 1:
         if not dist.is_initialized():
@@ -102,10 +107,37 @@ def make_comm(device: torch.device, rank: int, world_size: int, kind: str = "rcc
         uid = box[0]
     else:
         uid = C.RcclComm.new_unique_id()
-    comm = C.RcclComm(uid, rank, world_size, dev, n_ch, n_ch)
+    try:
+        comm = C.RcclComm(uid, rank, world_size, dev, n_ch, n_ch)
+        ok = 1
+    except RuntimeError as e:
+        comm, ok = None, 0
+        err = e
+    if world_size > 1:
+        # every rank takes the same branch (a communicator some ranks built and others did not
+        # would hang the first collective)
+        flag = torch.tensor([ok], dtype=torch.int32, device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = int(flag.item())
+    if not ok:
+        if comm is not None:
+            comm.destroy()
+        import warnings
+        warnings.warn(f"framework RCCL communicator unavailable on some rank "
+                      f"({err if comm is None else 'another rank'}); falling back to --comm c10d")
+        return _pg_comm(C, dev)
     if timeout_s and timeout_s > 0 and world_size > 1:
         comm.enable_watchdog(float(timeout_s), 0.5, float(exit_grace_s))
     return comm
+
+
+def _pg_comm(C, dev: int):
+    """ProcessGroupComm over the default group: a device backend (nccl = RCCL) is required."""
+    if not dist.is_initialized():
+        raise RuntimeError("--comm c10d needs an initialised torch.distributed process group")
+    if dist.get_backend() != "nccl":
+        raise RuntimeError(f"--comm c10d needs the nccl (RCCL) backend, not {dist.get_backend()!r}")
+    return C.ProcessGroupComm(dist.group.WORLD, dev)
 
 
 def broadcast_(tensor: torch.Tensor, comm, src: int = 0) -> None:

@@ -106,17 +106,28 @@ def test_reducer_single_rank_checks_buckets(cuda):
 
 
 @pytest.mark.parametrize("wire", [0, 1])
-def test_reducer_rccl_path_single_rank(cuda, wire, monkeypatch):
+@pytest.mark.parametrize("kind", ["rccl", "c10d"])
+def test_reducer_rccl_path_single_rank(cuda, wire, kind, monkeypatch):
     """Exercise ncclAllReduce (+ bf16 pack/unpack) through the C++ reducer on one GPU: a
     1-rank all-reduce is an identity, so gradients must come out unchanged (fp32 wire) or
-    bf16-rounded (bf16 wire)."""
+    bf16-rounded (bf16 wire).  ``rccl``: the framework communicator; ``c10d``: the same
+    collectives through torch's nccl (RCCL) process group (csrc/pg_comm.cpp)."""
+    import socket
     import subprocess
     import sys
     import textwrap
 
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
     code = textwrap.dedent(f"""
         import torch
+        import torch.distributed as dist
         from distributed_pytorch_training_amd import ops
+        if "{kind}" == "c10d":
+            dist.init_process_group("nccl", init_method="tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                    device_id=torch.device("cuda:0"))
         from distributed_pytorch_training_amd.parallel.bucketing import plan_for_arena
         from distributed_pytorch_training_amd.parallel.comm import make_comm
         from distributed_pytorch_training_amd.parallel.flat import FlatArena
@@ -131,7 +142,8 @@ def test_reducer_rccl_path_single_rank(cuda, wire, monkeypatch):
             p.grad = None
         arena = FlatArena(list(reversed(list(model.parameters()))))
         plan = plan_for_arena(arena, bucket_cap_mb=0.02, first_bucket_mb=0.001)
-        comm = make_comm(dev, 0, 1)
+        comm = make_comm(dev, 0, 1, kind="{kind}")
+        assert comm.kind == "{kind}"
         fi = torch.zeros(1, device=dev)
         wire_buf = torch.zeros(arena.numel, dtype=torch.bfloat16, device=dev) if {wire} else torch.empty(0)
         red = ops.native().Reducer(arena.params, arena.grad_views, arena.grad_flat, plan.offsets, plan.numels,
@@ -146,6 +158,10 @@ def test_reducer_rccl_path_single_rank(cuda, wire, monkeypatch):
         comm.all_reduce(t, True)
         torch.cuda.synchronize()
         assert torch.equal(t, torch.arange(16, dtype=torch.float32, device=dev))
+        assert comm.ops >= plan.num_buckets, (comm.ops, plan.num_buckets)
+        comm.destroy()
+        if dist.is_initialized():
+            dist.destroy_process_group()
         print("ok")
     """)
     env = dict(__import__("os").environ, DPT_FORCE_COLLECTIVES="1")
