@@ -2,12 +2,13 @@
 batch 256, synthetic data): one Trainer, arms interleaved over rounds (cdna_hip_programming.md
 §5.4 rule 24 - cross-process runs add variance that looks like a kernel property).
 
-    python bench/ab_step.py --arm base= --arm h256=conv_set_halo256:1 --rounds 4 --steps 10
+    python bench/ab_step.py --arm base= --arm hb3=conv_set_halo:3 --reset conv_set_halo:1 --rounds 4
 
 An arm is NAME=setter:value[,setter:value...] (setters of the native module, e.g.
-conv_set_halo256, conv_set_halo, conv_set_splitk, conv_set_variant); an empty list is the
-default configuration.  Every setter an arm touches is reset to its value in the first arm
-that names it, or to the value given by --reset, before each other arm runs.
+conv_set_halo, conv_set_splitk, conv_set_variant, or a dotted Python module attribute such as
+distributed_pytorch_training_amd.ops.conv.CONCURRENT_WGRAD_MAX_PIXELS); an empty list is the
+default configuration.  --reset setter:value pairs are applied before every arm (give one for
+each setter an arm changes, so the next arm starts from the default).
 """
 from __future__ import annotations
 
@@ -68,11 +69,21 @@ def main(argv=None):
     arms = [parse_arm(s) for s in a.arm]
     resets = [parse_arm("r=" + r)[1][0] for r in a.reset]
 
+    import importlib
+
+    def set_one(fn, v):
+        # "module.path.ATTR" sets a Python module attribute, anything else a native setter
+        if "." in fn:
+            mod, _, attr = fn.rpartition(".")
+            setattr(importlib.import_module(mod), attr, v)
+        else:
+            getattr(C, fn)(v)
+
     def apply(sets):
         for fn, v in resets:
-            getattr(C, fn)(v)
+            set_one(fn, v)
         for fn, v in sets:
-            getattr(C, fn)(v)
+            set_one(fn, v)
 
     def run(n):
         for i in range(n):
