@@ -105,7 +105,12 @@ def build_parser() -> argparse.ArgumentParser:
                    help="micro-batches per optimizer step (all-reduce only on the last)")
     g.add_argument("--save-every", default=0, type=int,
                    help="write a checkpoint every N epochs (0 = never, the reference default)")
-    g.add_argument("--resume", default=None, type=str, help="checkpoint file to resume from")
+    g.add_argument("--resume", default=None, type=str,
+                   help="checkpoint file to resume from, or 'auto': output-dir/checkpoint.pt when it "
+                        "exists (a job restarted by torchrun --max-restarts picks up its last epoch)")
+    g.add_argument("--inject-fault", default=None, type=str, metavar="EPOCH:RANK",
+                   help="testing: rank RANK exits (status 13) at the start of 0-based epoch EPOCH, once "
+                        "per output dir (a marker file there keeps the restarted job from failing again)")
     g.add_argument("--no-val", dest="validate", action="store_false", help="skip validation")
     g.add_argument("--dist-timeout", default=1800, type=int,
                    help="process-group timeout in seconds")

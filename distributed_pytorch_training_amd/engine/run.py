@@ -53,8 +53,14 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                       log=lambda s: print(s, flush=True))
 
     start_epoch = 0
-    if args.resume:
-        start_epoch = load_checkpoint(args.resume, trainer)
+    resume = args.resume
+    if resume == "auto":   # elastic restart: the last checkpoint of this output dir, if any
+        ck = Path(args.output_dir) / "checkpoint.pt"
+        resume = str(ck) if ck.exists() else None
+    if resume:
+        start_epoch = load_checkpoint(resume, trainer)
+        if rank == 0:
+            print(f"Resumed from {resume} at epoch {start_epoch}", flush=True)
 
     metrics_path = Path(args.output_dir) / "metrics_rank0.csv"
     perf_path = Path(args.output_dir) / "metrics_perf_rank0.csv"
@@ -90,7 +96,15 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
 
 def _epochs(args, trainer, train_loader, val_loader, train_sampler, start_epoch, rank, world_size,
             metrics_path, perf_path) -> None:
+    fault = None
+    if args.inject_fault:
+        fe, fr = (int(v) for v in args.inject_fault.split(":"))
+        fault = (fe, fr, Path(args.output_dir) / f".fault_injected_{fe}_{fr}")
     for epoch in range(start_epoch, args.epochs):
+        if fault is not None and fault[:2] == (epoch, rank) and not fault[2].exists():
+            fault[2].touch()   # once: the restarted job runs through
+            print(f"rank {rank}: injected fault at epoch {epoch}", flush=True)
+            os._exit(13)
         st = trainer.train_one_epoch(epoch, train_loader, train_sampler)
         if args.validate:
             vs = trainer.validate(val_loader)
@@ -110,6 +124,11 @@ def _epochs(args, trainer, train_loader, val_loader, train_sampler, start_epoch,
                     f.write(f"{epoch+1},{w['step']},{w['seconds']:.6f},{w['samples']},{w['throughput']:.2f}\n")
             if args.save_every and (epoch + 1) % args.save_every == 0:
                 save_checkpoint(str(Path(args.output_dir) / "checkpoint.pt"), trainer, epoch + 1, args)
+        if args.save_every and (epoch + 1) % args.save_every == 0 and world_size > 1:
+            # nobody starts the next epoch before the checkpoint is on disk: a failure from here on
+            # restarts (--resume auto) from this epoch, never from an older one
+            import torch.distributed as dist
+            dist.barrier()
 
     if trainer.timeline.enabled and rank == 0:
         out = args.profile_out or str(Path(args.output_dir) / "sync_profile.json")

@@ -78,3 +78,30 @@ def test_gloo_world_size_2(tmp_path):
                launcher=launcher)
     assert "Using device: cpu, world_size=2, amp=False" in out
     assert sum(1 for l in out.splitlines() if EPOCH_RE.match(l)) == 1
+
+
+@pytest.mark.slow
+def test_restart_after_rank_failure_resumes_from_checkpoint(tmp_path):
+    """SURVEY.md §5.3/§5.4 together: rank 1 of a gloo world-size-2 job dies at the start of epoch 3
+    (``--inject-fault``); the job fails non-zero after the epoch-2 checkpoint; the relaunched job
+    (what ``torchrun --max-restarts`` does, launched again here: this container's gloo cannot
+    reconnect inside one torchrun agent) continues with ``--resume auto`` from that checkpoint,
+    completes with exit 0 and runs epoch 3 exactly once."""
+    launcher = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                "--master-addr", "127.0.0.1", "--master-port", "29541"]
+    args = COMMON + ["--epochs", "3", "--output-dir", str(tmp_path), "--save-every", "1", "--resume", "auto",
+                     "--inject-fault", "2:1", "--dist-timeout", "60"]
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    first = subprocess.run(launcher + [os.path.join(ROOT, "train_ddp.py")] + args, capture_output=True, text=True,
+                           env=env, timeout=600, cwd=ROOT)
+    assert first.returncode != 0, first.stdout + first.stderr
+    assert "rank 1: injected fault at epoch 2" in first.stdout
+    assert torch.load(tmp_path / "checkpoint.pt", weights_only=True)["epoch"] == 2
+    out = _run(args, launcher=launcher[:-1] + ["29542"])
+    assert "Resumed from" in out and "at epoch 2" in out, out
+    epochs = [l.split("]")[0] for l in (first.stdout + out).splitlines() if EPOCH_RE.match(l)]
+    assert epochs == ["[Epoch 1/3", "[Epoch 2/3", "[Epoch 3/3"], epochs
+    assert torch.load(tmp_path / "checkpoint.pt", weights_only=True)["epoch"] == 3
+    csv = (tmp_path / "metrics_rank0.csv").read_text().splitlines()
+    assert [r.split(",")[0] for r in csv[1:]] == ["1", "2", "3"], csv
