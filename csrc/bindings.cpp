@@ -1161,6 +1161,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_set_variant", &dpt::conv_set_variant, py::arg("variant"));
   m.def("conv_set_big", &dpt::conv_set_big, py::arg("on"));
   m.def("conv_set_halo", &dpt::conv_set_halo, py::arg("on"));
+  m.def("conv_set_wgrad_target", &dpt::conv_set_wgrad_target, py::arg("blocks"));
   m.def("conv_set_wgrad_halo", &dpt::conv_set_wgrad_halo, py::arg("mode"));
   m.def("conv_fwd_splits", [](int64_t M, int Cout, int64_t K, bool graph) {
           return dpt::conv_fwd_splits_for(M, Cout, K, graph);

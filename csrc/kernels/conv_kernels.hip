@@ -2393,6 +2393,20 @@ static FastDiv make_fastdiv(uint32_t d) {
   return f;
 }
 
+// Block target of the split-K backward-weight plan.  Measured per ResNet-50 shape at batch 256
+// (bench/wgrad_target_sweep.py, profiles/wgrad_target_sweep_r3.md): 1x1 / stride-1 convs (one
+// tap, streaming both operands once) want ~512 blocks - fewer fp32 partial tiles to write and
+// reduce; convs with taps or a stride want more blocks to hide their K loop, 768 on the long
+// (>= 3136 K-step) reductions and 640 on the shorter ones.  Step total 3.65 -> 3.49 ms.
+// conv_set_wgrad_target(n > 0): n blocks for every shape (the sweep); 0: this policy.
+static int g_wgrad_target = 0;
+void conv_set_wgrad_target(int blocks) { g_wgrad_target = blocks; }
+static int wgrad_target(int R, int S, int stride, int steps) {
+  if (g_wgrad_target > 0) return g_wgrad_target;
+  if (R * S == 1 && stride == 1) return 512;
+  return steps >= 3136 ? 768 : 640;
+}
+
 ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad, int Ho,
                               int Wo) {
   ConvWgradPlan pl;
@@ -2433,7 +2447,7 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
   // (BMW x BNW x 4 B, written once and read once by the reduce) then costs < 1/8 of the
   // operand bytes it streams.  Small problems that cannot fill the chip that way (ResNet-18 on
   // 32x32 images: 2-128 K-steps) are K-loop-latency-bound instead: down to 2 K-steps per split.
-  int splits = (768 + tiles - 1) / tiles;
+  int splits = (wgrad_target(R, S, stride, steps) + tiles - 1) / tiles;
   const int min_steps = (int64_t)tiles * (steps / 32) >= 512 ? 32 : 2;
   splits = std::max(1, std::min(splits, steps / min_steps));
   pl.steps_per_split = (steps + splits - 1) / splits;

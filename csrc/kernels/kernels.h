@@ -151,6 +151,7 @@ int conv_m_tiles(int64_t M);
 void conv_set_variant(int v);
 void conv_set_big(int on);  // 8-wave 256-row tiles where conv_big_auto picks them (default off)
 void conv_set_halo(int on);  // 3x3 / stride-1 halo K loop (default on, DPT_CONV_HALO)
+void conv_set_wgrad_target(int blocks);  // split-K backward-weight block target (0 = policy)
 // Ho/Wo > 0: explicit output size (padding applied on top/left only beyond what it needs)
 // ws: split-K workspace of conv_fwd_splits(M, Cout, R*S*C) * M * Cout floats when that is > 1
 // (nullptr: never split).  Small tile grids split the K loop over blocks (fp32 partials).
