@@ -2423,7 +2423,7 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
     pl.bnw = pl.halo >= 3 ? 64 : 128;
     const int tiles = (Cout / 64) * 3 * (C / pl.bnw);
     const int steps = (int)(((int64_t)N * H * (W + 2) + 63) / 64);
-    const int target = pl.bnw == 128 ? 512 : 768;
+    const int target = g_wgrad_target > 0 ? g_wgrad_target : pl.bnw == 128 ? 512 : 768;
     int splits = (target + tiles - 1) / tiles;
     const int min_steps = (int64_t)tiles * (steps / 32) >= 512 ? 32 : 2;
     splits = std::max(1, std::min(splits, steps / min_steps));
