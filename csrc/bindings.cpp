@@ -1156,6 +1156,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pad"), py::arg("fp32_out"));
   m.def("im2col", &im2col, py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("Kp"));
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("heads"), py::arg("scale"));
+  m.def("attn_set_bwd_split", &dpt::attn_set_bwd_split, py::arg("on"));
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("grad_output"), py::arg("lse"),
         py::arg("heads"), py::arg("scale"));
   m.def("conv_set_variant", &dpt::conv_set_variant, py::arg("variant"));

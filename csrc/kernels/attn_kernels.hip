@@ -133,30 +133,50 @@ __global__ __launch_bounds__(NT * 64) void attn_fwd_kernel(const uint16_t* __res
   }
 }
 
-template <int NT>
-__global__ __launch_bounds__(NT * 64) void attn_bwd_kernel(const uint16_t* __restrict__ qkv,
-                                                           const uint16_t* __restrict__ out,
-                                                           const uint16_t* __restrict__ dout,
-                                                           const float* __restrict__ lse2,
-                                                           uint16_t* __restrict__ dqkv, int S, int H,
-                                                           float scale_log2, float scale) {
+// PHASE 0: both phases in one workgroup (four LDS images, one workgroup per CU); 1: dK / dV only
+// (Q and dO images); 2: dQ only (K and V images) - two launches at half the LDS each, so two
+// workgroups share a CU (attn_set_bwd_split; phase 1 reads K / V rows and phase 2 Q / dO rows as
+// register fragments straight from global memory)
+#ifndef DPT_ATTN_P1_WAVES  // min waves per SIMD of the split phase-1 kernel (4 = two workgroups per CU)
+#define DPT_ATTN_P1_WAVES 2
+#endif
+template <int NT, int PHASE = 0>
+__global__ __launch_bounds__(NT * 64, PHASE == 1 ? DPT_ATTN_P1_WAVES : PHASE == 2 ? 4 : 1) void attn_bwd_kernel(const uint16_t* __restrict__ qkv,
+                                                                        const uint16_t* __restrict__ out,
+                                                                        const uint16_t* __restrict__ dout,
+                                                                        const float* __restrict__ lse2,
+                                                                        uint16_t* __restrict__ dqkv, int S, int H,
+                                                                        float scale_log2, float scale) {
   using namespace attn;
   constexpr int SP = NT * 32, NTH = NT * 64;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[4 * SP * RB + 2 * SP * 4];
+  constexpr int NIMG = PHASE ? 2 : 4;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NIMG * SP * RB + 2 * SP * 4];
+  // phase-1 images: Q, dO; phase-2 images: K, V (PHASE 0: all four)
   unsigned char* qimg = lds;
-  unsigned char* kimg = lds + SP * RB;
-  unsigned char* vimg = lds + 2 * SP * RB;
-  unsigned char* oimg = lds + 3 * SP * RB;  // dO
-  float* ls = reinterpret_cast<float*>(lds + 4 * SP * RB);
+  unsigned char* oimg = lds + SP * RB;  // dO
+  unsigned char* kimg = lds + (PHASE == 2 ? 0 : 2) * SP * RB;
+  unsigned char* vimg = lds + (PHASE == 2 ? 1 : 3) * SP * RB;
+  float* ls = reinterpret_cast<float*>(lds + NIMG * SP * RB);
   float* dd = ls + SP;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int bh = blockIdx.x, b = bh / H, hh = bh - b * H;
   const int64_t ld = 3LL * H * D, ldo = (int64_t)H * D;
   const uint16_t* base = qkv + (int64_t)b * S * ld;
-  attn_stage(qimg, base + (int64_t)hh * D, ld, S, SP, tid, NTH);
-  attn_stage(kimg, base + (int64_t)(H + hh) * D, ld, S, SP, tid, NTH);
-  attn_stage(vimg, base + (int64_t)(2 * H + hh) * D, ld, S, SP, tid, NTH);
-  attn_stage(oimg, dout + (int64_t)b * S * ldo + hh * D, ldo, S, SP, tid, NTH);
+  const uint16_t* obase = dout + (int64_t)b * S * ldo + hh * D;
+  if (PHASE != 2) {
+    attn_stage(qimg, base + (int64_t)hh * D, ld, S, SP, tid, NTH);
+    attn_stage(oimg, obase, ldo, S, SP, tid, NTH);
+  }
+  if (PHASE != 1) {
+    attn_stage(kimg, base + (int64_t)(H + hh) * D, ld, S, SP, tid, NTH);
+    attn_stage(vimg, base + (int64_t)(2 * H + hh) * D, ld, S, SP, tid, NTH);
+  }
+  // row fragment (16 B) of a [S, ld] bf16 matrix straight from global memory (rows >= S: zero)
+  auto gfrag = [&](const uint16_t* src, int64_t ldm, int row, int ch) -> bf16x8_t {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row < S) v = *reinterpret_cast<const uint4*>(src + (int64_t)row * ldm + ch * 8);
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
   for (int t = tid; t < SP; t += NTH) {  // D[q] = sum_d dO * O (fp32), lse2 (+inf for padding)
     float acc = 0.f;
     if (t < S) {
@@ -181,7 +201,7 @@ __global__ __launch_bounds__(NT * 64) void attn_bwd_kernel(const uint16_t* __res
   const int r = lane & 31, h = lane >> 5;
 
   // ---- phase 1: this wave's 32 keys against every query tile -> dK, dV ----
-  {
+  if (PHASE != 2) {
     const int k0 = w * 32, key = k0 + r;
     f32x16_t dv[2], dk[2];
 #pragma unroll
@@ -191,8 +211,13 @@ __global__ __launch_bounds__(NT * 64) void attn_bwd_kernel(const uint16_t* __res
     bf16x8_t kf[4], vf[4];  // B operands: K[key][d], V[key][d] rows
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      kf[s] = row_frag<RB>(kimg, key, 2 * s + h);
-      vf[s] = row_frag<RB>(vimg, key, 2 * s + h);
+      if (PHASE == 1) {
+        kf[s] = gfrag(base + (int64_t)(H + hh) * D, ld, key, 2 * s + h);
+        vf[s] = gfrag(base + (int64_t)(2 * H + hh) * D, ld, key, 2 * s + h);
+      } else {
+        kf[s] = row_frag<RB>(kimg, key, 2 * s + h);
+        vf[s] = row_frag<RB>(vimg, key, 2 * s + h);
+      }
     }
     for (int qt = 0; qt < NT; ++qt) {
       f32x16_t sc, dp;
@@ -235,13 +260,18 @@ __global__ __launch_bounds__(NT * 64) void attn_bwd_kernel(const uint16_t* __res
   }
 
   // ---- phase 2: this wave's 32 queries against every key tile -> dQ ----
-  {
+  if (PHASE != 1) {
     const int q = w * 32 + r;
     bf16x8_t qf[4], of[4];  // B operands of S^T = K Q^T and dP^T = V dO^T
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      qf[s] = row_frag<RB>(qimg, q, 2 * s + h);
-      of[s] = row_frag<RB>(oimg, q, 2 * s + h);
+      if (PHASE == 2) {
+        qf[s] = gfrag(base + (int64_t)hh * D, ld, q, 2 * s + h);
+        of[s] = gfrag(obase, ldo, q, 2 * s + h);
+      } else {
+        qf[s] = row_frag<RB>(qimg, q, 2 * s + h);
+        of[s] = row_frag<RB>(oimg, q, 2 * s + h);
+      }
     }
     const float lq = ls[q], dq0 = dd[q];
     f32x16_t dq[2];
@@ -313,11 +343,22 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* ctx, float* lse2, int B, int
   DPT_ATTN_DISPATCH(nt, attn_fwd_kernel, qkv, ctx, lse2, S, H, sl2)
 }
 
+// Split by default for 7 query / key tiles (ViT-B/16, 197 tokens): 214-224 -> 194-202 us per
+// call at batch 128 x 12 heads, bitwise identical (bench/attn_bwd_ab.py).  The phase-2 kernel
+// holds two workgroups per CU (128 VGPRs); phase 1 stays at 168 VGPRs (at 128 it spills: 262 us).
+static int g_attn_bwd_split = 1;
+void attn_set_bwd_split(int on) { g_attn_bwd_split = on; }
+
 void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse2,
                      uint16_t* dqkv, int B, int S, int H, float scale, hipStream_t st) {
   const int nt = (S + 31) / 32;
   const dim3 grid((unsigned)(B * H));
   const float sl2 = scale * 1.4426950408889634f;
+  if (g_attn_bwd_split && nt == 7) {  // ViT-B/16 (197 tokens)
+    hipLaunchKernelGGL((attn_bwd_kernel<7, 1>), grid, dim3(448), 0, st, qkv, out, dout, lse2, dqkv, S, H, sl2, scale);
+    hipLaunchKernelGGL((attn_bwd_kernel<7, 2>), grid, dim3(448), 0, st, qkv, out, dout, lse2, dqkv, S, H, sl2, scale);
+    return;
+  }
   DPT_ATTN_DISPATCH(nt, attn_bwd_kernel, qkv, out, dout, lse2, dqkv, S, H, sl2, scale)
 }
 

@@ -263,6 +263,7 @@ void launch_conv_wt_flip(const uint16_t* w, uint16_t* wt, int Cout, int R, int S
 // lse2 [B*H][attn_lse_stride(S)] fp32 (log2-sum-exp of the scaled scores), dqkv like qkv.
 bool attn_supported(int S, int Dh);
 int attn_lse_stride(int S);
+void attn_set_bwd_split(int on);  // attention backward as two phase kernels (A/B)
 void launch_attn_fwd(const uint16_t* qkv, uint16_t* ctx, float* lse2, int B, int S, int H, float scale,
                      hipStream_t s);
 void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse2,

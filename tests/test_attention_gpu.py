@@ -47,3 +47,22 @@ def test_vit_uses_fused_attention(cuda):
     finally:
         fa.ENABLED = True
     torch.testing.assert_close(y1.float(), y2.float(), rtol=5e-2, atol=5e-2)
+
+
+def test_attention_bwd_phase_split_is_bitwise_identical(cuda):
+    """The backward as two phase kernels (dK/dV over Q and dO images, dQ over K and V images,
+    the ViT-B/16 default) computes exactly what the one two-phase kernel does."""
+    C = ops.native()
+    g = torch.Generator(device=cuda).manual_seed(5)
+    B, S, H = 3, 197, 4
+    qkv = (torch.randn(B, S, 3 * H * 64, device=cuda, generator=g) * 1.5).to(torch.bfloat16)
+    dout = torch.randn(B, S, H * 64, device=cuda, generator=g).to(torch.bfloat16)
+    out, lse = C.attn_fwd(qkv, H, 0.125)
+    try:
+        C.attn_set_bwd_split(0)
+        one = C.attn_bwd(qkv, out, dout, lse, H, 0.125)
+        C.attn_set_bwd_split(1)
+        split = C.attn_bwd(qkv, out, dout, lse, H, 0.125)
+    finally:
+        C.attn_set_bwd_split(1)
+    assert torch.equal(one, split)
