@@ -210,7 +210,10 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   constexpr int STAGE = A_BYTES + HB * B_BYTES;
   constexpr int C_STRIDE = BN * 2 + 16;  // epilogue image row stride (bytes), padded
   constexpr int RED = 2 * WM * BN * 4;   // BN-statistics cross-wave scratch
-  constexpr int LDS_MAIN = STAGES * STAGE;
+  // HALO: one zeroed 128-byte row after the K-loop buffers - a fragment row in the padding
+  // reads it instead of being zeroed in registers (4 v_cndmask per fragment and K-step)
+  constexpr int ZROW = STAGES * STAGE;
+  constexpr int LDS_MAIN = STAGES * STAGE + (HALO ? kRowBytes : 0);
   // HALF: the 128-row, 4-wave LDS epilogue stages its output image 64 rows at a time, so the
   // epilogue (17 KiB + statistics scratch) fits under the 32 KiB K-loop buffer of a 128 x 128
   // tile: 5 resident blocks per CU instead of 4 (36 KiB), i.e. 25 % more bytes in flight for a
@@ -380,6 +383,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
         fwo[i] = 0;
       }
     }
+    if (tid < kRowBytes / 16) *reinterpret_cast<uint4*>(lds + ZROW + tid * 16) = uint4{0u, 0u, 0u, 0u};
     const int64_t npix = (int64_t)p.N * p.H * p.W;
     const unsigned char* hb = lds;            // halo strip [HROWS][128 B]
     unsigned char* bb = lds + A_BYTES;        // B [BN][128 B]
@@ -404,20 +408,22 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
       }
     };
     auto mma_h = [&](int r, int sx) {
-      bool ok[MI];
+      // row base per fragment (the zero row for padding); the swizzle term (hrow >> 1) & 7 is
+      // the same for every i (rows 32 apart), so one chunk offset per kk serves all of them
+      int abase[MI];
+      const int hrow0 = wm * (MI * 32) + lr + sx;
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
-        ok[i] = ((unsigned)(fho[i] + r - 1) < (unsigned)p.H) & ((unsigned)(fwo[i] + sx - 1) < (unsigned)p.W);
+      for (int i = 0; i < MI; ++i) {
+        const bool ok = ((unsigned)(fho[i] + r - 1) < (unsigned)p.H) & ((unsigned)(fwo[i] + sx - 1) < (unsigned)p.W);
+        abase[i] = ok ? (hrow0 + i * 32) * kRowBytes : ZROW;
+      }
 #pragma unroll
       for (int kk = 0; kk < BK / 16; ++kk) {
-        const int ch = kk * 2 + lh;
+        const int coff = conv::swz(hrow0, kk * 2 + lh) * 16;
         bf16x8_t fa[MI], fb[NI];
 #pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const int hrow = wm * (MI * 32) + i * 32 + lr + sx;
-          fa[i] = *reinterpret_cast<const bf16x8_t*>(hb + hrow * kRowBytes + conv::swz(hrow, ch) * 16);
-          if (!ok[i]) fa[i] = bf16x8_t{};
-        }
+        for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8_t*>(hb + (abase[i] | coff));
+        const int ch = kk * 2 + lh;
         const unsigned char* bs = bb + (HB == 3 ? sx * B_BYTES : 0);
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
