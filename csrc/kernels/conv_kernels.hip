@@ -1179,7 +1179,13 @@ struct ConvWgradArgs {
 
 // NT = 256: 2 x 2 waves; NT = 512 (256 x 256 tiles): 2 x 4 waves of 128 x 64 - twice the MFMA
 // work per staged byte, one block per CU.
-template <int BMW, int BNW, int STAGES, bool F16 = false, int NT = conv::kThreads>
+// DIR: the 1x1 / stride-1 / pad-0 case (p.direct) as a compile-time path - the x row of a K-step
+// is its dy row, so a lane keeps one offset per load and no bounds state (rows past M and the
+// taps past R*S of a narrow tile read the descriptor's zero fill or land in columns that are
+// not stored): 44 fewer VALU per K-step, 120 VGPRs instead of 128 + spills, 1-7 % per call
+// (profiles/wgrad_direct_ab_r3.md; asking the freed registers for 5 waves/SIMD spills the
+// fragment addresses into the K loop: 2x slower).
+template <int BMW, int BNW, int STAGES, bool F16 = false, int NT = conv::kThreads, bool DIR = false>
 __global__ __launch_bounds__(NT, (NT == conv::kThreads && BNW <= 128) ? DPT_WGRAD_WAVES : 2) void conv_wgrad_kernel(ConvWgradArgs p) {
   using namespace conv;
   constexpr int NW = NT / 64;
@@ -1256,7 +1262,7 @@ __global__ __launch_bounds__(NT, (NT == conv::kThreads && BNW <= 128) ? DPT_WGRA
       delta = (bdr[i] * p.W + bds[i]) * p.C + (bchk[i] * 8 - sub * p.C);
       if (t >= p.R * p.S) delta = 0;
     }
-    if (p.direct) {
+    if (DIR || p.direct) {
       bh[i] = 0; bw[i] = 0;
       boff[i] = m * p.C + ci0 + delta;
     } else {
@@ -1292,6 +1298,12 @@ __global__ __launch_bounds__(NT, (NT == conv::kThreads && BNW <= 128) ? DPT_WGRA
     }
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i) {
+      if constexpr (DIR) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(b + (wid * B_INSTR + i) * 1024),
+                                                 16, (uint32_t)boff[i] * 2u, 0, 0, 0);
+        boff[i] += dp_step;
+        continue;
+      }
       // bitwise, not short-circuit: no exec-mask branches around the select
       const bool ok = (bm + (brow[i] - brow[0]) < p.M) &
                       ((p.direct != 0) | (((unsigned)(bh[i] + bdr[i]) < (unsigned)p.H) &
@@ -2060,6 +2072,10 @@ static bool maybe_split(ConvFwdArgs& a, float* ws, bool stats, bool bnb, bool bn
 template <int BMW, int BNW, int STAGES>
 static void wgrad_launch(dim3 grid, dim3 block, hipStream_t s, const ConvWgradArgs& a) {
   if constexpr (STAGES == 1) {
+    if (a.direct && !a.f16) {
+      hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, STAGES, false, conv::kThreads, true>), grid, block, 0, s, a);
+      return;
+    }
     if (a.f16) {
       hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, STAGES, true>), grid, block, 0, s, a);
       return;
