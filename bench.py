@@ -97,6 +97,7 @@ def parse(argv=None):
 ENV_PREFIXES = ("DPT_", "NCCL_", "RCCL_", "MIOPEN_", "HIP_", "HSA_", "AMD_", "GPU_MAX_HW_QUEUES",
                 "PYTORCH_TUNABLEOP", "TORCH_NCCL", "OMP_NUM_THREADS")
 CHILD_MARK = "DPT_BENCH_LAUNCHER"
+rccl_log = None  # distributed_pytorch_training_amd.utils.rccl_log, imported by the ranks only
 
 
 def env_in_effect() -> dict:
@@ -110,11 +111,43 @@ def _free_port() -> int:
 
 
 def _visible_gpus() -> int:
-    """Device count WITHOUT initialising the GPU runtime in this (launcher) process."""
+    """GPU count WITHOUT touching the GPU runtime in this (launcher) process.
+
+    A launcher must not initialise HIP before it starts its ranks, and ``torch.cuda.device_count()``
+    can fall back to a HIP call (``_cuda_getDeviceCount``) when amdsmi discovery fails.  So a
+    throwaway child process counts (whatever HIP state it creates dies with it; it sees the same
+    device cgroup and visibility variables the ranks will).  If the child cannot run, the KFD
+    topology in sysfs (GPU nodes have a non-zero ``gpu_id``) bounded by a ``ROCR_/HIP_/
+    CUDA_VISIBLE_DEVICES`` list is the fallback."""
     try:
-        return int(torch.cuda.device_count())
-    except Exception:
-        return 0
+        r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode == 0 and r.stdout.strip():
+            return int(r.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, OSError):
+        pass
+    n = _kfd_gpu_count() or 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([t for t in v.split(",") if t.strip() != ""]))
+    return n
+
+
+def _kfd_gpu_count(root: str = "/sys/class/kfd/kfd/topology/nodes"):
+    """GPU nodes in the KFD topology, or None when it cannot be read."""
+    try:
+        names = os.listdir(root)
+    except OSError:
+        return None
+    n = 0
+    for d in names:
+        try:
+            with open(os.path.join(root, d, "gpu_id")) as f:
+                n += int(f.read().strip() or 0) != 0
+        except (OSError, ValueError):
+            continue
+    return n
 
 
 def launch_ranks(a, argv, grace_s: float = 30.0) -> int:
@@ -189,6 +222,61 @@ def _red_dev(device):
     return "cpu" if dist.is_initialized() and dist.get_backend() == "gloo" else device
 
 
+def _rccl_log_prefix() -> str:
+    import tempfile
+    return os.path.join(tempfile.gettempdir(), f"dpt_bench_rccl_{os.environ.get('MASTER_PORT', '0')}_"
+                                               f"r{os.environ.get('RANK', '0')}")
+
+
+def verify_job(trainer, device, ws: int, rank: int, ms_per_step: float) -> dict:
+    """Self-verification of an N > 1 record: after the timed window
+    * parameters bit-identical on every rank (``Trainer.check_consistency``: fp64 checksum
+      MIN == MAX across ranks);
+    * one all-reduce of ``rank + 1``-filled data through the framework communicator (the
+      device collective the gradients used; the process group where there is none) equals
+      ``N (N + 1) / 2`` exactly;
+    * every rank's own ms/step (the headline is the max);
+    * the channel count RCCL actually opened for the framework communicator (its init log).
+    ``ok`` is the AND over ranks of the checks; ``main`` exits non-zero when it is false."""
+    if dist.get_backend() == "fake":      # every collective is a no-op: nothing to verify
+        return {"skipped": "fake process group", "ok": None, "selftest_ok": None,
+                "rccl_channels_opened": None}
+    out = {}
+    try:
+        trainer.check_consistency()
+        params_ok = True
+    except RuntimeError as e:
+        params_ok = False
+        out["consistency_error"] = str(e)[:300]
+    comm = trainer.ddp.comm if trainer.ddp is not None else None
+    if comm is not None:
+        t = torch.full((4096,), float(rank + 1), dtype=torch.float32, device=device)
+        comm.all_reduce(t, True)
+        torch.cuda.synchronize(device)
+        comm.check()
+        via = comm.kind
+    else:
+        t = torch.full((4096,), float(rank + 1), dtype=torch.float32, device=_red_dev(device))
+        dist.all_reduce(t)
+        via = "process-group:" + dist.get_backend()
+    want = ws * (ws + 1) / 2
+    self_ok = bool((t == want).all().item())
+    flag = torch.tensor([int(params_ok and self_ok)], dtype=torch.int32, device=_red_dev(device))
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    per_rank = [None] * ws
+    dist.all_gather_object(per_rank, round(ms_per_step, 3))
+    opened = None
+    if comm is not None and hasattr(comm, "handle") and os.environ.get("NCCL_DEBUG_FILE", "").startswith(
+            _rccl_log_prefix()):
+        opened = rccl_log.opened_channels(int(comm.handle), _rccl_log_prefix())
+    gathered = [None] * ws
+    dist.all_gather_object(gathered, opened)
+    out.update({"ok": bool(flag.item()), "params_consistent": params_ok, "selftest_ok": self_ok,
+                "selftest_via": via, "selftest_expected": want, "per_rank_ms_per_step": per_rank,
+                "rccl_channels_opened": gathered})
+    return out
+
+
 def _rccl_version():
     try:
         from distributed_pytorch_training_amd import ops
@@ -248,6 +336,8 @@ def main(argv=None) -> int:
     elif int(env_ws) != a.gpus:
         print(f"error: --gpus {a.gpus} but the launcher started WORLD_SIZE={env_ws} ranks", file=sys.stderr)
         return 2
+    global rccl_log
+    from distributed_pytorch_training_amd.utils import rccl_log
     launcher = ("fake" if a.fake_pg else os.environ.get(CHILD_MARK) or
                 ("torchrun" if env_ws is not None else "none"))
     from distributed_pytorch_training_amd.data import SyntheticLoader
@@ -273,11 +363,17 @@ def main(argv=None) -> int:
         dist.init_process_group("fake", store=FakeStore(), rank=0, world_size=a.gpus)
         info = DistInfo(0, a.gpus, 0, "fake", torch.device("cpu"))
     else:
-        if (env_ws is not None and int(env_ws) > 1 and _visible_gpus() > 0
-                and _visible_gpus() < int(os.environ.get("LOCAL_WORLD_SIZE", env_ws))):
+        # a rank may touch the GPU runtime (it is about to use it): count directly
+        ngpu = torch.cuda.device_count() if env_ws is not None and int(env_ws) > 1 else 0
+        if ngpu > 0 and ngpu < int(os.environ.get("LOCAL_WORLD_SIZE", env_ws)):
             print(f"error: {os.environ.get('LOCAL_WORLD_SIZE', env_ws)} local ranks but only "
-                  f"{_visible_gpus()} GPU(s) visible", file=sys.stderr)
+                  f"{ngpu} GPU(s) visible", file=sys.stderr)
             return 2
+        if (env_ws is not None and int(env_ws) > 1 and a.impl == "native" and a.comm == "rccl"
+                and "NCCL_DEBUG" not in os.environ):
+            # RCCL's init log, to a file (stdout stays one JSON line): the channel count the
+            # framework communicator actually opened is read back from it after the run
+            os.environ.update(rccl_log.debug_env(_rccl_log_prefix()))
         info = init_distributed("auto")
     gemm_db = setup_tunableop() if (a.impl == "native" and info.device.type == "cuda") else False
     rank, ws, device = info.rank, info.world_size, info.device
@@ -314,13 +410,14 @@ def main(argv=None) -> int:
     t0 = time.time()
     run(a.steps)
     fence()
-    dt = time.time() - t0
+    dt = own_dt = time.time() - t0
     if ws > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=_red_dev(device))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms = 1e3 * dt / max(a.steps, 1)
     value = a.batch_size * ws * a.steps / dt
+    verify = verify_job(trainer, device, ws, rank, 1e3 * own_dt / max(a.steps, 1)) if ws > 1 else None
 
     prof, prof_window = {}, None
     collective = ws > 1 and a.impl == "native" and trainer.ddp is not None and trainer.ddp.comm is not None
@@ -394,9 +491,14 @@ def main(argv=None) -> int:
                    "bucket_cap_mb": a.bucket_cap_mb, "first_bucket_mb": a.first_bucket_mb,
                    "last_bucket_mb": a.last_bucket_mb,
                    "grad_dtype": a.grad_dtype,
+                   # requested per-communicator bound (None = RCCL's own choice) and what RCCL
+                   # opened per rank (its init log; None where it could not be read)
                    "rccl_channels": (int(comm.max_ctas) or None) if comm is not None and hasattr(comm, "max_ctas")
                                     else None,
+                   "rccl_channels_opened": verify["rccl_channels_opened"] if verify else None,
+                   "selftest_ok": verify["selftest_ok"] if verify else None,
                    "rccl_version": _rccl_version()}
+    rec["verify"] = verify
     rec["config"]["launcher"] = launcher
     rec["config"]["env"] = env_in_effect()
     if rank == 0:
@@ -410,6 +512,9 @@ def main(argv=None) -> int:
     trainer.close()
     if ws > 1:
         dist.destroy_process_group()
+    if verify is not None and verify["ok"] is False:
+        print(f"bench: rank {rank}: self-verification FAILED: {json.dumps(verify)}", file=sys.stderr)
+        return 3
     return 0
 
 

@@ -1,0 +1,182 @@
+"""hipGraph replay vs eager on the reference's own default workload.
+
+Configuration = what ``train_ddp.py --dataset synthetic --image-size 32 --num-classes 10`` runs:
+ResNet-18, batch 128, fp32 (no --amp), native engine, channels_last, MIOpen convolutions in
+``cudnn.benchmark`` mode, SGD 0.1 / 0.9 / 5e-4, seed 42.
+
+Modes:
+* ``teacher``: after warmup + capture, every step k starts from ONE state S_k; the replayed
+  step and an eager step are both run from S_k (state restored in place between them) and
+  their parameters / arena gradients / BN buffers compared per tensor; the run continues
+  from the eager result.  Prints per-step relative differences and the worst tensors.
+* ``free``: two trainers from the same init, one replaying, one eager, N free-running steps
+  on the 4-batch synthetic pool; prints both loss curves (window means).
+* ``startup``: wall-clock marks around the warmup steps, the capture and the first replays.
+
+    python bench/graph_parity.py --mode teacher --steps 20
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from distributed_pytorch_training_amd.config import parse_args  # noqa: E402
+from distributed_pytorch_training_amd.data import get_dataloaders  # noqa: E402
+from distributed_pytorch_training_amd.engine.trainer import Trainer  # noqa: E402
+from distributed_pytorch_training_amd.models import build_model  # noqa: E402
+from distributed_pytorch_training_amd.utils.dist import set_seed  # noqa: E402
+from distributed_pytorch_training_amd.utils.env import setup_miopen_env, setup_tunableop  # noqa: E402
+
+
+def _state_tensors(tr):
+    """Every tensor a training step reads and writes (restorable in place)."""
+    out = {"param": tr.ddp.arena.param_flat, "step": tr.optimizer._step, "metrics": tr.metrics}
+    mb = getattr(tr.optimizer, "momentum_buffer", None)
+    if mb is not None:
+        out["momentum"] = mb
+    for n, b in tr.module.named_buffers():
+        out["buf:" + n] = b
+    if tr.ddp.shadow_flat is not None:
+        out["shadow"] = tr.ddp.shadow_flat
+    for k in ("scale_tensor", "growth_tracker", "found_inf"):
+        t = getattr(tr.scaler, k, None)
+        if isinstance(t, torch.Tensor):
+            out["scaler:" + k] = t
+    return out
+
+
+def _snap(tr):
+    return {k: v.detach().clone() for k, v in _state_tensors(tr).items()}
+
+
+def _restore(tr, snap):
+    with torch.no_grad():
+        for k, v in _state_tensors(tr).items():
+            v.copy_(snap[k])
+
+
+def make(argv, dev):
+    args = parse_args(argv)
+    set_seed(args.seed, 0)
+    model = build_model(args.model, args.num_classes, dev, image_size=args.image_size,
+                        channels_last=args.channels_last)
+    return args, Trainer(model, args, 0, 1, dev, log=print)
+
+
+def teacher(steps: int, extra):
+    dev = torch.device("cuda:0")
+    args, tr = make(["--dataset", "synthetic", "--image-size", "32", "--num-classes", "10", *extra], dev)
+    train, _, _ = get_dataloaders(args, 0, 1, dev)
+    assert tr.graphed is not None, "graph replay is not enabled for this configuration"
+    G = tr.graphed
+    it = iter(train)
+    for _ in range(G.warmup + 1):          # warmup + capture (+ first replay)
+        x, y = next(it)
+        tr.train_step(x, y)
+    torch.cuda.synchronize()
+    assert G.graph is not None, f"capture failed (failed={G.failed})"
+    names = [n for n in tr.ddp.arena.names] if hasattr(tr.ddp.arena, "names") else None
+    worst = []
+    rows = []
+    for k in range(steps):
+        x, y = next(it)
+        s0 = _snap(tr)
+        tr.train_step(x, y)                 # replay
+        torch.cuda.synchronize()
+        sg = _snap(tr)
+        gg = tr.ddp.arena.grad_flat.detach().clone()
+        _restore(tr, s0)
+        with G._on_stream():
+            tr._native_step(x, y)           # eager, same stream, same state
+        torch.cuda.synchronize()
+        se = _snap(tr)
+        ge = tr.ddp.arena.grad_flat.detach().clone()
+        upd = (se["param"] - s0["param"]).double().norm().item()
+        dp = (sg["param"] - se["param"]).double().norm().item()
+        dg = (gg - ge).double().norm().item() / max(ge.double().norm().item(), 1e-30)
+        dbuf = max(((sg[n] - se[n]).double().abs().max().item() if sg[n].is_floating_point()
+                    else float((sg[n] != se[n]).any())) for n in se if n.startswith("buf:"))
+        row = {"step": k, "rel_param_vs_update": dp / max(upd, 1e-30),
+               "rel_param_l2": dp / se["param"].double().norm().item(), "rel_grad": dg,
+               "max_buf_diff": dbuf, "metrics_g": sg["metrics"].tolist(), "metrics_e": se["metrics"].tolist()}
+        # per-parameter gradient differences
+        per = []
+        for i, (gv_g, gv_e) in enumerate(zip(tr.ddp.arena.views(gg), tr.ddp.arena.views(ge))):
+            r = (gv_g - gv_e).double().norm().item() / max(gv_e.double().norm().item(), 1e-30)
+            per.append((r, names[i] if names else str(i)))
+        per.sort(reverse=True)
+        row["worst_grads"] = per[:5]
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    return rows
+
+
+def free(steps: int, extra, pool_dtype=None):
+    dev = torch.device("cuda:0")
+    curves = {}
+    for mode in ("--cuda-graph", "--no-cuda-graph"):
+        args, tr = make(["--dataset", "synthetic", "--image-size", "32", "--num-classes", "10", mode, *extra], dev)
+        train, _, _ = get_dataloaders(args, 0, 1, dev)
+        losses = []
+        it = iter(train)
+        for k in range(steps):
+            try:
+                x, y = next(it)
+            except StopIteration:
+                it = iter(train)
+                x, y = next(it)
+            _, loss = tr.train_step(x, y)
+            losses.append(loss.detach().clone())
+        torch.cuda.synchronize()
+        curves[mode] = [float(v) for v in torch.stack(losses).cpu()]
+        del tr
+    w = 25
+    for i in range(0, steps, w):
+        a = sum(curves["--cuda-graph"][i:i + w]) / len(curves["--cuda-graph"][i:i + w])
+        b = sum(curves["--no-cuda-graph"][i:i + w]) / len(curves["--no-cuda-graph"][i:i + w])
+        print(f"steps {i:4d}-{i + w - 1:4d}: graph {a:.4f}  eager {b:.4f}", flush=True)
+    return curves
+
+
+def startup(extra):
+    dev = torch.device("cuda:0")
+    t0 = time.time()
+    args, tr = make(["--dataset", "synthetic", "--image-size", "32", "--num-classes", "10", *extra], dev)
+    train, _, _ = get_dataloaders(args, 0, 1, dev)
+    torch.cuda.synchronize()
+    print(f"build {time.time() - t0:.2f}s", flush=True)
+    it = iter(train)
+    for k in range(12):
+        x, y = next(it)
+        t = time.time()
+        tr.train_step(x, y)
+        torch.cuda.synchronize()
+        g = tr.graphed
+        print(f"call {k}: {1e3 * (time.time() - t):9.1f} ms  graph={'yes' if g and g.graph else 'no'}", flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", choices=["teacher", "free", "startup"], default="teacher")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--extra", default="", help="extra train_ddp flags, space separated")
+    a = ap.parse_args()
+    setup_miopen_env()
+    torch.cuda.set_device(0)
+    setup_tunableop()
+    torch.backends.cudnn.benchmark = True
+    extra = a.extra.split() if a.extra else []
+    {"teacher": lambda: teacher(a.steps, extra), "free": lambda: free(a.steps, extra),
+     "startup": lambda: startup(extra)}[a.mode]()
+
+
+if __name__ == "__main__":
+    main()

@@ -1227,10 +1227,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            "test hook: enqueue a wall-clock busy-wait on the communicator (or current) stream");
 
   py::class_<dpt::RcclComm, dpt::Collective, std::shared_ptr<dpt::RcclComm>>(m, "RcclComm")
-      .def(py::init<const std::string&, int, int, int, int, int>(), py::arg("unique_id"), py::arg("rank"),
-           py::arg("world_size"), py::arg("device"), py::arg("min_ctas") = 0, py::arg("max_ctas") = 0)
+      .def(py::init<const std::string&, int, int, int, int, int, double>(), py::arg("unique_id"), py::arg("rank"),
+           py::arg("world_size"), py::arg("device"), py::arg("min_ctas") = 0, py::arg("max_ctas") = 0,
+           py::arg("init_timeout_s") = 0.0,
+           // a peer's RCCL init may need this process's other threads; never hold the GIL there
+           py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("min_ctas", &dpt::RcclComm::min_ctas)
       .def_property_readonly("max_ctas", &dpt::RcclComm::max_ctas)
+      .def_property_readonly("handle", &dpt::RcclComm::handle)
       .def("inject_async_error", &dpt::RcclComm::inject_async_error, py::arg("message"))
       .def_static("new_unique_id", []() { return py::bytes(dpt::RcclComm::new_unique_id()); })
       .def("enable_watchdog", &dpt::RcclComm::enable_watchdog, py::arg("timeout_s"), py::arg("poll_s") = 0.5,

@@ -72,6 +72,27 @@ void HostBridgeComm::destroy() {
   }
   for (auto& kv : staging_) hipHostFree(kv.second);
   staging_.clear();
+  graph_staging_.clear();
+  graph_jobs_.clear();  // the device is drained above: no replay can still reference them
+}
+
+// Release the cached pinned buffers no captured graph references.  Only called outside capture;
+// drains the device first (a host function may still be reading a buffer), without the GIL so a
+// gloo peer that needs this process's Python side can still reach its matching collective.
+void HostBridgeComm::trim_staging() {
+  {
+    std::unique_ptr<py::gil_scoped_release> rel;
+    if (PyGILState_Check()) rel = std::make_unique<py::gil_scoped_release>();
+    DPT_HIP_THROW(hipDeviceSynchronize());
+  }
+  for (auto it = staging_.begin(); it != staging_.end();) {
+    if (graph_staging_.count(it->second)) {
+      ++it;
+      continue;
+    }
+    hipHostFree(it->second);
+    it = staging_.erase(it);
+  }
 }
 
 void HostBridgeComm::check() const {
@@ -107,7 +128,8 @@ void HostBridgeComm::call(int op, const at::Tensor& h, int root) {
 // Runs on HIP's host-function thread, between the D2H and the H2D copy of the stream.  No GIL,
 // no HIP call: a blocking c10d collective on the pinned staging buffer.
 void HostBridgeComm::host_fn(void* arg) {
-  std::unique_ptr<Job> j(static_cast<Job*>(arg));
+  Job* j = static_cast<Job*>(arg);
+  std::unique_ptr<Job> owned(j->persistent ? nullptr : j);  // graph jobs are reused per replay
   HostBridgeComm* self = j->self;
   try {
     if (self->aborted_.load()) throw std::runtime_error("aborted before the collective ran");
@@ -135,7 +157,13 @@ void HostBridgeComm::run(int op, void* ptr, size_t count, WireType t, int root, 
   // nullptr is the null stream (torch's default current stream), a real stream to order behind,
   // not "use the comm stream": substituting stream_ would race the caller's work.
   hipStream_t s = stream;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  DPT_HIP_THROW(hipStreamIsCapturing(s, &cap));
+  const bool capturing = cap != hipStreamCaptureStatusNone;
   if (!async_) {
+    // the synchronous bridge blocks on the stream, which a capture forbids: fail the capture
+    // loudly (the graph engine falls back to eager) instead of recording a broken graph
+    if (capturing) throw std::runtime_error("HostBridgeComm(host): a synchronous host collective cannot be captured");
     at::Tensor h = stage_in(ptr, count, t, s);
     call(op, h, root);
     stage_out(ptr, count, t, s);
@@ -143,13 +171,28 @@ void HostBridgeComm::run(int op, void* ptr, size_t count, WireType t, int root, 
   }
   if (world_size_ == 1) return;  // identity; stream order is all a caller can observe
   const size_t bytes = count * wire_bytes(t);
-  void*& buf = staging_[{ptr, bytes}];  // one pinned buffer per (tensor, size): reuse is stream-ordered
-  if (buf == nullptr) DPT_HIP_THROW(hipHostMalloc(&buf, bytes, hipHostMallocDefault));
+  const StagingKey key{ptr, bytes, s};
+  if (!capturing && staging_.size() >= kMaxStaging && !staging_.count(key)) trim_staging();
+  void*& buf = staging_[key];  // one pinned buffer per (tensor, size, stream): reuse is stream-ordered
+  if (buf == nullptr) {
+    // pinned allocation is not a stream operation a graph can record: warm up before capturing
+    if (capturing) {
+      staging_.erase(key);
+      throw std::runtime_error("HostBridgeComm(host-async): no staging buffer for this collective yet; "
+                               "run it eagerly once before capturing");
+    }
+    DPT_HIP_THROW(hipHostMalloc(&buf, bytes, hipHostMallocDefault));
+  }
   DPT_HIP_THROW(hipMemcpyAsync(buf, ptr, bytes, hipMemcpyDeviceToHost, s));
-  auto* job = new Job{this, op, root, buf, count, t};
+  Job* job = new Job{this, op, root, buf, count, t, capturing};
+  if (capturing) {
+    graph_jobs_.emplace_back(job);  // owned here; every replay's host node reads it
+    graph_staging_.insert(buf);
+  }
   hipError_t e = hipLaunchHostFunc(s, &HostBridgeComm::host_fn, job);
   if (e != hipSuccess) {
-    delete job;
+    if (capturing) graph_jobs_.pop_back();
+    else delete job;
     DPT_HIP_THROW(e);
   }
   DPT_HIP_THROW(hipMemcpyAsync(ptr, buf, bytes, hipMemcpyHostToDevice, s));

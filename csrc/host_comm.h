@@ -30,6 +30,10 @@
 
 #include <atomic>
 #include <map>
+#include <memory>
+#include <set>
+#include <tuple>
+#include <vector>
 #include <mutex>
 #include <string>
 
@@ -66,7 +70,14 @@ class HostBridgeComm : public Collective {
     void* host;
     size_t count;
     WireType t;
+    // Enqueued while a hipGraph was being captured: the host node runs once per REPLAY, so the
+    // job outlives every call (owned by graph_jobs_, freed at destroy()), never by host_fn.
+    bool persistent;
   };
+  using StagingKey = std::tuple<void*, size_t, hipStream_t>;
+  // Bound on cached pinned staging buffers; past it the idle ones are released (drain first).
+  static constexpr size_t kMaxStaging = 256;
+  void trim_staging();
   static void host_fn(void* job);
   // D2H of `bytes` from `ptr` behind `stream`, returns the host view as a CPU tensor.
   at::Tensor stage_in(void* ptr, size_t count, WireType t, hipStream_t stream);
@@ -81,7 +92,12 @@ class HostBridgeComm : public Collective {
   int rank_, world_size_, device_;
   std::atomic<bool> aborted_{false};
   bool async_ = false;
-  std::map<std::pair<void*, size_t>, void*> staging_;  // async: (device ptr, bytes) -> pinned buffer
+  // async: (device ptr, bytes, stream) -> pinned buffer.  Keyed by stream too: the caching
+  // allocator may hand one address to two streams, and two in-flight operations must never
+  // share a staging buffer.  Buffers a captured graph references are never released.
+  std::map<StagingKey, void*> staging_;
+  std::set<void*> graph_staging_;
+  std::vector<std::unique_ptr<Job>> graph_jobs_;
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;  // async mode: the collective the host function runs
   std::atomic<uint64_t> completed_{0};
   mutable std::mutex err_mu_;

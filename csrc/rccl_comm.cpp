@@ -1,8 +1,12 @@
 #include "rccl_comm.h"
 
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 namespace dpt {
 
@@ -39,7 +43,7 @@ std::string RcclComm::new_unique_id() {
 }
 
 RcclComm::RcclComm(const std::string& unique_id, int rank, int world_size, int device, int min_ctas,
-                   int max_ctas)
+                   int max_ctas, double init_timeout_s)
     : rank_(rank), world_size_(world_size), device_(device), min_ctas_(min_ctas), max_ctas_(max_ctas) {
   if (unique_id.size() != sizeof(ncclUniqueId))
     throw std::invalid_argument("RcclComm: unique id must be " + std::to_string(sizeof(ncclUniqueId)) + " bytes");
@@ -50,17 +54,55 @@ RcclComm::RcclComm(const std::string& unique_id, int rank, int world_size, int d
   int lo = 0, hi = 0;
   DPT_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   DPT_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
-  if (min_ctas > 0 || max_ctas > 0) {
-    // Only fields every config version since 2.14 carries are set; size/magic/version come
-    // from the header's initializer and the library copies what it knows.
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    if (min_ctas > 0) cfg.minCTAs = min_ctas;
-    if (max_ctas > 0) cfg.maxCTAs = max_ctas;
-    cfg.blocking = 1;
-    DPT_RCCL_CHECK(ncclCommInitRankConfig(&comm_, world_size, id, rank, &cfg));
-  } else {
-    DPT_RCCL_CHECK(ncclCommInitRank(&comm_, world_size, id, rank));
+  // RCCL's init is collective and blocking: a peer that failed inside its own init leaves this
+  // rank blocked in bootstrap forever.  Run it on a helper thread and give up after
+  // init_timeout_s (the caller then agrees on a fallback with its peers, parallel/comm.py).  A
+  // thread that is still blocked is detached: its communicator is never used, and the process
+  // normally exits or falls back to torch's communicator.
+  auto st = std::make_shared<InitState>();
+  std::thread worker([st, id, rank, world_size, device, min_ctas, max_ctas] {
+    ncclComm_t c = nullptr;
+    ncclResult_t r = ncclSuccess;
+    if (hipSetDevice(device) != hipSuccess) {
+      r = ncclUnhandledCudaError;
+    } else if (min_ctas > 0 || max_ctas > 0) {
+      // Only fields every config version since 2.14 carries are set; size/magic/version come
+      // from the header's initializer and the library copies what it knows.
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+      if (min_ctas > 0) cfg.minCTAs = min_ctas;
+      if (max_ctas > 0) cfg.maxCTAs = max_ctas;
+      cfg.blocking = 1;
+      r = ncclCommInitRankConfig(&c, world_size, id, rank, &cfg);
+    } else {
+      r = ncclCommInitRank(&c, world_size, id, rank);
+    }
+    std::lock_guard<std::mutex> lk(st->mu);
+    st->comm = c;
+    st->result = r;
+    st->done = true;
+    st->cv.notify_all();
+  });
+  std::unique_lock<std::mutex> lk(st->mu);
+  const bool finished = init_timeout_s <= 0
+      ? (st->cv.wait(lk, [&] { return st->done; }), true)
+      : st->cv.wait_for(lk, std::chrono::duration<double>(init_timeout_s), [&] { return st->done; });
+  if (!finished) {
+    lk.unlock();
+    worker.detach();
+    hipStreamDestroy(stream_);
+    stream_ = nullptr;
+    throw std::runtime_error("RcclComm: ncclCommInitRank did not complete within " +
+                             std::to_string(init_timeout_s) + " s (a peer failed or never joined)");
   }
+  lk.unlock();
+  worker.join();
+  if (st->result != ncclSuccess) {
+    hipStreamDestroy(stream_);
+    stream_ = nullptr;
+    throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(st->result) +
+                             " in communicator init (rank " + std::to_string(rank) + ")");
+  }
+  comm_ = st->comm;
 }
 
 RcclComm::~RcclComm() { destroy(); }

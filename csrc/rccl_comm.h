@@ -17,6 +17,7 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -32,8 +33,10 @@ class RcclComm : public Collective {
   // ncclCommInitRankConfig (ncclConfig_t.minCTAs / maxCTAs) - only this communicator is
   // affected, unlike the process-wide NCCL_MIN/MAX_NCHANNELS environment, which RCCL reads
   // once per process (torch's own communicator may already have read it).  0 = RCCL default.
+  // `init_timeout_s` > 0 bounds the (collective, blocking) ncclCommInitRank: past it the
+  // constructor throws instead of waiting forever for a peer that failed.
   RcclComm(const std::string& unique_id, int rank, int world_size, int device, int min_ctas = 0,
-           int max_ctas = 0);
+           int max_ctas = 0, double init_timeout_s = 0.0);
   ~RcclComm() override;
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
@@ -53,6 +56,9 @@ class RcclComm : public Collective {
   std::string kind() const override { return "rccl"; }
   void track(hipStream_t stream) override;
   int min_ctas() const { return min_ctas_; }
+  // The ncclComm_t as an integer: matches the "comm 0x..." of RCCL's NCCL_DEBUG=INFO init lines,
+  // which is how bench.py reads the channel count this communicator actually opened.
+  uintptr_t handle() const { return reinterpret_cast<uintptr_t>(comm_); }
   int max_ctas() const { return max_ctas_; }
 
   // Start the watchdog: a collective older than `timeout_s` (or an RCCL async error) aborts
@@ -66,6 +72,13 @@ class RcclComm : public Collective {
   void inject_async_error(const std::string& msg);
 
  private:
+  struct InitState {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    ncclComm_t comm = nullptr;
+    ncclResult_t result = ncclSuccess;
+  };
   int min_ctas_ = 0, max_ctas_ = 0;
   std::string injected_error_;
   mutable std::mutex inject_mu_;

@@ -108,9 +108,6 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--resume", default=None, type=str,
                    help="checkpoint file to resume from, or 'auto': output-dir/checkpoint.pt when it "
                         "exists (a job restarted by torchrun --max-restarts picks up its last epoch)")
-    g.add_argument("--inject-fault", default=None, type=str, metavar="EPOCH:RANK",
-                   help="testing: rank RANK exits (status 13) at the start of 0-based epoch EPOCH, once "
-                        "per output dir (a marker file there keeps the restarted job from failing again)")
     g.add_argument("--no-val", dest="validate", action="store_false", help="skip validation")
     g.add_argument("--dist-timeout", default=1800, type=int,
                    help="process-group timeout in seconds")
@@ -137,8 +134,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="native impl: time each step from after the loader yields to after a host sync "
                         "(the reference's step-line definition, train_ddp.py:196,224) instead of the "
                         "default sync-to-sync window, which has no per-step host sync")
-    g.add_argument("--fault-inject", default=None, type=str, metavar="RANK:STEP",
-                   help="testing: rank RANK exits abruptly (os._exit(17)) before global step STEP")
+    g.add_argument("--fault-inject", default=None, type=str, metavar="rank=R,step=S|rank=R,epoch=E",
+                   help="testing: rank R exits abruptly with status 17 before global optimizer step S, or at "
+                        "the start of 0-based epoch E; once per output dir (a marker file there lets a "
+                        "restarted job run through)")
     g.add_argument("--cuda-graph", dest="cuda_graph", action="store_true", default=None,
                    help="capture the training step in a hipGraph (static shapes, native impl); "
                         "default: on when the step is launch-bound (per-GPU batch x pixels <= 2^18, "
@@ -171,4 +170,6 @@ def finalize(args: argparse.Namespace) -> argparse.Namespace:
     args.betas = tuple(b)
     if args.grad_accum < 1:
         raise ValueError("--grad-accum must be >= 1")
+    from .utils.fault import FaultSpec
+    FaultSpec.parse(args.fault_inject)   # reject a malformed spec at start-up, not mid-run
     return args

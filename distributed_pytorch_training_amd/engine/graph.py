@@ -26,7 +26,16 @@ Rules (checked or documented):
 
 Default (``--cuda-graph`` not given): on for launch-bound steps only - per-GPU batch x
 pixels <= ``AUTO_GRAPH_MAX_PIXELS`` (the reference's own ResNet-18 / 32x32 / batch 128 is
-131k; ResNet-50 / 224 / 256 is 12.8M and GPU-bound), ``--no-cuda-graph`` turns it off.
+131k; ResNet-50 / 224 / 256 is 12.8M and GPU-bound) - and only at world size 1: replayed RCCL
+collectives have run on no multi-GPU node yet, so N > 1 replays only when asked for
+(``--cuda-graph``).  ``--no-cuda-graph`` turns it off.
+
+Multi-rank capture: every rank must take the same path (a rank replaying while another runs
+eagerly still pairs its collectives, but the steps would no longer be the same program), so
+after its capture each rank contributes "captured OK" to a MIN all-reduce over the control
+plane and all fall back to eager together if any failed.  The synchronous host bridge
+(``--comm host``) cannot be captured (it blocks on the stream) and is refused up front; the
+asynchronous one records its host collectives as graph host nodes (csrc/host_comm.cpp).
 """
 from __future__ import annotations
 
@@ -39,11 +48,13 @@ import torch
 AUTO_GRAPH_MAX_PIXELS = 1 << 18
 
 
-def auto_enabled(args, device) -> bool:
+def auto_enabled(args, device, world_size: int = 1) -> bool:
     """The ``--cuda-graph`` default: replay when the step is launch-bound."""
     if torch.device(device).type != "cuda" or getattr(args, "impl", "native") != "native":
         return False
     if getattr(args, "profile_sync", False) or getattr(args, "grad_accum", 1) != 1:
+        return False
+    if world_size > 1:
         return False
     return int(args.batch_size) * int(args.image_size) ** 2 <= AUTO_GRAPH_MAX_PIXELS
 
@@ -111,14 +122,38 @@ class GraphedStep:
         self.static_x = x.clone()
         self.static_y = y.clone()
         g = torch.cuda.CUDAGraph()
-        try:
-            with torch.cuda.graph(g, stream=self.stream):
-                out, loss = t._native_step(self.static_x, self.static_y)
-            t.global_step -= 1          # the captured call counted a step that did not run
-            torch.cuda.synchronize()
-        except Exception as e:  # capture is an optimisation: never fatal
-            warnings.warn(f"hipGraph capture failed, running eagerly: {e!r}")
+        comm = t.ddp.comm if t.ddp is not None else None
+        ok = True
+        if comm is not None and comm.kind == "host":
+            warnings.warn("hipGraph replay disabled: the synchronous host bridge (--comm host) blocks on "
+                          "the stream and cannot be captured; use --comm host-async")
+            ok = False
+        else:
+            try:
+                with torch.cuda.graph(g, stream=self.stream):
+                    out, loss = t._native_step(self.static_x, self.static_y)
+                t.global_step -= 1          # the captured call counted a step that did not run
+                torch.cuda.synchronize()
+            except Exception as e:  # capture is an optimisation: never fatal
+                warnings.warn(f"hipGraph capture failed, running eagerly: {e!r}")
+                ok = False
+                torch.cuda.synchronize()
+        if t.world_size > 1 and not agree(ok, t.device):
+            if ok:
+                warnings.warn("hipGraph capture failed on another rank: every rank runs eagerly")
+            ok = False
+        if not ok:
             self.failed = True
-            torch.cuda.synchronize()
             return
         self.graph, self.out, self.loss = g, out, loss
+
+
+def agree(ok: bool, device) -> bool:
+    """All ranks' capture outcomes, MIN-reduced over the control-plane process group."""
+    import torch.distributed as dist
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return ok
+    on = device if dist.get_backend() == "nccl" else "cpu"
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=on)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item())

@@ -22,6 +22,7 @@ from ..models import build_model
 from ..utils.checkpoint import load_checkpoint, save_checkpoint
 from ..utils.dist import cleanup_distributed, init_distributed, set_seed
 from ..utils.env import setup_miopen_env, setup_tunableop
+from ..utils.fault import FaultSpec
 from .trainer import Trainer, format_epoch_line
 
 CSV_HEADER = "epoch,train_loss,train_acc,val_loss,val_acc,epoch_time_seconds\n"
@@ -96,15 +97,10 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
 
 def _epochs(args, trainer, train_loader, val_loader, train_sampler, start_epoch, rank, world_size,
             metrics_path, perf_path) -> None:
-    fault = None
-    if args.inject_fault:
-        fe, fr = (int(v) for v in args.inject_fault.split(":"))
-        fault = (fe, fr, Path(args.output_dir) / f".fault_injected_{fe}_{fr}")
+    fault = FaultSpec.parse(args.fault_inject)
     for epoch in range(start_epoch, args.epochs):
-        if fault is not None and fault[:2] == (epoch, rank) and not fault[2].exists():
-            fault[2].touch()   # once: the restarted job runs through
-            print(f"rank {rank}: injected fault at epoch {epoch}", flush=True)
-            os._exit(13)
+        if fault is not None and fault.epoch == epoch and fault.rank == rank:
+            fault.fire(args.output_dir, lambda s: print(s, flush=True))  # once per output dir
         st = trainer.train_one_epoch(epoch, train_loader, train_sampler)
         if args.validate:
             vs = trainer.validate(val_loader)

@@ -133,7 +133,7 @@ class Trainer:
         from .graph import GraphedStep, auto_enabled
         cg = getattr(args, "cuda_graph", False)
         if cg is None:      # default: replay launch-bound steps (engine/graph.py)
-            cg = auto_enabled(args, self.device)
+            cg = auto_enabled(args, self.device, self.world_size)
         if cg and self.device.type == "cuda":
             self.graphed = GraphedStep(self)
 
@@ -239,12 +239,11 @@ class Trainer:
         return outputs, loss
 
     # ------------------------------------------------------------------ epochs
-    def _fault_step(self) -> Optional[int]:
-        spec = getattr(self.args, "fault_inject", None)
-        if not spec:
-            return None
-        r, st = (int(v) for v in str(spec).split(":"))
-        return st if r == self.rank else None
+    def _fault(self):
+        """``--fault-inject rank=R,step=S`` for this rank (utils/fault.py), else None."""
+        from ..utils.fault import FaultSpec
+        spec = FaultSpec.parse(getattr(self.args, "fault_inject", None))
+        return spec if spec is not None and spec.step is not None and spec.rank == self.rank else None
 
     def check_consistency(self) -> None:
         """Debug: parameters must be bit-identical across ranks; with
@@ -293,7 +292,7 @@ class Trainer:
             warm = max(0, int(getattr(args, "warmup_steps", 0) or 0))
             self._warmed = True
         check_every = int(getattr(args, "check_consistency", 0) or 0)
-        fault_at = self._fault_step()
+        fault = self._fault()
         if native:
             self.metrics.zero_()
         epoch_loss, epoch_correct, epoch_total = 0.0, 0, 0
@@ -304,8 +303,8 @@ class Trainer:
         win_start = time.time()
         steps = 0
         for i, (images, targets) in enumerate(loader):
-            if fault_at is not None and self.global_step >= fault_at:
-                os._exit(17)   # --fault-inject: die abruptly, peers must not hang
+            if fault is not None and self.global_step >= fault.step:
+                fault.fire(getattr(args, "output_dir", "."), self.log)   # dies; peers must not hang
             sync = (i + 1) % self.grad_accum == 0 or i + 1 == n
             batch_start = time.time()
             outputs, loss = self.train_step(images, targets, sync)

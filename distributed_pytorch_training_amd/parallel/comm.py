@@ -77,7 +77,7 @@ def _host_broadcast(t: torch.Tensor, root: int) -> None:
 
 def make_comm(device: torch.device, rank: int, world_size: int, kind: str = "rccl",
               timeout_s: Optional[float] = None, rccl_channels: int = 0,
-              exit_grace_s: float = 30.0):
+              exit_grace_s: float = 30.0, init_timeout_s: float = 300.0):
     """Create the device collective on ``device`` (GPU) or return None (CPU/gloo path)."""
     if device.type != "cuda":
         return None
@@ -99,35 +99,78 @@ def make_comm(device: torch.device, rank: int, world_size: int, kind: str = "rcc
     if kind == "c10d":
         return _pg_comm(C, dev)
     n_ch = max(0, int(rccl_channels or 0))
+    comm = rccl_or_fallback(
+        new_uid=C.RcclComm.new_unique_id,
+        create=lambda uid: C.RcclComm(uid, rank, world_size, dev, n_ch, n_ch, float(init_timeout_s)),
+        fallback=lambda: _pg_comm(C, dev), rank=rank, world_size=world_size, flag_device=device)
+    if timeout_s and timeout_s > 0 and world_size > 1 and comm.kind == "rccl":
+        comm.enable_watchdog(float(timeout_s), 0.5, float(exit_grace_s))
+    return comm
+
+
+def _agree(ok: bool, flag_device) -> bool:
+    on = flag_device if dist.get_backend() == "nccl" else "cpu"
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=on)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item())
+
+
+def rccl_or_fallback(new_uid, create, fallback, rank: int, world_size: int, flag_device):
+    """Create the framework communicator on every rank, or fall back on every rank.
+
+    RCCL's initialisation is collective and blocking: a rank that fails BEFORE it (no unique id,
+    a failed precondition) would leave its peers blocked inside ``ncclCommInitRank`` and never
+    reach an agreement afterwards.  So the ranks agree three times over the control plane:
+
+    1. rank 0's unique id travels with its creation status (a failed ``ncclGetUniqueId`` is a
+       ``None`` every rank sees, and nobody enters RCCL);
+    2. before init, a MIN all-reduce of "ready" (the test hook ``DPT_TEST_FAIL_COMM_INIT_RANK``
+       makes one rank not ready) - any rank not ready: nobody enters RCCL;
+    3. after init, a MIN all-reduce of "created" - a communicator some ranks built and others did
+       not would hang the first collective, so the built ones are destroyed.
+
+    A failure INSIDE ``ncclCommInitRank`` on some ranks only is bounded by the communicator's
+    init timeout (csrc/rccl_comm.cpp: the blocked ranks give up and reach step 3), then every
+    rank takes the fallback.  ``world_size == 1`` skips the agreements."""
+    import os
+    import warnings
+
+    err = None
+    uid = None
     if world_size > 1:
-        if not dist.is_initialized():
-            raise RuntimeError("make_comm needs an initialised torch.distributed process group")
-        box = [C.RcclComm.new_unique_id() if rank == 0 else None]
+        box = [None]
+        if rank == 0:
+            try:
+                box = [new_uid()]
+            except RuntimeError as e:
+                err = e
         dist.broadcast_object_list(box, src=0)
         uid = box[0]
+        ready = uid is not None and os.environ.get("DPT_TEST_FAIL_COMM_INIT_RANK") != str(rank)
+        if uid is None and err is None:
+            err = RuntimeError("rank 0 could not create an RCCL unique id")
+        elif not ready and err is None:
+            err = RuntimeError("injected pre-init failure (DPT_TEST_FAIL_COMM_INIT_RANK)")
+        if not _agree(ready, flag_device):
+            warnings.warn(f"framework RCCL communicator not created on any rank ({err or 'another rank was not ready'}); "
+                          "falling back to --comm c10d")
+            return fallback()
     else:
-        uid = C.RcclComm.new_unique_id()
+        uid = new_uid()
+    comm = None
     try:
-        comm = C.RcclComm(uid, rank, world_size, dev, n_ch, n_ch)
-        ok = 1
+        comm = create(uid)
     except RuntimeError as e:
-        comm, ok = None, 0
         err = e
+    ok = comm is not None
     if world_size > 1:
-        # every rank takes the same branch (a communicator some ranks built and others did not
-        # would hang the first collective)
-        flag = torch.tensor([ok], dtype=torch.int32, device=device)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        ok = int(flag.item())
+        ok = _agree(ok, flag_device)
     if not ok:
         if comm is not None:
             comm.destroy()
-        import warnings
         warnings.warn(f"framework RCCL communicator unavailable on some rank "
-                      f"({err if comm is None else 'another rank'}); falling back to --comm c10d")
-        return _pg_comm(C, dev)
-    if timeout_s and timeout_s > 0 and world_size > 1:
-        comm.enable_watchdog(float(timeout_s), 0.5, float(exit_grace_s))
+                      f"({err if err is not None else 'another rank'}); falling back to --comm c10d")
+        return fallback()
     return comm
 
 

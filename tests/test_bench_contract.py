@@ -84,6 +84,43 @@ def test_bench_self_launches_ranks_without_torchrun(tmp_path):
     assert rec["comm"]["world_size"] == 2 and rec["comm"]["pg_backend"] == "gloo"
     assert len(rec["comm"]["rank_devices"]) == 2
     assert rec["config"]["launcher"] == "self" and isinstance(rec["config"]["env"], dict)
+    # self-verification: identical parameters on both ranks after the window, an
+    # exact rank+1 all-reduce (1 + 2 = 3) through the collective the gradients used, per-rank times
+    v = rec["verify"]
+    assert v["ok"] is True and v["params_consistent"] is True and v["selftest_ok"] is True, v
+    assert v["selftest_expected"] == 3.0 and len(v["per_rank_ms_per_step"]) == 2
+    assert rec["comm"]["selftest_ok"] is True
+    # no RCCL communicator on gloo: nothing was opened, and the record says so (not a guess)
+    assert v["rccl_channels_opened"] == [None, None]
+
+
+def test_bench_launcher_never_initialises_hip(tmp_path, monkeypatch, capfd):
+    """The self-launching parent must not touch the GPU runtime before it spawns the ranks
+    (re-launching after HIP init is unsafe): run the launcher in-process with every torch entry
+    point that could initialise HIP made to fail - the job still runs, and nothing was
+    initialised in the parent."""
+    import importlib.util
+
+    import torch
+
+    def boom(*a, **k):
+        raise AssertionError("the launcher process touched the GPU runtime")
+
+    for name in ("device_count", "init", "is_available", "set_device", "synchronize"):
+        monkeypatch.setattr(torch.cuda, name, boom)
+    monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", boom, raising=False)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.chdir(tmp_path)
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    rc = bench.main(["--gpus", "2", *TINY])
+    out = capfd.readouterr()
+    assert rc == 0, out.err[-3000:]
+    assert not torch.cuda.is_initialized()
+    lines = _json_lines(out.out)
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 2
 
 
 def test_bench_dead_rank_fails_the_job(tmp_path):
@@ -123,6 +160,9 @@ def test_bench_self_launch_two_ranks_on_one_gpu(tmp_path):
     assert rec["n_gpus"] == 2 and rec["comm"]["world_size"] == 2 and rec["comm"]["kind"] == "host-async"
     assert rec["config"]["launcher"] == "self"
     assert [d["device"] for d in rec["comm"]["rank_devices"]] == ["cuda:0", "cuda:0"]
+    # self-verification through the host-async bridge: exact 1 + 2 and identical parameters
+    assert rec["verify"]["ok"] is True and rec["verify"]["selftest_ok"] is True, rec["verify"]
+    assert rec["verify"]["selftest_via"] == "host-async"
 
 
 @pytest.mark.gpu

@@ -44,7 +44,7 @@ def test_dead_peer_survivor_exits_nonzero(tmp_path):
         env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", WORLD_SIZE="2", RANK=str(r),
                    LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         cmd = [sys.executable, os.path.join(ROOT, "train_ddp.py"), *COMMON, "--output-dir", str(tmp_path),
-               "--dist-timeout", str(timeout_s), "--fault-inject", "1:3"]
+               "--dist-timeout", str(timeout_s), "--fault-inject", "rank=1,step=3"]
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                       text=True, cwd=ROOT))
     try:

@@ -117,7 +117,8 @@ def _run_native(rank, ws, device, extra, amp, steps, inf_step, record=False):
     torch.cuda.synchronize()
     if ws > 1:
         assert ddp.comm is not None and ddp.comm.kind.startswith("host")
-    res = {"params": {n: p.detach().float().cpu() for n, p in model.named_parameters()},
+    res = {"replays": tr.graphed.replays if tr.graphed is not None and tr.graphed.graph is not None else 0,
+           "params": {n: p.detach().float().cpu() for n, p in model.named_parameters()},
            "buffers": {n: b.detach().float().cpu() for n, b in model.named_buffers()},
            "comm_ops": int(ddp.comm.ops) if ddp.comm is not None else 0,
            "buckets": int(ddp.reducer.num_buckets), "snaps": snaps}
@@ -326,6 +327,9 @@ LOCAL_CASES = [
 ]
 
 
+GRAPH_STEPS = 6      # 3 eager warmup steps, the capture, then replays: the last step is a replay
+
+
 @pytest.mark.parametrize("variant,extra", LOCAL_CASES, ids=[c[0] for c in LOCAL_CASES])
 def test_world_size_2_reduces_local_gradients_exactly(cuda, tmp_path, variant, extra):
     """One step of the full native engine at world size 2 vs each rank's own local (world size
@@ -345,6 +349,27 @@ def test_world_size_2_reduces_local_gradients_exactly(cuda, tmp_path, variant, e
             worst = max(worst, err)
             assert err < 1e-6, (variant, r, n, err)
     print(f"{variant}: worst per-tensor relative error vs local sum {worst:.2e}")
+    for n in res[0]["native"]["params"]:
+        assert torch.equal(res[0]["native"]["params"][n], res[1]["native"]["params"][n]), n
+
+
+def test_world_size_2_graph_replay_reduces_local_gradients_exactly(cuda, tmp_path):
+    """the captured step at world size 2 (``--cuda-graph`` over ``--comm
+    host-async``: the bucket all-reduces and the rank-0 buffer broadcasts become graph host
+    nodes, csrc/host_comm.cpp) must reduce to exactly the sum of the two ranks' local gradients
+    on its REPLAYED steps.  lr = 0 keeps the parameters at rank 0's initial weights on every step,
+    so the last (replayed) step's local world-size-1 gradients are a fixed function of that
+    step's batches - the same for the replaying 2-rank job and each rank's eager local run."""
+    res = _spawn(tmp_path, ["--comm", "host-async", "--cuda-graph", "--lr", "0"], amp=True,
+                 steps=GRAPH_STEPS, inf_step=-1, mode="local", timeout=240)
+    a = res[0]["ref"]["raw_grads"]
+    b = res[1]["ref"]["raw_grads"]
+    for r in range(2):
+        nat = res[r]["native"]
+        assert nat["replays"] == GRAPH_STEPS - 3, nat["replays"]   # the capture call replays too
+        for n in a:
+            err = _rel(nat["raw_grads"][n], a[n] + b[n])
+            assert err < 1e-6, (r, n, err)
     for n in res[0]["native"]["params"]:
         assert torch.equal(res[0]["native"]["params"][n], res[1]["native"]["params"][n]), n
 

@@ -83,14 +83,14 @@ def test_gloo_world_size_2(tmp_path):
 @pytest.mark.slow
 def test_restart_after_rank_failure_resumes_from_checkpoint(tmp_path):
     """SURVEY.md §5.3/§5.4 together: rank 1 of a gloo world-size-2 job dies at the start of epoch 3
-    (``--inject-fault``); the job fails non-zero after the epoch-2 checkpoint; the relaunched job
+    (``--fault-inject rank=1,epoch=2``); the job fails non-zero after the epoch-2 checkpoint; the relaunched job
     (what ``torchrun --max-restarts`` does, launched again here: this container's gloo cannot
     reconnect inside one torchrun agent) continues with ``--resume auto`` from that checkpoint,
     completes with exit 0 and runs epoch 3 exactly once."""
     launcher = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                 "--master-addr", "127.0.0.1", "--master-port", "29541"]
     args = COMMON + ["--epochs", "3", "--output-dir", str(tmp_path), "--save-every", "1", "--resume", "auto",
-                     "--inject-fault", "2:1", "--dist-timeout", "60"]
+                     "--fault-inject", "rank=1,epoch=2", "--dist-timeout", "60"]
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     env.pop("WORLD_SIZE", None)
     first = subprocess.run(launcher + [os.path.join(ROOT, "train_ddp.py")] + args, capture_output=True, text=True,
