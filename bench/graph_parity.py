@@ -119,30 +119,39 @@ def teacher(steps: int, extra):
     return rows
 
 
-def free(steps: int, extra, pool_dtype=None):
+def free(steps: int, extra, arms=("--cuda-graph", "--no-cuda-graph"), task: str = "random"):
+    """Free-running loss curves of several arms from the same init; ``arms`` may repeat a mode
+    (two eager runs measure the run-to-run spread of the configuration itself)."""
     dev = torch.device("cuda:0")
     curves = {}
-    for mode in ("--cuda-graph", "--no-cuda-graph"):
-        args, tr = make(["--dataset", "synthetic", "--image-size", "32", "--num-classes", "10", mode, *extra], dev)
+    for k, mode in enumerate(arms):
+        data = ["--synthetic-task", task] + (["--synthetic-noise", "8"] if task == "prototypes" else [])
+        args, tr = make(["--dataset", "synthetic", "--image-size", "32", "--num-classes", "10", mode, *data,
+                         *extra], dev)
         train, _, _ = get_dataloaders(args, 0, 1, dev)
         losses = []
         it = iter(train)
-        for k in range(steps):
+        epoch = 0
+        for _ in range(steps):
             try:
                 x, y = next(it)
             except StopIteration:
+                epoch += 1
+                train.set_epoch(epoch)
                 it = iter(train)
                 x, y = next(it)
             _, loss = tr.train_step(x, y)
             losses.append(loss.detach().clone())
         torch.cuda.synchronize()
-        curves[mode] = [float(v) for v in torch.stack(losses).cpu()]
+        name = mode if mode not in curves else f"{mode}#{k}"
+        curves[name] = [float(v) for v in torch.stack(losses).cpu()]
         del tr
     w = 25
+    names = list(curves)
+    print("steps      | " + " | ".join(names), flush=True)
     for i in range(0, steps, w):
-        a = sum(curves["--cuda-graph"][i:i + w]) / len(curves["--cuda-graph"][i:i + w])
-        b = sum(curves["--no-cuda-graph"][i:i + w]) / len(curves["--no-cuda-graph"][i:i + w])
-        print(f"steps {i:4d}-{i + w - 1:4d}: graph {a:.4f}  eager {b:.4f}", flush=True)
+        vals = [sum(curves[n][i:i + w]) / len(curves[n][i:i + w]) for n in names]
+        print(f"{i:4d}-{i + w - 1:4d}  | " + " | ".join(f"{v:.4f}" for v in vals), flush=True)
     return curves
 
 
@@ -168,13 +177,16 @@ def main():
     ap.add_argument("--mode", choices=["teacher", "free", "startup"], default="teacher")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--extra", default="", help="extra train_ddp flags, space separated")
+    ap.add_argument("--arms", default="--cuda-graph,--no-cuda-graph",
+                    help="free mode: comma-separated modes, repeats allowed (spread of the configuration)")
+    ap.add_argument("--task", default="random", choices=["random", "prototypes"])
     a = ap.parse_args()
     setup_miopen_env()
     torch.cuda.set_device(0)
     setup_tunableop()
     torch.backends.cudnn.benchmark = True
     extra = a.extra.split() if a.extra else []
-    {"teacher": lambda: teacher(a.steps, extra), "free": lambda: free(a.steps, extra),
+    {"teacher": lambda: teacher(a.steps, extra), "free": lambda: free(a.steps, extra, tuple(a.arms.split(",")), a.task),
      "startup": lambda: startup(extra)}[a.mode]()
 
 

@@ -55,6 +55,12 @@ def build_parser() -> argparse.ArgumentParser:
                    help="samples per epoch for --dataset synthetic")
     g.add_argument("--synthetic-val-size", default=10000, type=int,
                    help="validation samples for --dataset synthetic")
+    g.add_argument("--synthetic-task", default="random", choices=["random", "prototypes"],
+                   help="--dataset synthetic: random = a pool of 4 random batches with random labels "
+                        "(benchmark input, memorisation only); prototypes = class prototype images plus "
+                        "pixel noise, fresh every step, learnable and with a held-out validation split")
+    g.add_argument("--synthetic-noise", default=2.0, type=float,
+                   help="pixel noise std of --synthetic-task prototypes (prototypes have unit std)")
     g.add_argument("--amp-dtype", default="fp16", choices=["fp16", "bf16"],
                    help="autocast dtype when --amp is set (reference: fp16)")
     g.add_argument("--optimizer", default="sgd", choices=["sgd", "adam", "adamw"],

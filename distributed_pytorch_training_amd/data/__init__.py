@@ -25,11 +25,14 @@ def get_dataloaders(args, rank: int, world_size: int, device: torch.device):
     if args.dataset == "synthetic":
         n_train = args.synthetic_train_size
         per_rank = math.ceil(n_train / world_size) if distributed else n_train
+        task = getattr(args, "synthetic_task", "random")
+        noise = getattr(args, "synthetic_noise", 2.0)
         train = SyntheticLoader(per_rank, args.batch_size, args.image_size, args.num_classes, device,
-                                channels_last=cl, seed=args.seed + rank, max_steps=max_steps)
+                                channels_last=cl, seed=args.seed + rank, max_steps=max_steps,
+                                task=task, noise=noise)
         val = SyntheticLoader(args.synthetic_val_size, args.batch_size, args.image_size,
                               args.num_classes, device, channels_last=cl, seed=args.seed + 10_000,
-                              pool=2)
+                              pool=2, task=task, noise=noise)
         return train, val, None
 
     # CIFAR-10 from local files (rank 0 "downloads" = checks presence, then barrier).

@@ -64,17 +64,45 @@ class DeviceImageLoader:
             yield out, self.labels.index_select(0, bidx)
 
 
+def class_prototypes(num_classes: int, image_size: int, device, seed: int = 1234) -> torch.Tensor:
+    """Fixed per-class mean images of the learnable synthetic task: smooth random fields
+    (upsampled 4x4 noise, unit variance), the same for every rank, split and engine."""
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed)
+    low = torch.randn((num_classes, 3, 4, 4), generator=g)
+    up = torch.nn.functional.interpolate(low, size=(image_size, image_size), mode="bilinear", align_corners=False)
+    up = up / up.flatten(1).std(dim=1).clamp_min(1e-6).view(-1, 1, 1, 1)
+    return up.to(device)
+
+
 class SyntheticLoader:
+    """On-device synthetic batches.
+
+    ``task="random"`` (benchmarks): a pool of ``pool`` random batches with random labels, cycled -
+    the model can only memorise it.  ``task="prototypes"`` (training-outcome checks): every sample
+    is its class prototype (``class_prototypes``) plus ``noise`` x N(0, 1) pixel noise, drawn
+    fresh for every batch from a generator seeded by (seed, epoch, step) - the same data for any
+    engine, and a held-out split (another seed) that is learnable and measures generalisation."""
+
     def __init__(self, num_samples: int, batch_size: int, image_size: int, num_classes: int,
                  device: torch.device, channels_last: bool = False, pool: int = 4,
-                 dtype: torch.dtype = torch.float32, seed: int = 0, max_steps: int = 0) -> None:
+                 dtype: torch.dtype = torch.float32, seed: int = 0, max_steps: int = 0,
+                 task: str = "random", noise: float = 2.0) -> None:
         self.num_samples, self.batch_size = num_samples, batch_size
         self.device = torch.device(device)
         self.max_steps = max_steps
+        self.task, self.noise, self.seed, self.epoch = task, float(noise), seed, 0
+        self.dtype, self.num_classes, self.image_size = dtype, num_classes, image_size
+        self.mf = torch.channels_last if channels_last else torch.contiguous_format
+        self.pool_x, self.pool_y = [], []
+        if task == "prototypes":
+            self.protos = class_prototypes(num_classes, image_size, self.device)
+            return
+        if task != "random":
+            raise ValueError(f"unknown synthetic task {task!r}")
         g = torch.Generator(device=self.device)
         g.manual_seed(seed)
-        mf = torch.channels_last if channels_last else torch.contiguous_format
-        self.pool_x, self.pool_y = [], []
+        mf = self.mf
         for _ in range(max(1, pool)):
             x = torch.randn((batch_size, 3, image_size, image_size), generator=g, device=self.device,
                             dtype=torch.float32).to(dtype)
@@ -83,15 +111,26 @@ class SyntheticLoader:
                                              device=self.device, dtype=torch.int64))
 
     def set_epoch(self, epoch: int) -> None:
-        pass
+        self.epoch = int(epoch)
 
     def __len__(self) -> int:
         n = math.ceil(self.num_samples / self.batch_size)
         return min(n, self.max_steps) if self.max_steps else n
 
+    def _prototype_batch(self, step: int, b: int):
+        g = torch.Generator(device=self.device)
+        g.manual_seed((self.seed * 1_000_003 + self.epoch * 10_007 + step) & 0x7FFFFFFF)
+        y = torch.randint(0, self.num_classes, (b,), generator=g, device=self.device, dtype=torch.int64)
+        x = torch.randn((b, 3, self.image_size, self.image_size), generator=g, device=self.device)
+        x = (self.protos.index_select(0, y) + self.noise * x).to(self.dtype)
+        return x.contiguous(memory_format=self.mf), y
+
     def __iter__(self):
         n = len(self)
         for step in range(n):
+            if self.task == "prototypes":
+                yield self._prototype_batch(step, min(self.batch_size, self.num_samples - step * self.batch_size))
+                continue
             k = step % len(self.pool_x)
             b = min(self.batch_size, self.num_samples - step * self.batch_size)
             if b == self.batch_size:

@@ -74,16 +74,55 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous(memory_format=_CL) else t.contiguous(memory_format=_CL)
 
 
+# In-step attribution (bench/conv_instep.py): when a list, every conv pass records a timing event
+# on the current stream before and after its launches, tagged (pass, shape, epilogue variant).
+# Off (None) in training: no event, no Python work.
+_CALLS = None
+
+
+def profile_calls(on: bool) -> None:
+    global _CALLS
+    _CALLS = [] if on else None
+
+
+def take_profile():
+    """[(pass, shape, variant, start_event, end_event)] recorded since profile_calls(True)."""
+    out = list(_CALLS or [])
+    if _CALLS is not None:
+        _CALLS.clear()
+    return out
+
+
+def _mark():
+    if _CALLS is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
+def _note(kind, x, w, stride, pad, variant, e0, out_hw=(0, 0)):
+    if _CALLS is None or e0 is None:
+        return
+    co, ci, r, _ = w.shape
+    key = (ci, x.shape[2], x.shape[3], co, r, int(stride), int(pad), tuple(int(v) for v in out_hw))
+    _CALLS.append((kind, key, variant, e0, _mark()))
+
+
 def _backward(ctx, dy):
     x, w = ctx.saved_tensors
     dy = _cl(dy.to(x.dtype))
     s, p = ctx.stride, ctx.pad
     dx = dw = red = None
+    e0 = _mark()
     if ctx.needs_input_grad[1]:
         if ctx.needs_input_grad[0] and WGRAD_REDUCE_FUSE:
             dw, red = native().conv_wgrad_deferred(dy, x, list(w.shape), s, p)
         else:
             dw = native().conv_wgrad(dy, x, list(w.shape), s, p, False)
+        _note("wgrad", x, w, s, p, "deferred-reduce" if red is not None else "reduce", e0)
+        e0 = _mark()
+    variant = None
     if ctx.needs_input_grad[0]:
         src = ctx.bn_src if (s == 1 and BN_BWD_FUSE) else None
         dres = None
@@ -93,6 +132,7 @@ def _backward(ctx, dy):
             dx, p1, p2, _ = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, bn_coef, w_flipped=wt,
                                                         wgrad_reduce=red)
             _put_bnb(dx, p1, p2, None, None)
+            variant = "bnrelu-stats"
         elif src is not None and _dres_ok(dres := src[2].pop("dres", None), x):  # (x, mean, slot)
             # block-tail BN+add+ReLU (ops/bn.py pair outputs): the next block's tail already
             # produced the identity-path gradient dres; dx becomes the tail's masked total
@@ -105,9 +145,11 @@ def _backward(ctx, dy):
             dx, p1, p2, p3 = native().conv_dgrad_bnstats(dy, w, p, bn_x, bn_mean, None, x, dres, wt, x2, mean2,
                                                          wgrad_reduce=red, bn_mask=src[2].get("mask"))
             _put_bnb(dx, p1, p2, dres.data_ptr(), p3 if x2 is not None else None)
+            variant = "tail+ds-stats" if x2 is not None else "tail-stats"
         elif s == 1:
             dx = (native().conv_dgrad_flip(dy, w, p, wgrad_reduce=red)[0] if wt is None
                   else native().conv_dgrad_preflipped(dy, wt, p, wgrad_reduce=red))
+            variant = "plain"
         elif s == 2 and S2_DGRAD and x.dim() == 4:
             src = ctx.bn_src if BN_BWD_FUSE else None
             if src is not None and not isinstance(src[2], dict) and w.shape[2] > 1:
@@ -115,13 +157,17 @@ def _backward(ctx, dy):
                 dx, p1, p2 = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3], src[0], src[1], src[2],
                                                     wgrad_reduce=red)
                 _put_bnb(dx, p1, p2, None, None)
+                variant = "s2-bnrelu-stats"
             else:
                 dx = native().conv_dgrad_s2(dy, w, p, x.shape[2], x.shape[3], wgrad_reduce=red)[0]
+                variant = "s2"
         else:
             dx = torch.ops.aten.convolution_backward(dy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
                                                      (True, False, False))[0]
     if red is not None and not red.done:
         native().conv_reduce_flush(red)   # no native backward-data launch took it
+    if variant is not None:
+        _note("dgrad", x, w, s, p, variant + ("+reduce" if red is not None else ""), e0)
     if dx is not None and ctx.res_slot is not None:
         # x is the identity alias of a fused block tail and this conv its downsample: hand the
         # identity-path gradient to the tail's conv-path consumer (see ops/bn.py)
@@ -183,7 +229,9 @@ def _dres_ok(dres, x) -> bool:
 class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride: int, pad: int, out_hw, bn_src, res_slot):
+        e0 = _mark()
         y = native().conv_fwd(x, w, stride, pad, False, *out_hw)[0]
+        _note("fwd", x, w, stride, pad, "plain", e0, out_hw)
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad, ctx.bn_src, ctx.res_slot = stride, pad, bn_src, res_slot
         return y
@@ -196,7 +244,9 @@ class _Conv(torch.autograd.Function):
 class _ConvStats(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride: int, pad: int, out_hw, bn_src, res_slot):
+        e0 = _mark()
         y, ps, pq = native().conv_fwd(x, w, stride, pad, True, *out_hw)
+        _note("fwd", x, w, stride, pad, "stats", e0, out_hw)
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad, ctx.bn_src, ctx.res_slot = stride, pad, bn_src, res_slot
         ctx.mark_non_differentiable(ps, pq)
