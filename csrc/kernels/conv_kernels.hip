@@ -218,8 +218,10 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   // epilogue (17 KiB + statistics scratch) fits under the 32 KiB K-loop buffer of a 128 x 128
   // tile: 5 resident blocks per CU instead of 4 (36 KiB), i.e. 25 % more bytes in flight for a
   // K loop that is latency-bound on its L2 -> LDS loads (profiles/conv_pmc_r2.md)
-  constexpr bool HALF = DPT_CONV_HALF_EPI && LDSEPI && BM == 128 && NT == conv::kThreads && MI * 32 <= 64 && !BNB &&
-                        !SPLIT;
+  // The 4-wave 128 x 256 tile (one wave per 64 output channels, 128 rows each) always stages half
+  // its output image at a time: 34 KiB instead of 68 KiB of epilogue LDS, 3 resident blocks per CU.
+  constexpr bool HALF = LDSEPI && BM == 128 && NT == conv::kThreads && !BNB && !SPLIT &&
+                        ((DPT_CONV_HALF_EPI && MI * 32 <= 64) || BN == 256);
   constexpr int EROWS = HALF ? 64 : BM;  // rows of the epilogue image
   constexpr int LDS_EPI = (LDSEPI ? EROWS * C_STRIDE : 0) + RED;
   constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
@@ -632,11 +634,12 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
     if (HALF) {
       // this half's 64 rows: the waves that own them round their accumulators into the image
       if (half) __syncthreads();  // every thread is done reading the first half
-      if ((wm * MI * 32) / 64 == half) {
+      {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NI; ++j) {
+            if ((wm * MI * 32 + i * 32) / 64 != half) continue;  // this 32-row fragment is in the other half
             const int col = wn * 64 + j * 32 + lr;
             const int rbase = wm * (MI * 32) + i * 32 + 4 * lh - half * 64;
 #pragma unroll
@@ -1936,7 +1939,7 @@ static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdAr
   ConvFwdArgs a = a0;
   if constexpr (NT == conv::kThreads) grid.x += (unsigned)take_attached_reduce(a);
   conv_check_offsets(a, BKN);
-  if constexpr (BMT == 128 && STAGES == 1 && LDSEPI && !BKN && !REMAP && NT == conv::kThreads) {
+  if constexpr (BMT == 128 && BN <= 128 && STAGES == 1 && LDSEPI && !BKN && !REMAP && NT == conv::kThreads) {
     if (halo_ok(a)) {
       if (halo_hb(a, BN) == 3) {  // all three B taps with the halo strip
         if (a.f16)
@@ -2160,6 +2163,13 @@ static bool conv_fwd_big(int v, ConvFwdArgs& a, hipStream_t s) {
   return true;
 }
 
+// Variant 14: the 4-wave 128 x 256 tile for expanding 1x1 convs (K <= 128, Cout % 256 == 0), whose
+// 128 x 128 tile re-reads the input once per 128 output channels and is bound by its output writes.
+static bool wide_n_tile(int v, const ConvFwdArgs& a) {
+  if (v != 14) return false;
+  return a.Cout % 256 == 0 && a.R == 1 && a.S == 1 && (int64_t)a.C <= 128 && a.C % 64 == 0;
+}
+
 static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
                           int R, int S, int stride, int pad, float* psum, float* psq, bool bkn, hipStream_t s,
                           int Ho = 0, int Wo = 0, bool f16 = false, float* ws = nullptr) {
@@ -2177,8 +2187,17 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
   const bool wide = Cout % 128 == 0;
   a.n_tiles = Cout / (wide ? 128 : 64);
   a.mt256 = 0;
-  const int v = fwd_variant();
+  const int v0 = fwd_variant();
   if (!bkn && maybe_split(a, ws, psum != nullptr, false, false, false, s)) return;
+  if (!bkn && wide_n_tile(v0, a)) {
+    // 128 x 256 tiles: A (the input) is read once per 256 output channels instead of per 128
+    a.n_tiles = Cout / 256;
+    const dim3 grid((unsigned)(a.m_tiles * a.n_tiles)), block(conv::kThreads);
+    if (psum) fwd_launch<128, 256, 1, true, false, true>(grid, block, s, a);
+    else fwd_launch<128, 256, 1, true, false, false>(grid, block, s, a);
+    return;
+  }
+  const int v = v0 == 14 ? 0 : v0;  // variant 14 is the wide tile only; everything else: default
   if (!bkn && !a.f16) {
     const int vb = (v >= 9 && v <= 13) ? v : v == 0 ? conv_big_auto(a.M, Cout, (int64_t)R * S * C) : 0;
     if (vb && conv_fwd_big(vb, a, s)) return;
