@@ -30,7 +30,7 @@ CONFIGS = {
                      "--amp"],
     # the flagship model under bf16 autocast
     "r50_bf16": ["--model", "resnet50", "--image-size", "64", "--num-classes", "100", "--batch-size", "128",
-                 "--amp", "--amp-dtype", "bf16", "--lr", "0.05"],
+                 "--amp", "--amp-dtype", "bf16", "--lr", "0.02"],
 }
 
 # pixel noise std against unit-std prototypes, per config: the classes separate only through the
