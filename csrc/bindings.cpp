@@ -301,46 +301,6 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bo
   return {y, ps, pq};
 }
 
-// out = conv2d(relu(x*a + b), w) with coef = [a | b] (a training BatchNorm+ReLU's forward
-// coefficients, bn_fwd_train apply=false): the activation is formed in the conv's staged operand
-// and written once to act (the backward's wgrad input) - no separate apply pass.  Shapes the
-// fused kernel does not cover (conv_fwd_act would return false: strided / split-K grids) run the
-// apply pass and the plain conv instead; same values either way.  Returns {out, act, psum, psq}.
-std::vector<Tensor> conv_fwd_act(Tensor x, Tensor coef, Tensor w, int64_t stride, int64_t pad, bool want_stats) {
-  check_cl_bf16(x, "x");
-  check_cl_bf16(w, "w");
-  same_16(x, w, "conv_fwd_act");
-  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
-  const int Cout = w.size(0), R = w.size(2), S = w.size(3);
-  TORCH_CHECK(w.size(1) == C && dpt::conv_supported(C, Cout), "conv_fwd_act: needs C % 64 == 0 and Cout % 64 == 0");
-  TORCH_CHECK(coef.is_cuda() && coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == 2 * C,
-              "conv_fwd_act: coef must be contiguous fp32 [2*C]");
-  TORCH_CHECK(stride >= 1 && pad >= 0 && R == S, "conv_fwd_act: bad stride/pad/kernel");
-  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
-  const int64_t M = (int64_t)N * H * W, Mo = (int64_t)N * Ho * Wo;
-  auto out = at::empty({N, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  auto act = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  c10::hip::HIPGuard guard(x.device().index());
-  Tensor ws = splitk_ws(x, Mo, Cout, (int64_t)R * S * C);
-  Tensor ps, pq;
-  if (want_stats) {
-    const int64_t mt = partial_cols(ws, Mo);
-    ps = at::empty({Cout, mt}, x.options().dtype(at::kFloat));
-    pq = at::empty({Cout, mt}, x.options().dtype(at::kFloat));
-  }
-  auto u16 = [](const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); };
-  const float* cf = coef.data_ptr<float>();
-  float* psp = want_stats ? ps.data_ptr<float>() : nullptr;
-  float* pqp = want_stats ? pq.data_ptr<float>() : nullptr;
-  if (!ws.defined() && dpt::launch_conv_fwd_act(u16(x), cf, u16(w), u16(out), u16(act), N, H, W, C, Cout, R, S,
-                                                 (int)stride, (int)pad, psp, pqp, cur_stream(x), is_f16(x)))
-    return {out, act, ps, pq};
-  dpt::launch_bn_apply(bn_dtype(x), x.data_ptr(), nullptr, act.data_ptr(), M, C, cf, cf + C, true, cur_stream(x));
-  dpt::launch_conv_fwd(u16(act), u16(w), u16(out), N, H, W, C, Cout, R, S, (int)stride, (int)pad, psp, pqp,
-                       cur_stream(x), Ho, Wo, is_f16(x), ws.defined() ? ws.data_ptr<float>() : nullptr);
-  return {out, act, ps, pq};
-}
-
 // dx = conv2d backward-data for a stride-1 conv (flip/transpose folded into the kernel's
 // weight addressing).
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t pad) {
@@ -1191,8 +1151,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn_x") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_coef") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"),
         py::arg("out_h") = 0, py::arg("out_w") = 0);
-  m.def("conv_fwd_act", &conv_fwd_act, py::arg("x"), py::arg("coef"), py::arg("w"), py::arg("stride"), py::arg("pad"),
-        py::arg("want_stats"));
   m.def("space_to_depth2", &space_to_depth2, py::arg("x"), py::arg("out_f16") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("grad_output"), py::arg("x"), py::arg("weight_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("fp32_out"));

@@ -134,12 +134,6 @@ struct ConvFwdArgs {
   // split-K partials of a backward-weight launched just before (the same conv's) instead of
   // computing a conv tile (AttachWgradReduce, kernels.h).  red.blocks = 0: none.
   ReduceCarry red;
-  // ACT (forward of a conv whose input is relu(bn(x)), conv_fwd_kernel): x is the BN input and
-  // every staged A chunk becomes relu(x*a + b) in LDS, coef = [a | b] (2C floats); act_y, when
-  // set, receives that activation (each element once, by the blocks of output-channel tile 0) -
-  // the BatchNorm's forward apply pass and its read of x disappear
-  const float* act_coef = nullptr;
-  uint16_t* act_y = nullptr;
 };
 
 
@@ -153,30 +147,6 @@ __device__ __forceinline__ void vmcnt_wait() {
 template <int RB>
 __device__ __forceinline__ bf16x8_t wg_frag(const unsigned char* img, int krow0, int col0, int lane) {
   return tr_frag<RB, false>(img, krow0, col0, lane);
-}
-
-// relu(x*a + b) of one 16-byte chunk (channels c0..c0+7) with coef = [a | b]: the BatchNorm
-// forward apply's arithmetic (fma, NaN-propagating clamp) and round-to-nearest-even store.
-template <bool F16>
-__device__ __forceinline__ uint4 act_chunk(uint4 v, const float* __restrict__ coef, int c0, int C) {
-  const float4 a0 = *reinterpret_cast<const float4*>(coef + c0), a1 = *reinterpret_cast<const float4*>(coef + c0 + 4);
-  const float4 b0 = *reinterpret_cast<const float4*>(coef + C + c0);
-  const float4 b1 = *reinterpret_cast<const float4*>(coef + C + c0 + 4);
-  const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-  const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-  const uint32_t u[4] = {v.x, v.y, v.z, v.w};
-  uint32_t o[4];
-#pragma unroll
-  for (int k2 = 0; k2 < 4; ++k2) {
-    f32x2_t t;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const float r = __builtin_fmaf(cunpack<F16>(u[k2], h), a[2 * k2 + h], b[2 * k2 + h]);
-      t[h] = r < 0.0f ? 0.0f : r;
-    }
-    o[k2] = cpack<F16>(t);
-  }
-  return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 // 16 zero bytes: the global source of glds lanes whose A row falls in the zero padding.
@@ -217,14 +187,9 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 // image border, where the flattened index wraps into the neighbouring row or image) is zeroed
 // in registers.  A operand bytes per three K-steps: 17 KiB instead of 48 KiB - the 128 x 128
 // tile is bound by what one CU can pull from L2 into LDS (docs/DESIGN.md 7.1).
-// ACT: the input x is a BatchNorm's input and the conv consumes relu(bn(x)): every lane turns the
-// 16-byte chunks its own LDS-DMA just wrote into relu(x*a + b) (the BN apply pass's arithmetic and
-// rounding) between its vmcnt wait and the block barrier, and the output-channel tile 0 blocks
-// store the activation for the backward (ConvFwdArgs::act_y).  Zero-filled padding chunks stay
-// zero (they are skipped), so padded taps read 0 = relu(bn(.)) of nothing, as the unfused conv.
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
           bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, bool F16 = false,
-          int NT = conv::kThreads, bool SPLIT = false, bool HALO = false, int HB = 1, bool ACT = false>
+          int NT = conv::kThreads, bool SPLIT = false, bool HALO = false, int HB = 1>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
   constexpr int BM = BMT;
@@ -237,7 +202,6 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   constexpr int A_PER_T = BM * 8 / NT;  // glds instructions per wave per K-step (A)
   constexpr int B_PER_T = BN * 8 / NT;  // (B)
   static_assert(!HALO || (BMT == 128 && STAGES == 1 && !BKN && !SPLIT && NT == conv::kThreads), "HALO config");
-  static_assert(!ACT || (BMT == 128 && STAGES == 1 && !BKN && !SPLIT && !BNB && NT == conv::kThreads), "ACT config");
   constexpr int HROWS = 136;  // halo strip rows: 128 + 2, rounded up to whole 8-row glds instructions
   // HB (HALO): B taps staged per load phase - 1: one per K-step; 3: all three taps of the row
   // with the halo strip, one wait per three K-steps (more LDS: fewer resident blocks)
@@ -443,23 +407,6 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
             ok ? (uint32_t)((int)q * p.C + cb * BK + chunk * 8) * 2u : kOOB, 0, 0, 0);
       }
     };
-    // ACT: this lane's strip chunks -> relu(bn(.)) in place; at tap row 1 the strip rows 1..128 are
-    // the block's own 128 pixels, stored once (output-channel tile 0) as the activation
-    auto act_halo = [&](int r, int cb) {
-      const bool yw = p.act_y != nullptr && nt == 0 && r == 1;
-      const int64_t q0 = m0 + (int64_t)(r - 1) * p.W - 1;
-      for (int gi = wid; gi < HROWS / 8; gi += NW) {
-        const int j = gi * 8 + (lane >> 3);
-        const int chunk = (lane & 7) ^ ((j >> 1) & 7);
-        const int64_t q = q0 + j;
-        if (q < 0 || q >= npix) continue;  // zero fill stays zero (only padded taps read it)
-        uint4* pl = reinterpret_cast<uint4*>(lds + gi * 1024 + lane * 16);
-        const int c0 = cb * BK + chunk * 8;
-        const uint4 t = act_chunk<F16>(*pl, p.act_coef, c0, p.C);
-        *pl = t;
-        if (yw && j >= 1 && j <= 128) *reinterpret_cast<uint4*>(p.act_y + q * p.C + c0) = t;
-      }
-    };
     auto mma_h = [&](int r, int sx) {
       // row base per fragment (the zero row for padding); the swizzle term (hrow >> 1) & 7 is
       // the same for every i (rows 32 apart), so one chunk offset per kk serves all of them
@@ -497,7 +444,6 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
 #pragma unroll
           for (int sx = 0; sx < 3; ++sx) stage_b(r, sx, cb);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if constexpr (ACT) act_halo(r, cb);
           __syncthreads();
 #pragma unroll 1
           for (int sx = 0; sx < 3; ++sx) mma_h(r, sx);
@@ -508,9 +454,6 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
             if (sx == 0) stage_halo(r, cb);
             stage_b(r, sx, cb);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if constexpr (ACT) {
-              if (sx == 0) act_halo(r, cb);
-            }
             __syncthreads();
             mma_h(r, sx);
             __syncthreads();
@@ -561,29 +504,9 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
       __syncthreads();
     }
   } else {
-    // ACT: this lane's A chunks -> relu(bn(.)) in place (in-bounds taps only: the zero-filled
-    // padding stays zero); 1x1 / stride 1: A row = output pixel, stored once as the activation
-    auto act_a = [&](int ks) {
-      const int rs = (ks / cblocks) * tps, cb = ks - (ks / cblocks) * cblocks;
-      const int r = rs / p.S, s = rs - r * p.S;
-      const int koff = (r * p.W + s) * p.C + cb * BK;
-      const bool yw = p.act_y != nullptr && nt == 0;
-#pragma unroll
-      for (int i = 0; i < A_PER_T; ++i) {
-        const int arow = (wid * A_PER_T + i) * 8 + (lane >> 3);
-        const int achunk = (lane & 7) ^ ((arow >> 1) & 7);
-        const int hi = hi0[i] + r, wi = wi0[i] + s;
-        if (!(((unsigned)hi < (unsigned)p.H) & ((unsigned)wi < (unsigned)p.W))) continue;
-        uint4* pl = reinterpret_cast<uint4*>(lds + (wid * A_PER_T + i) * 1024 + lane * 16);
-        const uint4 t = act_chunk<F16>(*pl, p.act_coef, cb * BK + achunk * 8, p.C);
-        *pl = t;
-        if (yw) *reinterpret_cast<uint4*>(p.act_y + aoff[i] + koff) = t;
-      }
-    };
     for (int ks = ks0; ks < ks1; ++ks) {
       stage(ks, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if constexpr (ACT) act_a(ks);
       __syncthreads();
       mma(0);
       __syncthreads();
@@ -2254,9 +2177,8 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
   const bool wide = Cout % 128 == 0;
   a.n_tiles = Cout / (wide ? 128 : 64);
   a.mt256 = 0;
-  const int v0 = fwd_variant();
+  const int v = fwd_variant();
   if (!bkn && maybe_split(a, ws, psum != nullptr, false, false, false, s)) return;
-  const int v = v0;
   if (!bkn && !a.f16) {
     const int vb = (v >= 9 && v <= 13) ? v : v == 0 ? conv_big_auto(a.M, Cout, (int64_t)R * S * C) : 0;
     if (vb && conv_fwd_big(vb, a, s)) return;
@@ -2338,62 +2260,6 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
     else if (res) fwd_launch<128, 64, 1, true, false, false, true, true>(grid, block, s, a);
     else fwd_launch<128, 64, 1, true, false, false, true>(grid, block, s, a);
   }
-}
-
-template <int BN, bool STATS, bool F16>
-static void act_launch(const ConvFwdArgs& a, hipStream_t s, bool halo, int hb) {
-  const dim3 grid((unsigned)(a.m_tiles * a.n_tiles)), block(conv::kThreads);
-  if (halo && hb == 3)
-    hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, false, STATS, false, false, false, false, false, F16,
-                                        conv::kThreads, false, true, 3, true>), grid, block, 0, s, a);
-  else if (halo)
-    hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, false, STATS, false, false, false, false, false, F16,
-                                        conv::kThreads, false, true, 1, true>), grid, block, 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 1, true, false, STATS, false, false, false, false, false, F16,
-                                        conv::kThreads, false, false, 1, true>), grid, block, 0, s, a);
-}
-
-bool launch_conv_fwd_act(const uint16_t* x, const float* coef, const uint16_t* w, uint16_t* y, uint16_t* act_y,
-                         int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad, float* psum,
-                         float* psq, hipStream_t s, bool f16) {
-  const bool one = R == 1 && S == 1 && stride == 1 && pad == 0;
-  const bool three = R == 3 && S == 3 && stride == 1 && pad == 1;
-  if (!(one || three) || C % conv::BK != 0 || Cout % 64 != 0 || fwd_variant() != 0) return false;
-  ConvFwdArgs a;
-  a.part = nullptr; a.splits = 1; a.kps = 0;
-  a.f16 = f16 ? 1 : 0;
-  a.x = x; a.w = w; a.y = y; a.psum = psum; a.psq = psq;
-  a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S; a.stride = stride; a.pad = pad;
-  a.Ho = H; a.Wo = W;
-  a.M = (int64_t)N * H * W;
-  a.m_tiles = conv_m_tiles(a.M);
-  a.mt256 = 0;
-  a.Rw = R; a.Sw = S; a.tr0 = R - 1; a.trs = -1; a.ts0 = S - 1; a.tss = -1;
-  a.act_coef = coef;
-  a.act_y = act_y;
-  const bool wide = Cout % 128 == 0;
-  a.n_tiles = Cout / (wide ? 128 : 64);
-  // the unsplit kernel only: a grid small enough to split (ResNet-18 / 32x32, captured steps)
-  // keeps the separate apply pass and the split-K conv
-  if (conv_fwd_splits(a.M, Cout, (int64_t)R * S * C, nullptr, s) > 1) return false;
-  if (three && !halo_ok(a)) return false;
-  conv_check_offsets(a, false);
-  const int hb = three ? halo_hb(a, wide ? 128 : 64) : 1;
-#define DPT_ACT(BNV, ST)                                              \
-  do {                                                                \
-    if (f16) act_launch<BNV, ST, true>(a, s, three, hb);              \
-    else act_launch<BNV, ST, false>(a, s, three, hb);                 \
-  } while (0)
-  if (wide) {
-    if (psum) DPT_ACT(128, true);
-    else DPT_ACT(128, false);
-  } else {
-    if (psum) DPT_ACT(64, true);
-    else DPT_ACT(64, false);
-  }
-#undef DPT_ACT
-  return true;
 }
 
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,

@@ -161,12 +161,6 @@ int conv_fwd_splits(int64_t M, int Cout, int64_t K, int* kps = nullptr, hipStrea
 int conv_fwd_splits_for(int64_t M, int Cout, int64_t K, bool graph, int* kps = nullptr);
 int conv_split_cols(int64_t M);
 void conv_set_splitk(int mode);  // 0 off / 1 auto (default, DPT_CONV_SPLITK) / 2 in-graph policy always
-// Forward of relu(bn(x)) -> conv with the BN+ReLU applied to the conv's staged input (ACT):
-// 1x1 / stride 1 / pad 0 and 3x3 / stride 1 / pad 1 (HALO) convs, unsplit grids.  act_y receives
-// relu(bn(x)) for the backward.  Returns false (nothing launched) when the shape is not covered.
-bool launch_conv_fwd_act(const uint16_t* x, const float* coef, const uint16_t* w, uint16_t* y, uint16_t* act_y,
-                         int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad, float* psum,
-                         float* psq, hipStream_t s, bool f16);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
                      int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s, int Ho = 0,
                      int Wo = 0, bool f16 = false, float* ws = nullptr);

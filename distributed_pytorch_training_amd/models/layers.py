@@ -56,19 +56,6 @@ def bn_act(bn: nn.Module, x: torch.Tensor, relu: bool = True,
     return F.relu(out, inplace=True) if relu else out
 
 
-def bn_relu_conv(bn: nn.Module, x: torch.Tensor, conv: nn.Module) -> torch.Tensor:
-    """``conv(relu(bn(x)))``.  A training ``FusedBatchNorm2d`` feeding a native (weight-shadow)
-    conv runs as ONE op whose BN+ReLU is applied to the conv's staged input (ops/conv.py
-    ``bn_relu_conv2d``: no separate apply pass); otherwise the plain composition."""
-    if isinstance(bn, FusedBatchNorm2d) and bn.training and torch.is_grad_enabled() and bn.can_fuse(x):
-        fwd = getattr(conv, "forward_bn_relu", None)
-        if fwd is not None:
-            y = fwd(bn, x)
-            if y is not None:
-                return y
-    return conv(bn_act(bn, x))
-
-
 class DeferredBN:
     """A downsample branch whose BatchNorm is not applied yet: ``bn(x)`` is folded into the block
     tail by ``bn_act_block_out`` (ops/bn.py ``_BN2AddReLUPair``) and never materialised."""

@@ -25,7 +25,7 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
-from .layers import bn_act, bn_act_block_out, bn_relu_conv, bn_relu_maxpool, downsample_branch, split_block_input
+from .layers import bn_act, bn_act_block_out, bn_relu_maxpool, downsample_branch, split_block_input
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -52,12 +52,11 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         xc, xi = split_block_input(x)
-        h = self.conv1(xc)
+        out = bn_act(self.bn1, self.conv1(xc))
         # downsample after conv1 (same values): autograd then runs its backward before conv1's,
         # so conv1's backward-data sees the whole identity-path gradient (ops/bn.py block tails)
         identity = xi if self.downsample is None else downsample_branch(self.downsample, xi, self.bn2)
-        # relu(bn1(.)) -> conv2 as one op where it can (layers.bn_relu_conv)
-        return bn_act_block_out(self.bn2, bn_relu_conv(self.bn1, h, self.conv2), identity)
+        return bn_act_block_out(self.bn2, self.conv2(out), identity)
 
 
 class Bottleneck(nn.Module):
@@ -80,13 +79,12 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         xc, xi = split_block_input(x)
-        h = self.conv1(xc)
+        out = bn_act(self.bn1, self.conv1(xc))
         # downsample after conv1 (same values): autograd then runs its backward before conv1's,
         # so conv1's backward-data sees the whole identity-path gradient (ops/bn.py block tails)
         identity = xi if self.downsample is None else downsample_branch(self.downsample, xi, self.bn3)
-        # relu(bn(.)) -> conv as one op where it can (layers.bn_relu_conv)
-        out = bn_relu_conv(self.bn2, bn_relu_conv(self.bn1, h, self.conv2), self.conv3)
-        return bn_act_block_out(self.bn3, out, identity)
+        out = bn_act(self.bn2, self.conv2(out))
+        return bn_act_block_out(self.bn3, self.conv3(out), identity)
 
 
 class ResNet(nn.Module):

@@ -28,10 +28,6 @@ from .conv import MASKED_NO_RES, take_bnb_partials
 
 # Block-tail BN+add+ReLU backward statistics in the consuming conv's dgrad epilogue (see _bwd)
 BNR_FUSE = os.environ.get("DPT_BNR_FUSE", "1") != "0"
-# Measurement only (bench/ab_step.py arm): skip the BN+ReLU forward apply pass and hand the BN
-# input on as its output - WRONG values, the upper bound of what folding that pass into the
-# consuming convolution could save.  Never set in training.
-EXPERIMENT_NO_RELU_APPLY = 0
 
 
 def _cl(t: torch.Tensor) -> torch.Tensor:
@@ -86,12 +82,9 @@ def _fwd(ctx, x, residual, weight, bias, running_mean, running_var, num_batches,
     # block tail whose output feeds a native conv: the 1-bit ReLU mask that conv's dgrad epilogue
     # reads instead of y (1/16 of y's bytes; ops/conv.py BNR)
     mask = _relu_mask(x) if (own_slot is not None and relu and residual is not None) else None
-    skip = EXPERIMENT_NO_RELU_APPLY and relu and residual is None and not pair
     y, mean, invstd, coef = native().bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
                                                   num_batches, float(momentum), float(eps), bool(relu), ps, pq,
-                                                  not skip, mask_out=mask)
-    if skip:
-        y = x.view_as(x)
+                                                  mask_out=mask)
     ctx.relu = bool(relu)
     ctx.has_res = residual is not None
     mask_from_x = ctx.relu and not ctx.has_res and not pair   # pair outputs always write dz

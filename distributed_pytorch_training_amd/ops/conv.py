@@ -277,91 +277,6 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn_stats: bo
     return y
 
 
-# conv(relu(bn(x))) with the BatchNorm+ReLU applied to the conv's staged input (ACT,
-# conv_kernels.hip): the BN's forward apply pass (a read of x and a write of its output) becomes a
-# write of the activation by the conv (kept for the backward-weight).  DPT_ACT_FUSE=0 disables.
-ACT_FUSE = os.environ.get("DPT_ACT_FUSE", "0") == "1"
-
-
-class _Shim:
-    """The attributes ``_backward`` reads from a conv autograd context."""
-
-    def __init__(self, saved, stride, pad, bn_src, needs_input_grad):
-        self.saved_tensors = saved
-        self.stride, self.pad, self.bn_src, self.res_slot = stride, pad, bn_src, None
-        self.needs_input_grad = needs_input_grad
-
-
-class _BNReLUConv(torch.autograd.Function):
-    """``conv2d(relu(batch_norm(x)), w)`` in training mode as ONE op (a bottleneck's bn1 -> conv2
-    and bn2 -> conv3).
-
-    Forward: the BN's statistics (from the producing conv's epilogue partials), running stats and
-    coefficients [a | b]; then the conv with relu(x*a + b) formed in its staged input
-    (``conv_fwd_act``), which also writes the activation once for the backward-weight.  The
-    separate apply pass - a read of x and a write of the activation - is gone.
-    Backward: the conv backward exactly as ``_backward`` runs it for a BN+ReLU input (backward-data
-    with the BN's statistics in its epilogue, backward-weight on the stored activation), then the
-    BN backward from those statistics (mask recomputed from x).  Same kernels and arithmetic as
-    the unfused pair, so the values are bit-identical."""
-
-    @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, num_batches, momentum, eps, partials,
-                w, stride, pad, want_stats):
-        ps, pq = partials if partials is not None else (None, None)
-        C = native()
-        _, mean, invstd, coef = C.bn_fwd_train(x, None, weight, bias, running_mean, running_var, num_batches,
-                                               float(momentum), float(eps), True, ps, pq, False)
-        e0 = _mark()
-        out, act, ops, opq = C.conv_fwd_act(x, coef, w, int(stride), int(pad), bool(want_stats))
-        _note("fwd", x, w, stride, pad, "act-stats" if want_stats else "act", e0)
-        ctx.save_for_backward(act, w, x, weight, mean, invstd, coef)
-        ctx.stride, ctx.pad = int(stride), int(pad)
-        ctx.set_materialize_grads(False)
-        if want_stats:
-            ctx.mark_non_differentiable(ops, opq)
-            return out, ops, opq
-        return out, None, None
-
-    @staticmethod
-    def backward(ctx, dout, _dps, _dpq):
-        act, w, x, weight, mean, invstd, coef = ctx.saved_tensors
-        need_x, need_params, need_w = ctx.needs_input_grad[0], any(ctx.needs_input_grad[1:3]), ctx.needs_input_grad[9]
-        shim = _Shim((act, w), ctx.stride, ctx.pad, (x, mean, coef), (True, need_w))
-        g, dw = _backward(shim, dout)
-        part = take_bnb_partials(g)
-        if part is not None:
-            dx, dg, db = native().bn_bwd_partials(g, x, weight, mean, invstd, coef, part[0], part[1],
-                                                  bool(need_params))
-        else:
-            dx, dg, db, _ = native().bn_bwd(_cl(g), None, act, x, weight, mean, invstd, True, False,
-                                            bool(need_params), coef)
-        return (dx if need_x else None, dg if need_params else None, db if need_params else None,
-                None, None, None, None, None, None, dw, None, None, None)
-
-
-def act_supported(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups) -> bool:
-    """conv(relu(bn(x))) as one op: a native conv on a 16-bit channels_last training input whose
-    channel count the BN kernels handle (shapes the fused kernel does not cover run its fallback:
-    the apply pass + the plain conv, inside the same op)."""
-    return (ACT_FUSE and x.requires_grad and supported(x, w, stride, padding, dilation, groups)
-            and x.shape[1] % 64 == 0)
-
-
-def bn_relu_conv2d(x: torch.Tensor, bn, w: torch.Tensor, stride: int, pad: int, bn_stats: bool = False):
-    """``conv2d(relu(bn(x)), w)`` for a training ``FusedBatchNorm2d`` (see _BNReLUConv); with
-    ``bn_stats`` the output carries its own BatchNorm's partials (``_dpt_bn_partials``)."""
-    w = _cl(w)
-    if _FLIP["on"] and int(stride) == 1:
-        _FLIP["pending"].setdefault((w.data_ptr(), tuple(w.shape)), w)
-    partials = x.__dict__.pop("_dpt_bn_partials", None)
-    y, ps, pq = _BNReLUConv.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
-                                  bn.momentum, bn.eps, partials, w, int(stride), int(pad), bool(bn_stats))
-    if bn_stats:
-        y._dpt_bn_partials = (ps, pq)
-    return y
-
-
 # dres_ptr of an entry whose gradient is a block tail's already-masked gradient with no
 # identity-path gradient folded in (the last tail, whose output only fed the average pool)
 MASKED_NO_RES = -1

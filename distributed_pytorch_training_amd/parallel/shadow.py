@@ -62,21 +62,6 @@ class ShadowConv2d(nn.Conv2d):
         return self._conv_forward(x, w, b)
 
 
-    def forward_bn_relu(self, bn, x: torch.Tensor):
-        """``self(relu(bn(x)))`` as one native op (ops/conv.py ``bn_relu_conv2d``), or None when
-        this conv does not run natively on ``x``."""
-        sh = active_shadow(self, x)
-        if sh is None or not self.dpt_native_conv or self.bias is not None:
-            return None
-        w = sh["weight"]
-        if not native_conv.act_supported(x, w, self.stride, self.padding, self.dilation, self.groups):
-            return None
-        if self.dpt_min_pixels is not None and not native_conv.supported(
-                x, w, self.stride, self.padding, self.dilation, self.groups, self.dpt_min_pixels):
-            return None
-        return native_conv.bn_relu_conv2d(x, bn, w, self.stride[0], self.padding[0], self.dpt_bn_stats)
-
-
 class ShadowLinear(nn.Linear):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         sh = active_shadow(self, x)
