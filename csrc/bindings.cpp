@@ -1160,6 +1160,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("grad_output"), py::arg("lse"),
         py::arg("heads"), py::arg("scale"));
   m.def("conv_set_variant", &dpt::conv_set_variant, py::arg("variant"));
+  m.def("bn_set_skip_finalize", &dpt::bn_set_skip_finalize, py::arg("on"),
+        "measurement only: skip every BatchNorm finalize launch (wrong values; timing upper bound)");
   m.def("conv_set_big", &dpt::conv_set_big, py::arg("on"));
   m.def("conv_set_halo", &dpt::conv_set_halo, py::arg("on"));
   m.def("conv_set_wgrad_target", &dpt::conv_set_wgrad_target, py::arg("blocks"));

@@ -455,7 +455,14 @@ BnBwdFin make_bn_bwd_fin(const float* p1, const float* p2, int chunks, int C, in
 
 // Wide finalizes (one block per channel, thousands of partials) run 256-thread blocks too: 512
 // and 1024 measured 0.3-0.5 % slower in the step (docs/DESIGN.md §9).
+// Measurement only (bench/ab_step.py arm bn_set_skip_finalize:1): skip every BatchNorm finalize
+// launch - WRONG values (stale coefficients), the upper bound of what folding the finalizes into
+// neighbouring kernels could save.  Never set in training.
+static int g_bn_skip_finalize = 0;
+void bn_set_skip_finalize(int on) { g_bn_skip_finalize = on; }
+
 static void launch_bn_bwd_fin(const BnBwdFin& f, hipStream_t s) {
+  if (g_bn_skip_finalize) return;
   hipLaunchKernelGGL(bn_bwd_finalize_kernel<kBlock>, dim3((unsigned)f.blocks), dim3(kBlock), 0, s, f);
 }
 
@@ -633,7 +640,8 @@ void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void
   BnGeometry g = bn_geometry(M, C);
   float* ca = save_coef;
   float* cb = ca + C;
-  if (chunks > 256) {
+  if (g_bn_skip_finalize) {
+  } else if (chunks > 256) {
 #define DPT_FWD_FIN(NT)                                                                                        \
   hipLaunchKernelGGL(bn_fwd_finalize_wide_kernel<NT>, dim3((unsigned)C), dim3(NT), 0, s, psum, psq, chunks, (int)C, \
                      M, gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd, ca, cb)
@@ -787,7 +795,8 @@ void launch_bn2_bwd_from_partials(int dtype, const void* dz, const void* x, cons
   const BnBwdFin f1 = make_bn_bwd_fin(p1, p2, chunks, (int)C, M, gamma, invstd, dgamma, dbeta, k, k + C, k + 2 * C, -1);
   const BnBwdFin f2 =
       make_bn_bwd_fin(p1, p3, chunks, (int)C, M, gamma2, invstd2, dgamma2, dbeta2, j, j + C, j + 2 * C, -1);
-  hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((unsigned)(f1.blocks + f2.blocks)), dim3(kBlock), 0, s, f1, f2);
+  if (!g_bn_skip_finalize)
+    hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((unsigned)(f1.blocks + f2.blocks)), dim3(kBlock), 0, s, f1, f2);
   dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
   switch (dtype) {
     case 0: hipLaunchKernelGGL(bn_bwd_apply2_kernel<F32>, ga, bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, kBnReverse); break;

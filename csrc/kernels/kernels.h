@@ -79,6 +79,7 @@ void launch_bn2_bwd_from_partials(int dtype, const void* dz, const void* x, cons
                                   const float* mean2, const float* invstd2, const float* p1, const float* p2,
                                   const float* p3, int chunks, float* dgamma, float* dbeta, float* dgamma2,
                                   float* dbeta2, void* dx, void* dx2, float* kbuf, hipStream_t s);
+void bn_set_skip_finalize(int on);  // measurement only (bench/ab_step.py): skip BN finalize launches
 void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                      const float* coef_a, const float* coef_b, bool relu, hipStream_t s);
 void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, const void* x, int64_t M,
