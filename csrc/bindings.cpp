@@ -699,54 +699,6 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> residual, c10::
   return {y, mean, invstd, coef};
 }
 
-// Block tail with a downsample BatchNorm, training mode, both BNs' statistics from conv-epilogue
-// partials: y = relu(bn(x) + bn2(x2)); both finalizes and the apply run as ONE launch (in-launch
-// hand-off, csrc/kernels/handoff.h).  Returns {y, mean, invstd, coef, mean2, invstd2, coef2}.
-std::vector<Tensor> bn2_fwd_train(Tensor x, Tensor x2, c10::optional<Tensor> weight, c10::optional<Tensor> bias,
-                                  c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
-                                  c10::optional<Tensor> num_batches, double momentum, double eps,
-                                  c10::optional<Tensor> weight2, c10::optional<Tensor> bias2,
-                                  c10::optional<Tensor> running_mean2, c10::optional<Tensor> running_var2,
-                                  c10::optional<Tensor> num_batches2, double momentum2, double eps2, Tensor psum,
-                                  Tensor psq, Tensor psum2, Tensor psq2, c10::optional<Tensor> mask_out) {
-  auto [M, C] = bn_rows(x, "x");
-  TORCH_CHECK(dpt::bn_supported(C), "fused BN: unsupported channel count ", C);
-  TORCH_CHECK(x2.sizes() == x.sizes() && x2.scalar_type() == x.scalar_type(), "bn2_fwd_train: x2 mismatch");
-  bn_rows(x2, "x2");
-  for (const Tensor* t : {&psum, &psq, &psum2, &psq2})
-    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->dim() == 2 && t->size(0) == C && t->is_contiguous(),
-                "bn2_fwd_train: partials must be contiguous fp32 [C, chunks]");
-  TORCH_CHECK(psq.sizes() == psum.sizes() && psq2.sizes() == psum2.sizes(), "bn2_fwd_train: partials mismatch");
-  auto nb_ptr = [](const c10::optional<Tensor>& t) -> int64_t* {
-    if (!t.has_value() || !t->defined()) return nullptr;
-    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong, "num_batches must be int64 GPU");
-    return t->data_ptr<int64_t>();
-  };
-  auto fopt = x.options().dtype(at::kFloat);
-  auto y = at::empty_like(x);
-  auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), coef = at::empty({2 * C}, fopt);
-  auto mean2 = at::empty({C}, fopt), invstd2 = at::empty({C}, fopt), coef2 = at::empty({2 * C}, fopt);
-  uint8_t* mp = relu_mask_ptr(mask_out, M, C, x, "bn2_fwd_train");
-  c10::hip::HIPGuard guard(x.device().index());
-  dpt::BnFwdArgs a1, a2;
-  a1.psum = psum.data_ptr<float>(); a1.psq = psq.data_ptr<float>(); a1.chunks = (int)psum.size(1);
-  a1.gamma = f32_param(weight, C, "weight"); a1.beta = f32_param(bias, C, "bias");
-  a1.eps = (float)eps; a1.momentum = (float)momentum;
-  a1.run_mean = f32_param(running_mean, C, "running_mean"); a1.run_var = f32_param(running_var, C, "running_var");
-  a1.num_batches = nb_ptr(num_batches);
-  a1.save_mean = mean.data_ptr<float>(); a1.save_invstd = invstd.data_ptr<float>(); a1.save_coef = coef.data_ptr<float>();
-  a2.psum = psum2.data_ptr<float>(); a2.psq = psq2.data_ptr<float>(); a2.chunks = (int)psum2.size(1);
-  a2.gamma = f32_param(weight2, C, "weight2"); a2.beta = f32_param(bias2, C, "bias2");
-  a2.eps = (float)eps2; a2.momentum = (float)momentum2;
-  a2.run_mean = f32_param(running_mean2, C, "running_mean2"); a2.run_var = f32_param(running_var2, C, "running_var2");
-  a2.num_batches = nb_ptr(num_batches2);
-  a2.save_mean = mean2.data_ptr<float>(); a2.save_invstd = invstd2.data_ptr<float>();
-  a2.save_coef = coef2.data_ptr<float>();
-  dpt::launch_bn2_fwd_from_partials(bn_dtype(x), x.data_ptr(), x2.data_ptr(), y.data_ptr(), M, C, a1, a2,
-                                    cur_stream(x), mp);
-  return {y, mean, invstd, coef, mean2, invstd2, coef2};
-}
-
 // y = relu(x*a + b + x2*a2 + b2), coef = [a | b], coef2 = [a2 | b2] (bn_fwd_train coefficients)
 Tensor bn_apply_aff(Tensor x, Tensor x2, Tensor coef, Tensor coef2, c10::optional<Tensor> mask_out) {
   auto [M, C] = bn_rows(x, "x");
@@ -1172,22 +1124,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("relu"), py::arg("psum") = py::none(), py::arg("psq") = py::none(), py::arg("apply") = true,
         py::arg("mask_out") = py::none());
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("residual"), py::arg("a"), py::arg("b"), py::arg("relu"));
-  m.def("bn2_fwd_train", &bn2_fwd_train, py::arg("x"), py::arg("x2"), py::arg("weight"), py::arg("bias"),
-        py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches"), py::arg("momentum"), py::arg("eps"),
-        py::arg("weight2"), py::arg("bias2"), py::arg("running_mean2"), py::arg("running_var2"),
-        py::arg("num_batches2"), py::arg("momentum2"), py::arg("eps2"), py::arg("psum"), py::arg("psq"),
-        py::arg("psum2"), py::arg("psq2"), py::arg("mask_out") = py::none());
-  m.def("bn_set_fuse_finalize", &dpt::bn_set_fuse_finalize, py::arg("on"),
-        "run BatchNorm finalizes inside the apply launch (in-launch hand-off; default on)");
-  m.def("bn_fuse_finalize_enabled", &dpt::bn_fuse_finalize_enabled);
-  m.def("bn_set_fused_apply_cap", &dpt::bn_set_fused_apply_cap, py::arg("blocks"));
-  m.def("bn_handoff_begin", []() { dpt::bn_handoff_begin(c10::hip::getCurrentHIPStream().stream()); },
-        "start of a training step: zero the BatchNorm hand-off granules of the previous step on the current stream");
-  m.def("bn_handoff_fused_launches", &dpt::bn_handoff_fused_launches);
-  m.def("bn_set_handoff_idle_finalizers", &dpt::bn_set_handoff_idle_finalizers, py::arg("on"),
-        "test only: the fused launches' finalize blocks exit at once, so the apply blocks must help");
-  m.def("bn_handoff_errors", &dpt::bn_handoff_errors,
-        "bounded-spin time-outs of the BatchNorm in-launch hand-off on the current device (synchronises; expect 0)");
   m.def("bn_apply_aff", &bn_apply_aff, py::arg("x"), py::arg("x2"), py::arg("coef"), py::arg("coef2"),
         py::arg("mask_out") = py::none());
   m.def("bn2_bwd_partials", &bn2_bwd_partials, py::arg("dz"), py::arg("x"), py::arg("x2"), py::arg("weight"),

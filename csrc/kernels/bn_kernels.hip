@@ -24,11 +24,9 @@
 // Reductions are deterministic two-level: fixed row chunks -> fp32 partials [C][chunks]
 // -> fp64 per-channel sums in a finalize kernel (one wave per 2 channels).  No atomics.
 #include <cstdlib>
-#include <mutex>
 
 #include "carry.h"
 #include "common.h"
-#include "handoff.h"
 #include "kernels.h"
 
 namespace dpt {
@@ -186,198 +184,102 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_stats_kernel(const void* __rest
   }
 }
 
-// ---- forward finalize: partials -> mean, invstd, coefficients, running statistics ------------
-// One half-wave per channel (8 channels per block) for up to 256 partials per channel, else one
-// 256-thread block per channel (the conv epilogue writes one partial per 128 rows: up to ~6k at
-// ResNet-50's 56x56 layers; 25k for the stem); fp64 sums.  Runs as its own launch or in the first
-// blocks of the apply launch (handoff.h).
-struct BnFwdFin {
-  const float* psum = nullptr;
-  const float* psq = nullptr;
-  int chunks = 0, C = 0;
-  int64_t M = 0;
-  const float* gamma = nullptr;  // nullptr: 1
-  const float* beta = nullptr;   // nullptr: 0
-  float eps = 0.f, momentum = 0.f;
-  float* run_mean = nullptr;  // optional (with run_var)
-  float* run_var = nullptr;
-  int64_t* num_batches = nullptr;  // optional
-  float* save_mean = nullptr;
-  float* save_invstd = nullptr;
-  float* coef_a = nullptr;
-  float* coef_b = nullptr;
-  int wide = 0, blocks = 0;
-  unsigned long long* gran = nullptr;  // in-launch hand-off (handoff.h): a | b granules [2C]
-};
-
-static BnFwdFin make_bn_fwd_fin(const float* psum, const float* psq, int chunks, int C, int64_t M, const float* gamma,
-                                const float* beta, float eps, float momentum, float* run_mean, float* run_var,
-                                int64_t* num_batches, float* save_mean, float* save_invstd, float* coef_a,
-                                float* coef_b, int wide = -1) {
-  BnFwdFin f;
-  f.psum = psum; f.psq = psq; f.chunks = chunks; f.C = C; f.M = M; f.gamma = gamma; f.beta = beta;
-  f.eps = eps; f.momentum = momentum; f.run_mean = run_mean; f.run_var = run_var; f.num_batches = num_batches;
-  f.save_mean = save_mean; f.save_invstd = save_invstd; f.coef_a = coef_a; f.coef_b = coef_b;
-  f.wide = wide < 0 ? (chunks > 256 ? 1 : 0) : wide;
-  f.blocks = f.wide ? C : (C + 7) / 8;
-  return f;
-}
-
-// Statistics -> mean, invstd and coefficients of channel c (idempotent stores: a block that helps
-// with a fused launch's finalize may repeat them, handoff.h); returns mean and biased variance.
-__device__ __forceinline__ void bn_fwd_fin_coef(const BnFwdFin& f, int64_t c, double s, double q, double& mean,
-                                                double& var) {
-  mean = s / (double)f.M;
-  var = q / (double)f.M - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
-  const float g = f.gamma ? f.gamma[c] : 1.0f, bt = f.beta ? f.beta[c] : 0.0f;
-  const float a = g * invstd;
-  const float b = bt - (float)mean * a;
-  f.save_mean[c] = (float)mean;
-  f.save_invstd[c] = invstd;
-  f.coef_a[c] = a;
-  f.coef_b[c] = b;
-  if (f.gran) {  // handed to the apply blocks of this launch (handoff.h)
-    put_gran(f.gran + c, a);
-    put_gran(f.gran + f.C + c, b);
-  }
-}
-
-// The read-modify-write part: running statistics (momentum, unbiased variance) - exactly once.
-__device__ __forceinline__ void bn_fwd_fin_running(const BnFwdFin& f, int64_t c, double mean, double var) {
-  if (f.run_mean) {
-    const double unbiased = f.M > 1 ? var * (double)f.M / (double)(f.M - 1) : var;
-    f.run_mean[c] = (1.0f - f.momentum) * f.run_mean[c] + f.momentum * (float)mean;
-    f.run_var[c] = (1.0f - f.momentum) * f.run_var[c] + f.momentum * (float)unbiased;
-  }
-}
-
-// Block `bid` of the finalize (NT threads - wide only, kBlock otherwise; red: 2 * NT / 64 doubles
-// of LDS).  claim (fused launches, handoff.h): the item's claim word - the running statistics and
-// num_batches_tracked are updated only by the block that wins it; nullptr: always.
-template <int NT = kBlock>
-__device__ __forceinline__ void bn_fwd_finalize_block(const BnFwdFin& f, int bid, double* red,
-                                                      unsigned* claim = nullptr) {
+__global__ __launch_bounds__(kBlock) void bn_fwd_finalize_kernel(
+    const float* __restrict__ psum, const float* __restrict__ psq, int chunks, int C, int64_t M,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    float* run_mean, float* run_var, int64_t* num_batches, float* save_mean, float* save_invstd,
+    float* coef_a, float* coef_b) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (f.wide) {
-    const int c = bid;
-    double s, q;
-    block_row_sum2<NT>(f.psum + (int64_t)c * f.chunks, f.psq + (int64_t)c * f.chunks, f.chunks, s, q);
-    if (lane == 0) { red[wave] = s; red[NT / 64 + wave] = q; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      s = 0.0;
-      q = 0.0;
-#pragma unroll
-      for (int w = 0; w < NT / 64; ++w) { s += red[w]; q += red[NT / 64 + w]; }
-      double mean, var;
-      bn_fwd_fin_coef(f, c, s, q, mean, var);
-      if (claim == nullptr || handoff_claim(claim)) {
-        bn_fwd_fin_running(f, c, mean, var);
-        if (bid == 0 && f.num_batches) f.num_batches[0] += 1;
-      }
-    }
-    __syncthreads();  // red is reused by the next item of a helping block
-  } else if constexpr (NT == kBlock) {
-    const int64_t c = (int64_t)bid * 8 + wave * 2 + (lane >> 5);
-    const int part = lane & 31;
-    double mean = 0.0, var = 0.0;
-    if (c < f.C) {
-      double s, q;
-      half_wave_sum2(f.psum, f.psq, c, f.chunks, part, s, q);
-      if (part == 0) bn_fwd_fin_coef(f, c, s, q, mean, var);
-    }
-    bool won = true;
-    if (claim != nullptr) {
-      unsigned* flag = reinterpret_cast<unsigned*>(red);
-      if (threadIdx.x == 0) flag[0] = handoff_claim(claim) ? 1u : 0u;
-      __syncthreads();
-      won = flag[0] != 0u;
-      __syncthreads();
-    }
-    if (won) {
-      if (c < f.C && part == 0) bn_fwd_fin_running(f, c, mean, var);
-      if (bid == 0 && threadIdx.x == 0 && f.num_batches) f.num_batches[0] += 1;
-    }
+  const int64_t c = (int64_t)blockIdx.x * 8 + wave * 2 + (lane >> 5);
+  const int part = lane & 31;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && num_batches) num_batches[0] += 1;
+  if (c >= C) return;
+  double s, q;
+  half_wave_sum2(psum, psq, c, chunks, part, s, q);
+  if (part != 0) return;
+  const double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.0f, bt = beta ? beta[c] : 0.0f;
+  const float a = g * invstd;
+  save_mean[c] = (float)mean;
+  save_invstd[c] = invstd;
+  coef_a[c] = a;
+  coef_b[c] = bt - (float)mean * a;
+  if (run_mean) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    run_mean[c] = (1.0f - momentum) * run_mean[c] + momentum * (float)mean;
+    run_var[c] = (1.0f - momentum) * run_var[c] + momentum * (float)unbiased;
   }
 }
+
+// Same finalize for MANY partials per channel (the conv epilogue writes one per 128 rows: up
+// to ~6k at ResNet-50's 56x56 layers): one 256-thread block per channel, fp64 block reduce.
+// Wave-reduced fp64 sums of two contiguous fp32 rows of `chunks` partials (one block per
+// channel): 8 loads of each row in flight per thread - the finalize is a latency chain of
+// chunks / (kBlock * U) dependent round trips, not a bandwidth problem.
 
 template <int NT>
-__global__ __launch_bounds__(NT) void bn_fwd_finalize_kernel(BnFwdFin f) {
-  __shared__ double red[2 * (NT / 64)];
-  bn_fwd_finalize_block<NT>(f, (int)blockIdx.x, red);
-}
-
-// A finalize as its own launch.  Tens of thousands of partials per channel (the ResNet stem's
-// conv epilogue: 25,088 at batch 256) take 1024-thread blocks - 4x the loads in flight of the
-// latency-bound 256-thread sweep; everywhere else 256 (512/1024 measured 0.3-0.5 % slower in the
-// step, docs/DESIGN.md §9).
-constexpr int kFinHugeChunks = 8192;
-static void launch_bn_fwd_fin(const BnFwdFin& f, hipStream_t s) {
-  if (f.wide && f.chunks > kFinHugeChunks)
-    hipLaunchKernelGGL(bn_fwd_finalize_kernel<1024>, dim3((unsigned)f.blocks), dim3(1024), 0, s, f);
-  else
-    hipLaunchKernelGGL(bn_fwd_finalize_kernel<kBlock>, dim3((unsigned)f.blocks), dim3(kBlock), 0, s, f);
+__global__ __launch_bounds__(NT) void bn_fwd_finalize_wide_kernel(
+    const float* __restrict__ psum, const float* __restrict__ psq, int chunks, int C, int64_t M,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    float* run_mean, float* run_var, int64_t* num_batches, float* save_mean, float* save_invstd,
+    float* coef_a, float* coef_b) {
+  __shared__ double red[2][NT / 64];
+  const int c = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (c == 0 && threadIdx.x == 0 && num_batches) num_batches[0] += 1;
+  double s, q;
+  block_row_sum2<NT>(psum + (int64_t)c * chunks, psq + (int64_t)c * chunks, chunks, s, q);
+  if (lane == 0) { red[0][wave] = s; red[1][wave] = q; }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  s = 0.0;
+  q = 0.0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) { s += red[0][w]; q += red[1][w]; }
+  const double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.0f, bt = beta ? beta[c] : 0.0f;
+  const float a = g * invstd;
+  save_mean[c] = (float)mean;
+  save_invstd[c] = invstd;
+  coef_a[c] = a;
+  coef_b[c] = bt - (float)mean * a;
+  if (run_mean) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    run_mean[c] = (1.0f - momentum) * run_mean[c] + momentum * (float)mean;
+    run_var[c] = (1.0f - momentum) * run_var[c] + momentum * (float)unbiased;
+  }
 }
 
 // ---- forward apply: y = relu(x*a + b [+ r]) --------------------------------------------------
 // AFF: the residual is itself a BatchNorm input (a residual block's downsample branch): y =
 // relu(x*a + b + r*a2 + b2) - the downsample BN's output is never materialised.
-// FUSED: the launch also runs the finalize(s) f1 [, f2 (AFF)] in its first h.nfin blocks and the
-// apply blocks take their coefficients from them inside the launch (handoff.h); coef_a.. are
-// then f1's / f2's coefficient arrays.
-template <typename IO, bool RELU, bool RES, bool AFF = false, bool FUSED = false>
+template <typename IO, bool RELU, bool RES, bool AFF = false>
 __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(const void* __restrict__ x,
                                                               const void* __restrict__ res,
                                                               void* __restrict__ y,
-                                                              const float* coef_a,
-                                                              const float* coef_b,
+                                                              const float* __restrict__ coef_a,
+                                                              const float* __restrict__ coef_b,
                                                               int64_t M, int C, int rev,
-                                                              const float* coef_a2 = nullptr,
-                                                              const float* coef_b2 = nullptr,
-                                                              uint8_t* __restrict__ mask = nullptr,
-                                                              BnFwdFin f1 = {}, BnFwdFin f2 = {},
-                                                              BnHandoff h = {}) {
-  int bid = (int)blockIdx.x, nblk = (int)gridDim.x;
+                                                              const float* __restrict__ coef_a2 = nullptr,
+                                                              const float* __restrict__ coef_b2 = nullptr,
+                                                              uint8_t* __restrict__ mask = nullptr) {
   const int tpr = C >> 3, rpi = kBlock / tpr;
   const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
   float a[8], b[8], a2[8], b2[8];
-  if constexpr (FUSED) {  // in-launch finalize hand-off (handoff.h)
-    __shared__ double red[2 * (kBlock / 64)];
-    auto fin = [&](int i) {
-      if (i < f1.blocks) bn_fwd_finalize_block(f1, i, red, h.claim + i);
-      else bn_fwd_finalize_block(f2, i - f1.blocks, red, h.claim + i);
-    };
-    if (bid < h.nfin) {  // a finalize block: its coefficients go out as granules
-      if (!h.idle_fin) fin(bid);
-      return;
-    }
-    bid -= h.nfin;
-    nblk -= h.nfin;
-    // granules [a | b] (AFF: [a | b | a2 | b2], f2's follow f1's), staged in LDS for C <= kStageC
-    __shared__ float cs[4 * kStageC];
-    const bool stage = C <= kStageC;
-    handoff_acquire(f1.gran, (AFF ? 4 : 2) * C, cs, stage, h, fin);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = cg * 8 + k;
-      a[k] = stage ? cs[c] : get_gran(f1.gran + c, h.err);
-      b[k] = stage ? cs[C + c] : get_gran(f1.gran + C + c, h.err);
-      a2[k] = !AFF ? 0.f : (stage ? cs[2 * C + c] : get_gran(f1.gran + 2 * C + c, h.err));
-      b2[k] = !AFF ? 0.f : (stage ? cs[3 * C + c] : get_gran(f1.gran + 3 * C + c, h.err));
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      a[k] = coef_a[cg * 8 + k];
-      b[k] = coef_b[cg * 8 + k];
-      a2[k] = AFF ? coef_a2[cg * 8 + k] : 0.f;
-      b2[k] = AFF ? coef_b2[cg * 8 + k] : 0.f;
-    }
+  for (int k = 0; k < 8; ++k) {
+    a[k] = coef_a[cg * 8 + k];
+    b[k] = coef_b[cg * 8 + k];
+    a2[k] = AFF ? coef_a2[cg * 8 + k] : 0.f;
+    b2[k] = AFF ? coef_b2[cg * 8 + k] : 0.f;
   }
-  const int64_t stride = (int64_t)nblk * rpi;
-  for (int64_t rf = (int64_t)bid * rpi + rr; rf < M; rf += 2 * stride) {
+  const int64_t stride = (int64_t)gridDim.x * rpi;
+  for (int64_t rf = (int64_t)blockIdx.x * rpi + rr; rf < M; rf += 2 * stride) {
     const bool two = rf + stride < M;
     // rev: walk the rows last-to-first so the first blocks re-read what the stats pass
     // touched last (still resident in the 256 MB Infinity Cache / L2)
@@ -564,188 +466,42 @@ static void launch_bn_bwd_fin(const BnBwdFin& f, hipStream_t s) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel<kBlock>, dim3((unsigned)f.blocks), dim3(kBlock), 0, s, f);
 }
 
-// ---- in-launch finalize hand-off: granule arena (handoff.h) ---------------------------------
-// Per device: 1M granules (8 MB) + the error word.  bn_handoff_begin(stream) - once per training
-// step (ops/conv.py begin_step) - zeroes the granules the previous step drew (one memset node; a
-// captured step replays it) and opens the arena to fused launches on that stream; each fused
-// launch then draws a fresh range (2C / 3C granules per BatchNorm).  Launches on another stream,
-// outside a step, beyond the zeroed range, or with more than kMaxFinBlocks finalize blocks run
-// unfused.  DPT_BN_FUSE_FINALIZE=0 (or bn_set_fuse_finalize(0)) turns the fusion off.
-constexpr size_t kArenaGranules = (size_t)1 << 20;
-constexpr size_t kArenaBytes = kArenaGranules * sizeof(unsigned long long) + 64;
-constexpr size_t kMinZeroGranules = (size_t)1 << 16;
-constexpr int kMaxFinBlocks = 4096;
-struct HandoffArena {
-  unsigned long long* base = nullptr;
-  hipStream_t stream = nullptr;
-  size_t cursor = 0, zeroed = 0, wanted = 0;
-  bool active = false;
-};
-static HandoffArena g_arena[64];
-static std::mutex g_handoff_mu;
-static int g_bn_fuse_fin = -1;  // -1: from the environment (DPT_BN_FUSE_FINALIZE=1: on)
-static int g_bn_fused_wait_cap = 0;  // 0: the apply keeps its full grid (A/B knob)
-static int64_t g_fused_launches = 0;
-static int g_handoff_idle_fin = 0;  // test only: finalize blocks idle, apply blocks must help
-void bn_set_handoff_idle_finalizers(int on) { g_handoff_idle_fin = on ? 1 : 0; }  // host-side count (tests: the fused path did run)
-int64_t bn_handoff_fused_launches() { return g_fused_launches; }
-
-void bn_set_fuse_finalize(int on) { g_bn_fuse_fin = on ? 1 : 0; }
-static bool bn_fuse_enabled();
-int bn_fuse_finalize_enabled() { return bn_fuse_enabled() ? 1 : 0; }
-void bn_set_fused_apply_cap(int cap) { g_bn_fused_wait_cap = cap < 0 ? 0 : cap; }
-
-static bool bn_fuse_enabled() {
-  if (g_bn_fuse_fin < 0) {
-    const char* e = std::getenv("DPT_BN_FUSE_FINALIZE");
-    g_bn_fuse_fin = (e != nullptr && e[0] == '1') ? 1 : 0;
-  }
-  return g_bn_fuse_fin == 1;
-}
-
-static bool stream_capturing(hipStream_t s) {
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  return hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone;
-}
-
-void bn_handoff_begin(hipStream_t s) {
-  if (!bn_fuse_enabled()) return;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
-  std::lock_guard<std::mutex> lk(g_handoff_mu);
-  HandoffArena& A = g_arena[dev];
-  A.active = false;
-  const bool capturing = stream_capturing(s);
-  if (A.base == nullptr) {
-    if (capturing) return;
-    void* b = nullptr;
-    if (hipMalloc(&b, kArenaBytes) != hipSuccess) return;
-    if (hipMemset(b, 0, kArenaBytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-      (void)hipFree(b);
-      return;
-    }
-    A.base = static_cast<unsigned long long*>(b);
-    A.zeroed = kArenaGranules;
-  } else {
-    if (A.stream != s) {
-      // the previous step's launches ran on another stream: order the zeroing after them
-      if (capturing) return;
-      hipEvent_t ev;
-      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
-      const bool ok = hipEventRecord(ev, A.stream) == hipSuccess && hipStreamWaitEvent(s, ev, 0) == hipSuccess;
-      (void)hipEventDestroy(ev);
-      if (!ok) return;
-    }
-    // what the previous step drew, and at least 512 KB (a first step of a new shape still fuses)
-    size_t n = A.wanted > kMinZeroGranules ? A.wanted : kMinZeroGranules;
-    if (n > kArenaGranules) n = kArenaGranules;
-    n = (n + 1) & ~(size_t)1;  // whole 16-byte units from the allocation's start
-    if (n > 0 && hipMemsetAsync(A.base, 0, n * sizeof(unsigned long long), s) != hipSuccess) return;
-    A.zeroed = n;
-  }
-  A.stream = s;
-  A.cursor = 0;
-  A.wanted = 0;
-  A.active = true;
-}
-
-// A granule range for one fused launch: ngran coefficient granules, then nfin claim words (zeroed
-// with them), or false: the launch runs unfused.
-static bool handoff_take(hipStream_t s, int nfin, size_t ngran, BnHandoff& h, unsigned long long** gran) {
-  if (g_bn_skip_finalize || nfin <= 0 || nfin > kMaxFinBlocks || !bn_fuse_enabled()) return false;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-  std::lock_guard<std::mutex> lk(g_handoff_mu);
-  HandoffArena& A = g_arena[dev];
-  if (!A.active || A.stream != s) return false;
-  ngran = (ngran + 1) & ~(size_t)1;
-  const size_t total = ngran + (((size_t)nfin + 3) / 4) * 2;  // claims: 4 per 16 bytes
-  A.wanted += total;
-  if (A.cursor + total > A.zeroed) return false;
-  *gran = A.base + A.cursor;
-  h.claim = reinterpret_cast<unsigned*>(A.base + A.cursor + ngran);
-  A.cursor += total;
-  ++g_fused_launches;
-  h.err = reinterpret_cast<unsigned*>(A.base + kArenaGranules);
-  h.nfin = nfin;
-  h.idle_fin = g_handoff_idle_fin;
-  return true;
-}
-
-// apply blocks of a fused launch (the A/B knob bn_set_fused_apply_cap caps them)
-static int fused_apply_blocks(int apply, int nfin) {
-  (void)nfin;
-  return g_bn_fused_wait_cap > 0 && apply > g_bn_fused_wait_cap ? g_bn_fused_wait_cap : apply;
-}
-
-int64_t bn_handoff_errors() {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || g_arena[dev].base == nullptr) return 0;
-  unsigned v = 0;
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpy(&v, g_arena[dev].base + kArenaGranules, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return (int64_t)v;
-}
-
 // dx = k1*dz + k2*(x - mean) + k3, dz = dy*(y>0) recomputed (RELU; mask from x if MX) or
-// read back (FROM_DZ).  Roles in the grid: [FUSED: finalize f1 | apply | carried reduce].
-template <typename IO, bool RELU, bool FROM_DZ, bool MX, bool FUSED = false>
+// read back (FROM_DZ).
+template <typename IO, bool RELU, bool FROM_DZ, bool MX>
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const void* __restrict__ dy,
                                                               const void* __restrict__ y,
                                                               const void* __restrict__ x,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ coef,
-                                                              const float* k1,
-                                                              const float* k2,
-                                                              const float* k3, void* dx,
-                                                              int64_t M, int C, int rev, ReduceCarry rc,
-                                                              BnBwdFin f1 = {}, BnHandoff h = {}) {
-  int bid = (int)blockIdx.x, nblk = (int)gridDim.x - rc.blocks;  // apply blocks: [0, nblk)
-  __shared__ double red[2 * (kBlock / 64)];
-  auto fin = [&](int i) { bn_bwd_finalize_block<kBlock>(f1, i, red); };  // idempotent: no claim
-  if constexpr (FUSED) {
-    if (bid < h.nfin) {  // a finalize block: k1..k3 go out as granules (handoff.h)
-      if (!h.idle_fin) fin(bid);
+                                                              const float* __restrict__ k1,
+                                                              const float* __restrict__ k2,
+                                                              const float* __restrict__ k3, void* dx,
+                                                              int64_t M, int C, int rev, ReduceCarry rc) {
+  if (rc.blocks) {  // carried backward-weight reduce (carry.h): the grid's last rc.blocks blocks
+    const int napply = (int)gridDim.x - rc.blocks;
+    if ((int)blockIdx.x >= napply) {
+      __shared__ float4 red[kBlock];
+      carry_reduce(rc, (int)blockIdx.x - napply, red);
       return;
     }
-    bid -= h.nfin;
-    nblk -= h.nfin;
-  }
-  if (bid >= nblk) {  // carried backward-weight reduce (carry.h): the last rc.blocks blocks
-    __shared__ float4 cred[kBlock];
-    carry_reduce(rc, bid - nblk, cred);
-    return;
   }
   const int tpr = C >> 3, rpi = kBlock / tpr;
+  // grid-stride over the apply blocks only (carry blocks excluded)
+  const int apply_grid = (int)gridDim.x - rc.blocks;
   const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
   float mu[8], c1[8], c2[8], c3[8], fa[8], fb[8];
-  if constexpr (FUSED) {
-    __shared__ float cs[3 * kStageC];  // granules [k1 | k2 | k3]
-    const bool stage = C <= kStageC;
-    handoff_acquire(f1.gran, 3 * C, cs, stage, h, fin);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = cg * 8 + k;
-      c1[k] = stage ? cs[c] : get_gran(f1.gran + c, h.err);
-      c2[k] = stage ? cs[C + c] : get_gran(f1.gran + C + c, h.err);
-      c3[k] = stage ? cs[2 * C + c] : get_gran(f1.gran + 2 * C + c, h.err);
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      c1[k] = k1[cg * 8 + k];
-      c2[k] = k2[cg * 8 + k];
-      c3[k] = k3[cg * 8 + k];
-    }
-  }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     mu[k] = mean[cg * 8 + k];
+    c1[k] = k1[cg * 8 + k];
+    c2[k] = k2[cg * 8 + k];
+    c3[k] = k3[cg * 8 + k];
     fa[k] = MX ? coef[cg * 8 + k] : 0.f;
     fb[k] = MX ? coef[C + cg * 8 + k] : 0.f;
   }
-  const int64_t stride = (int64_t)nblk * rpi;
-  for (int64_t rf = (int64_t)bid * rpi + rr; rf < M; rf += stride) {
+  const int64_t stride = (int64_t)apply_grid * rpi;
+  for (int64_t rf = (int64_t)blockIdx.x * rpi + rr; rf < M; rf += stride) {
     const int64_t r = rev ? M - 1 - rf : rf;  // see bn_fwd_apply_kernel
     float g[8], xv[8], o[8];
     bool m[8];
@@ -763,60 +519,28 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const void* __rest
 
 // Block tail with a downsample branch (ops/bn.py _BN2AddReLUPair): one pass over dz writes both
 // BatchNorms' input gradients, dx = k1*dz + k2*(x - mean) + k3 and dx2 = j1*dz + j2*(x2 - mean2) + j3.
-template <typename IO, bool FUSED = false>
+template <typename IO>
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply2_kernel(const void* __restrict__ dz,
                                                                const void* __restrict__ x,
                                                                const void* __restrict__ x2,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ mean2,
-                                                               const float* k,
-                                                               const float* j, void* dx, void* dx2,
-                                                               int64_t M, int C, int rev, BnBwdFin f1 = {},
-                                                               BnBwdFin f2 = {}, BnHandoff h = {}) {
-  int bid = (int)blockIdx.x, nblk = (int)gridDim.x;
+                                                               const float* __restrict__ k,
+                                                               const float* __restrict__ j, void* dx, void* dx2,
+                                                               int64_t M, int C, int rev) {
   const int tpr = C >> 3, rpi = kBlock / tpr;
   const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
   float mu[8], mu2[8], c1[8], c2[8], c3[8], e1[8], e2[8], e3[8];
-  if constexpr (FUSED) {  // in-launch finalize hand-off (handoff.h)
-    __shared__ double red[2 * (kBlock / 64)];
-    auto fin = [&](int i) {  // idempotent: no claim
-      if (i < f1.blocks) bn_bwd_finalize_block<kBlock>(f1, i, red);
-      else bn_bwd_finalize_block<kBlock>(f2, i - f1.blocks, red);
-    };
-    if (bid < h.nfin) {
-      if (!h.idle_fin) fin(bid);
-      return;
-    }
-    bid -= h.nfin;
-    nblk -= h.nfin;
-    __shared__ float cs[6 * kStageC];  // granules [k1 | k2 | k3] of the tail, then of the downsample
-    const bool stage = C <= kStageC;
-    handoff_acquire(f1.gran, 6 * C, cs, stage, h, fin);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int c = cg * 8 + q;
-      c1[q] = stage ? cs[c] : get_gran(f1.gran + c, h.err);
-      c2[q] = stage ? cs[C + c] : get_gran(f1.gran + C + c, h.err);
-      c3[q] = stage ? cs[2 * C + c] : get_gran(f1.gran + 2 * C + c, h.err);
-      e1[q] = stage ? cs[3 * C + c] : get_gran(f1.gran + 3 * C + c, h.err);
-      e2[q] = stage ? cs[4 * C + c] : get_gran(f1.gran + 4 * C + c, h.err);
-      e3[q] = stage ? cs[5 * C + c] : get_gran(f1.gran + 5 * C + c, h.err);
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int c = cg * 8 + q;
-      c1[q] = k[c]; c2[q] = k[C + c]; c3[q] = k[2 * C + c];
-      e1[q] = j[c]; e2[q] = j[C + c]; e3[q] = j[2 * C + c];
-    }
-  }
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    mu[q] = mean[cg * 8 + q];
-    mu2[q] = mean2[cg * 8 + q];
+    const int c = cg * 8 + q;
+    mu[q] = mean[c];
+    mu2[q] = mean2[c];
+    c1[q] = k[c]; c2[q] = k[C + c]; c3[q] = k[2 * C + c];
+    e1[q] = j[c]; e2[q] = j[C + c]; e3[q] = j[2 * C + c];
   }
-  const int64_t stride = (int64_t)nblk * rpi;
-  for (int64_t rf = (int64_t)bid * rpi + rr; rf < M; rf += stride) {
+  const int64_t stride = (int64_t)gridDim.x * rpi;
+  for (int64_t rf = (int64_t)blockIdx.x * rpi + rr; rf < M; rf += stride) {
     const int64_t r = rev ? M - 1 - rf : rf;
     const int64_t off = r * C + cg * 8;
     float g[8], xv[8], x2v[8], o[8], o2[8];
@@ -868,53 +592,17 @@ BnGeometry bn_geometry(int64_t M, int64_t C) {
   return g;
 }
 
-// Forward apply.  fin: the finalize producing a/b (nullptr: coefficients already computed) - it
-// runs inside this launch (handoff.h) when a hand-off slot is available, else as its own launch.
 template <typename IO>
 static void fwd_apply_dispatch(bool relu, bool res, const void* x, const void* r, void* y, const float* a,
-                               const float* b, int64_t M, int C, int blocks, hipStream_t s, uint8_t* mask = nullptr,
-                               const BnFwdFin* fin = nullptr) {
-  dim3 bl(kBlock);
+                               const float* b, int64_t M, int C, int blocks, hipStream_t s, uint8_t* mask = nullptr) {
+  dim3 gr(blocks), bl(kBlock);
   const int rev = kBnReverse;
-  BnHandoff h;
-  BnFwdFin fg = fin != nullptr ? *fin : BnFwdFin{};
-  if (fin != nullptr && !(fin->wide && fin->chunks > kFinHugeChunks) && handoff_take(s, fin->blocks, 2 * (size_t)C, h, &fg.gran)) {
-    dim3 gr((unsigned)(fused_apply_blocks(blocks, h.nfin) + h.nfin));
-    const BnFwdFin none;
-#define DPT_FWD_FUSED(RL, RS)                                                                                   \
-  hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, RL, RS, false, true>), gr, bl, 0, s, x, r, y, a, b, M, C, rev, nullptr, \
-                     nullptr, mask, fg, none, h)
-    if (relu && res) DPT_FWD_FUSED(true, true);
-    else if (relu) DPT_FWD_FUSED(true, false);
-    else if (res) DPT_FWD_FUSED(false, true);
-    else DPT_FWD_FUSED(false, false);
-#undef DPT_FWD_FUSED
-    return;
-  }
-  if (fin != nullptr && !g_bn_skip_finalize)
-    launch_bn_fwd_fin(*fin, s);
-  dim3 gr(blocks);
   if (relu && res)
     hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, true, true>), gr, bl, 0, s, x, r, y, a, b, M, C, rev, nullptr, nullptr,
                        mask);
   else if (relu) hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, true, false>), gr, bl, 0, s, x, r, y, a, b, M, C, rev);
   else if (res) hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, false, true>), gr, bl, 0, s, x, r, y, a, b, M, C, rev);
   else hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, false, false>), gr, bl, 0, s, x, r, y, a, b, M, C, rev);
-}
-
-static void fwd_finalize_then_apply(int dtype, const BnFwdFin& f, const void* x, const void* res, void* y, int64_t M,
-                                    int64_t C, bool relu, hipStream_t s, uint8_t* mask) {
-  if (y == nullptr) {  // statistics only (the apply is fused elsewhere)
-    if (!g_bn_skip_finalize)
-      launch_bn_fwd_fin(f, s);
-    return;
-  }
-  BnGeometry g = bn_geometry(M, C);
-  switch (dtype) {
-    case 0: fwd_apply_dispatch<F32>(relu, res != nullptr, x, res, y, f.coef_a, f.coef_b, M, (int)C, g.apply_blocks, s, mask, &f); break;
-    case 1: fwd_apply_dispatch<BF16>(relu, res != nullptr, x, res, y, f.coef_a, f.coef_b, M, (int)C, g.apply_blocks, s, mask, &f); break;
-    default: fwd_apply_dispatch<F16>(relu, res != nullptr, x, res, y, f.coef_a, f.coef_b, M, (int)C, g.apply_blocks, s, mask, &f); break;
-  }
 }
 
 void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
@@ -932,10 +620,14 @@ void launch_bn_fwd_train(int dtype, const void* x, const void* res, void* y, int
     case 1: hipLaunchKernelGGL(bn_fwd_stats_kernel<BF16>, dim3(g.chunks), bl, 0, s, x, M, (int)C, g.rows_per_chunk, g.chunks, psum, psq); break;
     default: hipLaunchKernelGGL(bn_fwd_stats_kernel<F16>, dim3(g.chunks), bl, 0, s, x, M, (int)C, g.rows_per_chunk, g.chunks, psum, psq); break;
   }
-  // <= 512 partials per channel here: the half-wave finalize
-  const BnFwdFin f = make_bn_fwd_fin(psum, psq, g.chunks, (int)C, M, gamma, beta, eps, momentum, run_mean, run_var,
-                                     num_batches, save_mean, save_invstd, ca, cb, 0);
-  fwd_finalize_then_apply(dtype, f, x, res, y, M, C, relu, s, mask);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), bl, 0, s, psum, psq, g.chunks, (int)C, M,
+                     gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd, ca, cb);
+  if (y == nullptr) return;  // statistics only (the apply is fused elsewhere)
+  switch (dtype) {
+    case 0: fwd_apply_dispatch<F32>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s, mask); break;
+    case 1: fwd_apply_dispatch<BF16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s, mask); break;
+    default: fwd_apply_dispatch<F16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s, mask); break;
+  }
 }
 
 // BN forward whose statistics were already summed by the producing convolution's epilogue
@@ -945,46 +637,30 @@ void launch_bn_fwd_from_partials(int dtype, const void* x, const void* res, void
                                  const float* beta, float eps, float momentum, float* run_mean, float* run_var,
                                  int64_t* num_batches, float* save_mean, float* save_invstd, float* save_coef,
                                  bool relu, hipStream_t s, uint8_t* mask) {
-  const BnFwdFin f = make_bn_fwd_fin(psum, psq, chunks, (int)C, M, gamma, beta, eps, momentum, run_mean, run_var,
-                                     num_batches, save_mean, save_invstd, save_coef, save_coef + C);
-  fwd_finalize_then_apply(dtype, f, x, res, y, M, C, relu, s, mask);
-}
-
-// Residual-block tail with a downsample BatchNorm, both from conv-epilogue partials:
-// y = relu(bn1(x) + bn2(x2)) - both finalizes and the apply in one launch when fused.
-void launch_bn2_fwd_from_partials(int dtype, const void* x, const void* x2, void* y, int64_t M, int64_t C,
-                                  const BnFwdArgs& a1, const BnFwdArgs& a2, hipStream_t s, uint8_t* mask) {
-  BnFwdFin f1 = make_bn_fwd_fin(a1.psum, a1.psq, a1.chunks, (int)C, M, a1.gamma, a1.beta, a1.eps, a1.momentum,
-                                      a1.run_mean, a1.run_var, a1.num_batches, a1.save_mean, a1.save_invstd,
-                                      a1.save_coef, a1.save_coef + C);
-  BnFwdFin f2 = make_bn_fwd_fin(a2.psum, a2.psq, a2.chunks, (int)C, M, a2.gamma, a2.beta, a2.eps, a2.momentum,
-                                      a2.run_mean, a2.run_var, a2.num_batches, a2.save_mean, a2.save_invstd,
-                                      a2.save_coef, a2.save_coef + C);
-  BnHandoff h;
-  unsigned long long* gr4 = nullptr;  // [a | b] of bn1, then [a | b] of bn2
-  const bool huge = (f1.wide && f1.chunks > kFinHugeChunks) || (f2.wide && f2.chunks > kFinHugeChunks);
-  if (!huge && handoff_take(s, f1.blocks + f2.blocks, 4 * (size_t)C, h, &gr4)) {
-    f1.gran = gr4;
-    f2.gran = gr4 + 2 * C;
-    BnGeometry g = bn_geometry(M, C);
-    dim3 gr((unsigned)(fused_apply_blocks(g.apply_blocks, h.nfin) + h.nfin));
-    dim3 bl(kBlock);
-#define DPT_AFF_FUSED(IO)                                                                                          \
-  hipLaunchKernelGGL((bn_fwd_apply_kernel<IO, true, true, true, true>), gr, bl, 0, s, x, x2, y, f1.coef_a, f1.coef_b, \
-                     M, (int)C, kBnReverse, f2.coef_a, f2.coef_b, mask, f1, f2, h)
-    switch (dtype) {
-      case 0: DPT_AFF_FUSED(F32); break;
-      case 1: DPT_AFF_FUSED(BF16); break;
-      default: DPT_AFF_FUSED(F16); break;
-    }
-#undef DPT_AFF_FUSED
-    return;
+  BnGeometry g = bn_geometry(M, C);
+  float* ca = save_coef;
+  float* cb = ca + C;
+  if (g_bn_skip_finalize) {
+  } else if (chunks > 256) {
+#define DPT_FWD_FIN(NT)                                                                                        \
+  hipLaunchKernelGGL(bn_fwd_finalize_wide_kernel<NT>, dim3((unsigned)C), dim3(NT), 0, s, psum, psq, chunks, (int)C, \
+                     M, gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd, ca, cb)
+    // tens of thousands of partials per channel (the ResNet stem's conv epilogue: 25,088 at
+    // batch 256, 64 channels = 64 blocks): 1024 threads, 4x the loads in flight of this
+    // latency-bound sweep
+    if (chunks > 8192) DPT_FWD_FIN(1024);
+    else DPT_FWD_FIN(kBlock);
+#undef DPT_FWD_FIN
+  } else
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)((C + 7) / 8)), dim3(kBlock), 0, s, psum, psq, chunks,
+                       (int)C, M, gamma, beta, eps, momentum, run_mean, run_var, num_batches, save_mean, save_invstd,
+                       ca, cb);
+  if (y == nullptr) return;  // statistics only (the apply is fused elsewhere)
+  switch (dtype) {
+    case 0: fwd_apply_dispatch<F32>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s, mask); break;
+    case 1: fwd_apply_dispatch<BF16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s, mask); break;
+    default: fwd_apply_dispatch<F16>(relu, res != nullptr, x, res, y, ca, cb, M, (int)C, g.apply_blocks, s, mask); break;
   }
-  if (!g_bn_skip_finalize) {
-    launch_bn_fwd_fin(f1, s);
-    launch_bn_fwd_fin(f2, s);
-  }
-  launch_bn_apply_aff(dtype, x, x2, y, M, C, f1.coef_a, f1.coef_b, f2.coef_a, f2.coef_b, s, mask);
 }
 
 void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
@@ -1019,39 +695,19 @@ static void bwd_stats_dispatch(bool relu, const void* dy, const void* dy2, const
 #undef DPT_BN_STATS
 }
 
-// Backward apply, carried reduce blocks (rc) appended.  fin: the finalize producing k1..k3 - it
-// runs inside this launch when a hand-off slot is available, else as its own launch first.
-template <typename IO, bool RELU, bool FROM_DZ, bool MX>
-static void bwd_apply_launch(int napply, const void* dy, const void* y, const void* x, const float* mean,
-                             const float* coef, const float* k1, const float* k2, const float* k3, void* dx, int64_t M,
-                             int C, const ReduceCarry& rc, const BnBwdFin* fin, hipStream_t s) {
-  dim3 bl(kBlock);
-  BnHandoff h;
-  BnBwdFin fg = fin != nullptr ? *fin : BnBwdFin{};
-  if (fin != nullptr && handoff_take(s, fin->blocks, 3 * (size_t)C, h, &fg.gran)) {
-    const int na = fused_apply_blocks(napply, h.nfin);
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, RELU, FROM_DZ, MX, true>), dim3((unsigned)(h.nfin + na + rc.blocks)), bl,
-                       0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse, rc, fg, h);
-    return;
-  }
-  if (fin != nullptr) launch_bn_bwd_fin(*fin, s);
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, RELU, FROM_DZ, MX>), dim3((unsigned)(napply + rc.blocks)), bl, 0, s, dy, y,
-                     x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse, rc);
-}
-
 template <typename IO>
 static void bwd_dispatch(bool relu, const void* dy, const void* dy2, const void* y, const void* x,
                          const float* mean, const float* coef, int64_t M, int C, const BnGeometry& g, float* p1,
                          float* p2, const float* gamma, const float* invstd, float* dgamma, float* dbeta,
                          float* k1, float* k2, float* k3, void* dx, void* dz, hipStream_t s) {
+  dim3 bl(kBlock);
   bwd_stats_dispatch<IO, kBnBwdUnroll>(relu, dy, dy2, y, x, mean, coef, M, C, g, p1, p2, dz, s);
-  const BnBwdFin f = make_bn_bwd_fin(p1, p2, g.chunks, C, M, gamma, invstd, dgamma, dbeta, k1, k2, k3, 0);
-  const int ga = g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2;
-  const ReduceCarry none;
-  if (dz != nullptr) bwd_apply_launch<IO, false, true, false>(ga, dz, y, x, mean, coef, k1, k2, k3, dx, M, C, none, &f, s);
-  else if (relu && coef) bwd_apply_launch<IO, true, false, true>(ga, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, none, &f, s);
-  else if (relu) bwd_apply_launch<IO, true, false, false>(ga, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, none, &f, s);
-  else bwd_apply_launch<IO, false, false, false>(ga, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, none, &f, s);
+  launch_bn_bwd_fin(make_bn_bwd_fin(p1, p2, g.chunks, C, M, gamma, invstd, dgamma, dbeta, k1, k2, k3, 0), s);
+  dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
+  if (dz != nullptr) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, true, false>), ga, bl, 0, s, dz, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse, ReduceCarry{});
+  else if (relu && coef) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false, true>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse, ReduceCarry{});
+  else if (relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, true, false, false>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse, ReduceCarry{});
+  else hipLaunchKernelGGL((bn_bwd_apply_kernel<IO, false, false, false>), ga, bl, 0, s, dy, y, x, mean, coef, k1, k2, k3, dx, M, C, kBnReverse, ReduceCarry{});
 }
 
 // dz: if non-null, receives dz = (dy [+ dy2]) * relu_mask (the residual-path gradient);
@@ -1073,47 +729,48 @@ void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, co
   }
 }
 
+// Backward finalize over MANY [C][chunks] partials (the dgrad epilogue of the consuming conv
+// writes one per 128 rows): one 256-thread block per channel, fp64 block reduce.
+
 // BN+ReLU backward whose statistics (s1 = sum dz, s2 = sum dz*(x - mean), dz = dy * relu mask)
 // were summed by the dgrad epilogue of the conv that consumed this BN's output: [C][chunks]
 // partials -> finalize -> apply (mask recomputed from x and the forward coefficients).
-static void bn_bwd_apply_pre_fin(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* mean,
-                                 const float* coef, const float* kbuf, void* dx, hipStream_t s, bool from_dz,
-                                 const BnBwdFin* fin) {
+void launch_bn_bwd_apply_pre(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* mean,
+                             const float* coef, const float* kbuf, void* dx, hipStream_t s, bool from_dz) {
   BnGeometry g = bn_geometry(M, C);
   const float* k1 = kbuf;
   const float* k2 = k1 + C;
   const float* k3 = k2 + C;
+  dim3 bl(kBlock);
   ReduceCarry rc;
-  const int ga = g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2;
-  take_attached_reduce(rc);
-  const int Ci = (int)C;
+  const int ga = (g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2) +
+                 take_attached_reduce(rc);
   if (from_dz) {  // dy is already the masked gradient dz (block-tail BN, ops/conv.py BNR)
     switch (dtype) {
-      case 0: bwd_apply_launch<F32, false, true, false>(ga, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, Ci, rc, fin, s); break;
-      case 1: bwd_apply_launch<BF16, false, true, false>(ga, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, Ci, rc, fin, s); break;
-      default: bwd_apply_launch<F16, false, true, false>(ga, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, Ci, rc, fin, s); break;
+      case 0: hipLaunchKernelGGL((bn_bwd_apply_kernel<F32, false, true, false>), dim3(ga), bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse, rc); break;
+      case 1: hipLaunchKernelGGL((bn_bwd_apply_kernel<BF16, false, true, false>), dim3(ga), bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse, rc); break;
+      default: hipLaunchKernelGGL((bn_bwd_apply_kernel<F16, false, true, false>), dim3(ga), bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse, rc); break;
     }
     return;
   }
   switch (dtype) {
-    case 0: bwd_apply_launch<F32, true, false, true>(ga, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, Ci, rc, fin, s); break;
-    case 1: bwd_apply_launch<BF16, true, false, true>(ga, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, Ci, rc, fin, s); break;
-    default: bwd_apply_launch<F16, true, false, true>(ga, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, Ci, rc, fin, s); break;
+    case 0: hipLaunchKernelGGL((bn_bwd_apply_kernel<F32, true, false, true>), dim3(ga), bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse, rc); break;
+    case 1: hipLaunchKernelGGL((bn_bwd_apply_kernel<BF16, true, false, true>), dim3(ga), bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse, rc); break;
+    default: hipLaunchKernelGGL((bn_bwd_apply_kernel<F16, true, false, true>), dim3(ga), bl, 0, s, dy, nullptr, x, mean, coef, k1, k2, k3, dx, M, (int)C, kBnReverse, rc); break;
   }
-}
-
-void launch_bn_bwd_apply_pre(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* mean,
-                             const float* coef, const float* kbuf, void* dx, hipStream_t s, bool from_dz) {
-  bn_bwd_apply_pre_fin(dtype, dy, x, M, C, mean, coef, kbuf, dx, s, from_dz, nullptr);
 }
 
 void launch_bn_bwd_from_partials(int dtype, const void* dy, const void* x, int64_t M, int64_t C, const float* gamma,
                                  const float* mean, const float* invstd, const float* coef, const float* p1,
                                  const float* p2, int chunks, float* dgamma, float* dbeta, void* dx, float* kbuf,
                                  hipStream_t s, bool from_dz) {
-  const BnBwdFin f = make_bn_bwd_fin(p1, p2, chunks, (int)C, M, gamma, invstd, dgamma, dbeta, kbuf, kbuf + C,
-                                     kbuf + 2 * C, -1);
-  bn_bwd_apply_pre_fin(dtype, dy, x, M, C, mean, coef, kbuf, dx, s, from_dz, &f);
+  BnGeometry g = bn_geometry(M, C);
+  float* k1 = kbuf;
+  float* k2 = k1 + C;
+  float* k3 = k2 + C;
+  dim3 bl(kBlock);
+  launch_bn_bwd_fin(make_bn_bwd_fin(p1, p2, chunks, (int)C, M, gamma, invstd, dgamma, dbeta, k1, k2, k3, -1), s);
+  launch_bn_bwd_apply_pre(dtype, dy, x, M, C, mean, coef, kbuf, dx, s, from_dz);
 }
 
 void launch_bn_apply_aff(int dtype, const void* x, const void* x2, void* y, int64_t M, int64_t C, const float* a,
@@ -1139,32 +796,16 @@ void launch_bn2_bwd_from_partials(int dtype, const void* dz, const void* x, cons
   float* k = kbuf;          // [3C] tail
   float* j = kbuf + 3 * C;  // [3C] downsample
   dim3 bl(kBlock);
-  BnBwdFin f1 = make_bn_bwd_fin(p1, p2, chunks, (int)C, M, gamma, invstd, dgamma, dbeta, k, k + C, k + 2 * C, -1);
-  BnBwdFin f2 = make_bn_bwd_fin(p1, p3, chunks, (int)C, M, gamma2, invstd2, dgamma2, dbeta2, j, j + C, j + 2 * C, -1);
-  const int ga = g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2;
-  BnHandoff h;
-  unsigned long long* gr6 = nullptr;  // [k1 | k2 | k3] of the tail, then of the downsample
-  if (handoff_take(s, f1.blocks + f2.blocks, 6 * (size_t)C, h, &gr6)) {
-    f1.gran = gr6;
-    f2.gran = gr6 + 3 * C;
-    dim3 gr((unsigned)(fused_apply_blocks(ga, h.nfin) + h.nfin));
-#define DPT_APPLY2_FUSED(IO)                                                                                       \
-  hipLaunchKernelGGL((bn_bwd_apply2_kernel<IO, true>), gr, bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, \
-                     kBnReverse, f1, f2, h)
-    switch (dtype) {
-      case 0: DPT_APPLY2_FUSED(F32); break;
-      case 1: DPT_APPLY2_FUSED(BF16); break;
-      default: DPT_APPLY2_FUSED(F16); break;
-    }
-#undef DPT_APPLY2_FUSED
-    return;
-  }
+  const BnBwdFin f1 = make_bn_bwd_fin(p1, p2, chunks, (int)C, M, gamma, invstd, dgamma, dbeta, k, k + C, k + 2 * C, -1);
+  const BnBwdFin f2 =
+      make_bn_bwd_fin(p1, p3, chunks, (int)C, M, gamma2, invstd2, dgamma2, dbeta2, j, j + C, j + 2 * C, -1);
   if (!g_bn_skip_finalize)
     hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((unsigned)(f1.blocks + f2.blocks)), dim3(kBlock), 0, s, f1, f2);
+  dim3 ga(g.apply_blocks * 2 > kBnBwdApplyMax ? kBnBwdApplyMax : g.apply_blocks * 2);
   switch (dtype) {
-    case 0: hipLaunchKernelGGL(bn_bwd_apply2_kernel<F32>, dim3(ga), bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, kBnReverse); break;
-    case 1: hipLaunchKernelGGL(bn_bwd_apply2_kernel<BF16>, dim3(ga), bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, kBnReverse); break;
-    default: hipLaunchKernelGGL(bn_bwd_apply2_kernel<F16>, dim3(ga), bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, kBnReverse); break;
+    case 0: hipLaunchKernelGGL(bn_bwd_apply2_kernel<F32>, ga, bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, kBnReverse); break;
+    case 1: hipLaunchKernelGGL(bn_bwd_apply2_kernel<BF16>, ga, bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, kBnReverse); break;
+    default: hipLaunchKernelGGL(bn_bwd_apply2_kernel<F16>, ga, bl, 0, s, dz, x, x2, mean, mean2, k, j, dx, dx2, M, (int)C, kBnReverse); break;
   }
 }
 

@@ -15,7 +15,6 @@
 #pragma once
 
 #include "common.h"
-#include "handoff.h"
 
 namespace dpt {
 
@@ -85,25 +84,28 @@ __device__ __forceinline__ void carry_reduce(const ReduceCarry& r, int bid, void
 
 // Sum `chunks` partials of channel c with 32 lanes (one half-wave) in fp64.  Eight
 // independent loads in flight per lane: the partials are L2-resident, so this loop is
-// latency-bound, not bandwidth-bound.  One fp64 accumulator pair (the adds are nothing next to
-// the load latency; eight pairs cost 24 VGPRs, which the fused finalize+apply kernels share with
-// the apply - handoff.h).
+// latency-bound, not bandwidth-bound.
 __device__ __forceinline__ void half_wave_sum2(const float* p1, const float* p2, int64_t c, int chunks,
                                                int part, double& s1, double& s2) {
   constexpr int U = 8;
+  double a[U], b[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) { a[u] = 0.0; b[u] = 0.0; }
   const float* q1 = p1 + c * chunks;
   const float* q2 = p2 + c * chunks;
-  s1 = 0.0;
-  s2 = 0.0;
   int k = part;
   for (; k + 32 * (U - 1) < chunks; k += 32 * U) {
     float x[U], y[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) { x[u] = q1[k + 32 * u]; y[u] = q2[k + 32 * u]; }
 #pragma unroll
-    for (int u = 0; u < U; ++u) { s1 += (double)x[u]; s2 += (double)y[u]; }
+    for (int u = 0; u < U; ++u) { a[u] += (double)x[u]; b[u] += (double)y[u]; }
   }
-  for (; k < chunks; k += 32) { s1 += (double)q1[k]; s2 += (double)q2[k]; }
+  for (; k < chunks; k += 32) { a[0] += (double)q1[k]; b[0] += (double)q2[k]; }
+  s1 = 0.0;
+  s2 = 0.0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) { s1 += a[u]; s2 += b[u]; }
 #pragma unroll
   for (int off = 16; off > 0; off >>= 1) {
     s1 += __shfl_xor(s1, off, 64);
@@ -119,21 +121,26 @@ template <int NT = kBlock>
 __device__ __forceinline__ void block_row_sum2(const float* __restrict__ q1, const float* __restrict__ q2,
                                                int chunks, double& s, double& q) {
   constexpr int U = 8;
-  s = 0.0;
-  q = 0.0;
+  double a[U], b[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) { a[u] = 0.0; b[u] = 0.0; }
   int k = threadIdx.x;
   for (; k + (U - 1) * NT < chunks; k += U * NT) {
     float x[U], y[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) { x[u] = q1[k + u * NT]; y[u] = q2[k + u * NT]; }
 #pragma unroll
-    for (int u = 0; u < U; ++u) { s += (double)x[u]; q += (double)y[u]; }
+    for (int u = 0; u < U; ++u) { a[u] += (double)x[u]; b[u] += (double)y[u]; }
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int kk = k + u * NT;
-    if (kk < chunks) { s += (double)q1[kk]; q += (double)q2[kk]; }
+    if (kk < chunks) { a[u] += (double)q1[kk]; b[u] += (double)q2[kk]; }
   }
+  s = 0.0;
+  q = 0.0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) { s += a[u]; q += b[u]; }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     s += __shfl_xor(s, off, 64);
@@ -159,7 +166,6 @@ struct BnBwdFin {
   float* k3 = nullptr;
   int wide = 0;
   int blocks = 0;  // carry blocks (0: none)
-  unsigned long long* gran = nullptr;  // in-launch hand-off (handoff.h): k1 | k2 | k3 granules [3C]
 };
 
 __host__ __device__ inline int bn_bwd_fin_wide(int chunks) { return chunks > 256 ? 1 : 0; }
@@ -175,15 +181,9 @@ __device__ __forceinline__ void bn_bwd_fin_store(const BnBwdFin& f, int64_t c, d
   if (f.dgamma) f.dgamma[c] = (float)(s2 * is);
   if (f.dbeta) f.dbeta[c] = (float)s1;
   const double a = g * is;
-  const float v1 = (float)a, v2 = (float)(-a * is * is * s2 / (double)f.M), v3 = (float)(-a * s1 / (double)f.M);
-  f.k1[c] = v1;
-  f.k2[c] = v2;
-  f.k3[c] = v3;
-  if (f.gran) {  // handed to the apply blocks of this launch (handoff.h)
-    put_gran(f.gran + c, v1);
-    put_gran(f.gran + f.C + c, v2);
-    put_gran(f.gran + 2 * f.C + c, v3);
-  }
+  f.k1[c] = (float)a;
+  f.k2[c] = (float)(-a * is * is * s2 / (double)f.M);
+  f.k3[c] = (float)(-a * s1 / (double)f.M);
 }
 
 // Block `bid` of the finalize (NT threads - wide only, kBlock otherwise; lds: >= NT bytes).
@@ -197,21 +197,20 @@ __device__ __forceinline__ void bn_bwd_finalize_block(const BnBwdFin& f, int bid
     block_row_sum2<NT>(f.p1 + (int64_t)c * f.chunks, f.p2 + (int64_t)c * f.chunks, f.chunks, s1, s2);
     if (lane == 0) { red[wave] = s1; red[NT / 64 + wave] = s2; }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      s1 = 0.0;
-      s2 = 0.0;
+    if (threadIdx.x != 0) return;
+    s1 = 0.0;
+    s2 = 0.0;
 #pragma unroll
-      for (int w = 0; w < NT / 64; ++w) { s1 += red[w]; s2 += red[NT / 64 + w]; }
-      bn_bwd_fin_store(f, c, s1, s2);
-    }
+    for (int w = 0; w < NT / 64; ++w) { s1 += red[w]; s2 += red[NT / 64 + w]; }
+    bn_bwd_fin_store(f, c, s1, s2);
   } else if constexpr (NT == kBlock) {
     const int64_t c = (int64_t)bid * 8 + wave * 2 + (lane >> 5);
     const int part = lane & 31;
-    if (c < f.C) {
-      double s1, s2;
-      half_wave_sum2(f.p1, f.p2, c, f.chunks, part, s1, s2);
-      if (part == 0) bn_bwd_fin_store(f, c, s1, s2);
-    }
+    if (c >= f.C) return;
+    double s1, s2;
+    half_wave_sum2(f.p1, f.p2, c, f.chunks, part, s1, s2);
+    if (part != 0) return;
+    bn_bwd_fin_store(f, c, s1, s2);
   }
 }
 

@@ -79,37 +79,7 @@ void launch_bn2_bwd_from_partials(int dtype, const void* dz, const void* x, cons
                                   const float* mean2, const float* invstd2, const float* p1, const float* p2,
                                   const float* p3, int chunks, float* dgamma, float* dbeta, float* dgamma2,
                                   float* dbeta2, void* dx, void* dx2, float* kbuf, hipStream_t s);
-// One training-mode BatchNorm's finalize: [C][chunks] partials in, statistics / running stats /
-// coefficients [a | b] (save_coef, 2C floats) out.
-struct BnFwdArgs {
-  const float* psum = nullptr;
-  const float* psq = nullptr;
-  int chunks = 0;
-  const float* gamma = nullptr;
-  const float* beta = nullptr;
-  float eps = 1e-5f, momentum = 0.1f;
-  float* run_mean = nullptr;
-  float* run_var = nullptr;
-  int64_t* num_batches = nullptr;
-  float* save_mean = nullptr;
-  float* save_invstd = nullptr;
-  float* save_coef = nullptr;
-};
-// y = relu(bn1(x) + bn2(x2)), both from conv-epilogue partials: both finalizes and the apply in
-// one launch (handoff.h) - the forward of ops/bn.py _BN2AddReLUPair
-void launch_bn2_fwd_from_partials(int dtype, const void* x, const void* x2, void* y, int64_t M, int64_t C,
-                                  const BnFwdArgs& a1, const BnFwdArgs& a2, hipStream_t s, uint8_t* mask = nullptr);
 void bn_set_skip_finalize(int on);  // measurement only (bench/ab_step.py): skip BN finalize launches
-// BatchNorm finalize run inside the apply launch (handoff.h; default on, DPT_BN_FUSE_FINALIZE=0 off)
-void bn_set_fuse_finalize(int on);
-int bn_fuse_finalize_enabled();
-void bn_set_fused_apply_cap(int cap);  // finalize + waiting apply blocks of a fused launch (A/B knob)
-// start of a training step on stream s: zero the hand-off granules the previous step drew and
-// open the arena to fused launches on s (ops/bn.py begin_step)
-void bn_handoff_begin(hipStream_t s);
-int64_t bn_handoff_errors();            // bounded-spin time-outs so far on this device (expect 0)
-int64_t bn_handoff_fused_launches();    // fused finalize+apply launches issued by this process
-void bn_set_handoff_idle_finalizers(int on);  // test only: every apply block runs the finalize itself
 void launch_bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int64_t C,
                      const float* coef_a, const float* coef_b, bool relu, hipStream_t s);
 void launch_bn_bwd(int dtype, const void* dy, const void* dy2, const void* y, const void* x, int64_t M,

@@ -29,7 +29,6 @@ import torch.nn as nn
 
 from .. import ops
 from ..amp import DeviceGradScaler, autocast
-from ..ops import bn as native_bn
 from ..ops import conv as native_conv
 from ..profiling.timeline import StepTimeline, roctx_range
 from ..utils.dist import all_reduce_
@@ -183,8 +182,6 @@ class Trainer:
             native_conv.begin_step()  # weights changed since the last step: new flip cache
         else:
             native_conv.reset_side_channels()
-        if self.device.type == "cuda":
-            native_bn.begin_step()    # BatchNorm finalize hand-off granules of this step
         ctx = self.ddp.no_sync() if not sync else contextlib.nullcontext()
         rx = self.roctx
         with ctx:

@@ -30,15 +30,6 @@ from .conv import MASKED_NO_RES, take_bnb_partials
 BNR_FUSE = os.environ.get("DPT_BNR_FUSE", "1") != "0"
 
 
-def begin_step() -> None:
-    """Start of a training step (engine/trainer.py, on the step's stream): the BatchNorm finalizes
-    of this step run inside their apply launches (csrc/kernels/handoff.h) - this zeroes the
-    hand-off granules the previous step used (one memset; replayed with a captured step).
-    Without it (ops called outside a training step) every finalize is its own launch."""
-    if native_available() and torch.cuda.is_available() and torch.cuda.is_initialized():
-        native().bn_handoff_begin()
-
-
 def _cl(t: torch.Tensor) -> torch.Tensor:
     if t.dim() == 4 and not t.is_contiguous(memory_format=torch.channels_last):
         return t.contiguous(memory_format=torch.channels_last)
@@ -177,18 +168,12 @@ class _BN2AddReLUPair(torch.autograd.Function):
         C = native()
         ps, pq = partials if partials is not None else (None, None)
         ps2, pq2 = partials2 if partials2 is not None else (None, None)
+        _, mean, invstd, coef = C.bn_fwd_train(x, None, w, b, rm, rv, nb, float(momentum), float(eps), True,
+                                               ps, pq, False)
+        _, mean2, invstd2, coef2 = C.bn_fwd_train(x2, None, w2, b2, rm2, rv2, nb2, float(momentum2), float(eps2),
+                                                  False, ps2, pq2, False)
         mask = _relu_mask(x) if own_slot is not None else None
-        if ps is not None and ps2 is not None:
-            # both finalizes and the apply in one launch (csrc/kernels/handoff.h)
-            y, mean, invstd, coef, mean2, invstd2, coef2 = C.bn2_fwd_train(
-                x, x2, w, b, rm, rv, nb, float(momentum), float(eps), w2, b2, rm2, rv2, nb2, float(momentum2),
-                float(eps2), ps, pq, ps2, pq2, mask_out=mask)
-        else:
-            _, mean, invstd, coef = C.bn_fwd_train(x, None, w, b, rm, rv, nb, float(momentum), float(eps), True,
-                                                   ps, pq, False)
-            _, mean2, invstd2, coef2 = C.bn_fwd_train(x2, None, w2, b2, rm2, rv2, nb2, float(momentum2),
-                                                      float(eps2), False, ps2, pq2, False)
-            y = C.bn_apply_aff(x, x2, coef, coef2, mask_out=mask)
+        y = C.bn_apply_aff(x, x2, coef, coef2, mask_out=mask)
         ctx.save_for_backward(x, x2, y, w, w2, mean, invstd, mean2, invstd2)
         ctx.set_materialize_grads(False)
         if own_slot is not None:

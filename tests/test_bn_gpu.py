@@ -317,3 +317,28 @@ def test_stem_bn_relu_maxpool_fused(cuda, dtype, monkeypatch):
     assert torch.equal(a, b)
     for u, v in zip(ra, rb):
         torch.testing.assert_close(u, v, rtol=2e-2, atol=2e-2 * v.abs().max().item() + 1e-6)
+
+
+def test_finalize_of_tens_of_thousands_of_partials(cuda):
+    """The stem's conv epilogue leaves 25,088 partials per channel at batch 256: that finalize runs
+    1024-thread blocks (bn_kernels.hip, > 8192 partials); same statistics as the fp32 reference."""
+    from distributed_pytorch_training_amd import ops
+    C_ = ops.native()
+    c, chunks = 64, 10000
+    x = (torch.randn(chunks * 8, c, device=cuda) * 0.5 + 2.0).to(torch.bfloat16)
+    rows = x.float().view(chunks, 8, c)
+    ps = rows.sum(1).t().contiguous()
+    pq = (rows ** 2).sum(1).t().contiguous()
+    x4 = x.view(chunks * 8, 1, 1, c).permute(0, 3, 1, 2)      # channels_last [M, C, 1, 1]
+    w = torch.rand(c, device=cuda) + 0.5
+    b = torch.rand(c, device=cuda) - 0.5
+    rm, rv = torch.zeros(c, device=cuda), torch.ones(c, device=cuda)
+    nb = torch.zeros((), dtype=torch.long, device=cuda)
+    y, mean, invstd, _ = C_.bn_fwd_train(x4, None, w, b, rm, rv, nb, 0.1, 1e-5, False, ps, pq)
+    xf = x.float()
+    torch.testing.assert_close(mean, xf.mean(0), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(invstd, torch.rsqrt(xf.var(0, unbiased=False) + 1e-5), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rv, 0.9 + 0.1 * xf.var(0, unbiased=True), rtol=1e-4, atol=1e-5)
+    zr = (xf - xf.mean(0)) * torch.rsqrt(xf.var(0, unbiased=False) + 1e-5) * w + b
+    torch.testing.assert_close(y.permute(0, 2, 3, 1).reshape(-1, c).float(), zr, rtol=2e-2, atol=2e-2)
+    assert int(nb) == 1
