@@ -28,15 +28,17 @@ CONFIGS = {
     # the reference's --amp (fp16 autocast + GradScaler)
     "r18_amp_fp16": ["--model", "resnet18", "--image-size", "32", "--num-classes", "10", "--batch-size", "128",
                      "--amp"],
-    # the flagship model under bf16 autocast
-    "r50_bf16": ["--model", "resnet50", "--image-size", "64", "--num-classes", "100", "--batch-size", "128",
+    # the flagship model under bf16 autocast (10 classes, lr 0.02: at 100 classes / lr 0.05 neither
+    # engine left chance level in 500 steps - profiles/train_parity_r4.md)
+    "r50_bf16": ["--model", "resnet50", "--image-size", "64", "--num-classes", "10", "--batch-size", "128",
                  "--amp", "--amp-dtype", "bf16", "--lr", "0.02"],
 }
 
 # pixel noise std against unit-std prototypes, per config: the classes separate only through the
 # prototypes' low-frequency structure; the nearest-prototype (Bayes) accuracy is ~87 % for 10
-# classes at 32x32 with noise 20 and ~80 % for 100 classes at 64x64 with noise 32, so the curves
-# take hundreds of steps to flatten and the held-out accuracy measures generalisation.
+# classes at 32x32 with noise 20 (64x64: 4x the pixels to average over, so noise 32 keeps the task
+# about as hard), so the curves take hundreds of steps to flatten and the held-out accuracy
+# measures generalisation.
 NOISE = {"r18_fp32": 20.0, "r18_amp_fp16": 20.0, "r50_bf16": 32.0}
 
 STEP_RE = re.compile(r"Epoch \[(\d+)\] Step \[(\d+)/(\d+)\] Loss: ([\d.]+)  Acc: ([\d.]+)%  "
@@ -89,9 +91,10 @@ def _thr(res, skip_epochs=1):
     return sum(v) / len(v) if v else float("nan")
 
 
-def markdown(config: str, res) -> str:
+def markdown(config: str, res, extra=()) -> str:
     nat, ref = res["native"], res["torch"]
-    lines = [f"## {config}: `train_ddp.py {' '.join(CONFIGS[config])} --dataset synthetic --synthetic-task prototypes`",
+    flags = " ".join([*CONFIGS[config], *extra])
+    lines = [f"## {config}: `train_ddp.py {flags} --dataset synthetic --synthetic-task prototypes`",
              "", "| epoch | train loss native / torch | train acc % native / torch | val loss native / torch | "
              "val acc % native / torch | epoch s native / torch |", "|---|---|---|---|---|---|"]
     for a, b in zip(nat["epochs"], ref["epochs"]):
@@ -111,10 +114,12 @@ def main():
     ap.add_argument("--epochs", type=int, default=5)
     ap.add_argument("--steps-per-epoch", type=int, default=100)
     ap.add_argument("--json", default=None, help="append the raw results as JSON lines here")
+    ap.add_argument("--extra", default="", help="more train_ddp.py flags, space separated (later flags win)")
     a = ap.parse_args()
+    extra = a.extra.split() if a.extra else []
     for c in a.config:
-        res = compare(c, a.epochs, a.steps_per_epoch)
-        print(markdown(c, res), flush=True)
+        res = compare(c, a.epochs, a.steps_per_epoch, extra)
+        print(markdown(c, res, extra), flush=True)
         if a.json:
             with open(a.json, "a") as f:
                 for impl in ("native", "torch"):
