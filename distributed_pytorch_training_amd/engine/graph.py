@@ -40,6 +40,7 @@ asynchronous one records its host collectives as graph host nodes (csrc/host_com
 from __future__ import annotations
 
 import contextlib
+import gc
 import warnings
 
 import torch
@@ -129,6 +130,12 @@ class GraphedStep:
                           "the stream and cannot be captured; use --comm host-async")
             ok = False
         else:
+            # No Python garbage collection while the stream is captured: a cycle collected there
+            # runs destructors (graphs, allocator pools, extension objects of earlier trainers)
+            # whose HIP calls are illegal during capture - one such collection aborted the
+            # process in a GPU test run.  torch.cuda.graph collects once before it starts.
+            gc_was = gc.isenabled()
+            gc.disable()
             try:
                 with torch.cuda.graph(g, stream=self.stream):
                     out, loss = t._native_step(self.static_x, self.static_y)
@@ -138,6 +145,9 @@ class GraphedStep:
                 warnings.warn(f"hipGraph capture failed, running eagerly: {e!r}")
                 ok = False
                 torch.cuda.synchronize()
+            finally:
+                if gc_was:
+                    gc.enable()
         if t.world_size > 1 and not agree(ok, t.device):
             if ok:
                 warnings.warn("hipGraph capture failed on another rank: every rank runs eagerly")
