@@ -29,7 +29,7 @@ def parse_arm(spec: str):
     sets = []
     for item in filter(None, rest.split(",")):
         fn, _, val = item.partition(":")
-        sets.append((fn, int(val)))
+        sets.append((fn, tuple(int(v) for v in val.split("/"))))  # "fn:a/b/c" -> fn(a, b, c)
     return name, sets
 
 
@@ -75,9 +75,9 @@ def main(argv=None):
         # "module.path.ATTR" sets a Python module attribute, anything else a native setter
         if "." in fn:
             mod, _, attr = fn.rpartition(".")
-            setattr(importlib.import_module(mod), attr, v)
+            setattr(importlib.import_module(mod), attr, v[0])
         else:
-            getattr(C, fn)(v)
+            getattr(C, fn)(*v)
 
     def apply(sets):
         for fn, v in resets:

@@ -1162,6 +1162,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_set_variant", &dpt::conv_set_variant, py::arg("variant"));
   m.def("bn_set_skip_finalize", &dpt::bn_set_skip_finalize, py::arg("on"),
         "measurement only: skip every BatchNorm finalize launch (wrong values; timing upper bound)");
+  m.def("conv_set_splitk_policy", &dpt::conv_set_splitk_policy, py::arg("tiles"), py::arg("eager_tiles"),
+        py::arg("eager_min_k"), py::arg("target"), "split-K thresholds (A/B knob; <= 0 keeps a value)");
   m.def("conv_set_big", &dpt::conv_set_big, py::arg("on"));
   m.def("conv_set_halo", &dpt::conv_set_halo, py::arg("on"));
   m.def("conv_set_wgrad_target", &dpt::conv_set_wgrad_target, py::arg("blocks"));

@@ -1990,7 +1990,14 @@ int conv_fwd_splits(int64_t M, int Cout, int64_t K, int* kps_out, hipStream_t s)
 // Thresholds of the policy below: split grids of fewer than kSplitTiles tiles (eagerly: at most
 // kSplitEager tiles with >= 24 K-steps) to about kSplitTarget blocks (512 / 1024 targets
 // measured -1 % / -5 %, docs/DESIGN.md §7.2).
-constexpr int kSplitTiles = 160, kSplitEager = 32, kSplitTarget = 512;
+static int kSplitTiles = 160, kSplitEager = 32, kSplitTarget = 512, kSplitEagerMinK = 24;
+// A/B knob (bench/ab_step.py): the thresholds above; a value <= 0 keeps the current one
+void conv_set_splitk_policy(int tiles, int eager_tiles, int eager_min_k, int target) {
+  if (tiles > 0) kSplitTiles = tiles;
+  if (eager_tiles > 0) kSplitEager = eager_tiles;
+  if (eager_min_k > 0) kSplitEagerMinK = eager_min_k;
+  if (target > 0) kSplitTarget = target;
+}
 
 int conv_fwd_splits_for(int64_t M, int Cout, int64_t K, bool graph, int* kps_out) {
   const int n_tiles = Cout % 128 == 0 ? Cout / 128 : Cout / 64;
@@ -2001,7 +2008,7 @@ int conv_fwd_splits_for(int64_t M, int Cout, int64_t K, bool graph, int* kps_out
   if (mode == 0 || tiles >= kSplitTiles || nk < 4) return 1;
   // Eager launches are host-bound at these sizes: the extra epilogue launch only pays where the
   // single-block K loop is long (tens of microseconds); inside a hipGraph capture it always does.
-  if (!graph && mode == 1 && (tiles > kSplitEager || nk < 24)) return 1;
+  if (!graph && mode == 1 && (tiles > kSplitEager || nk < kSplitEagerMinK)) return 1;
   const int want = (int)((kSplitTarget + tiles - 1) / tiles);
   const int kps = std::max(2, (nk + want - 1) / want);
   const int splits = (nk + kps - 1) / kps;
