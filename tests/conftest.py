@@ -13,6 +13,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: multi-process or long CPU test")
 
 
+@pytest.fixture(autouse=True)
+def _collect_before_gpu_tests(request):
+    """Collect the previous tests' garbage BEFORE a GPU test starts: a reference cycle collected in
+    the middle of a later hipGraph capture runs destructors whose HIP calls are illegal there (one
+    such collection aborted a GPU test run; engine/graph.py also disables collection while it
+    captures)."""
+    if request.node.get_closest_marker("gpu") is not None:
+        import gc
+        gc.collect()
+    yield
+
+
 @pytest.fixture(scope="session")
 def cuda():
     import torch
