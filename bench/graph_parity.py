@@ -18,7 +18,6 @@ Modes:
 from __future__ import annotations
 
 import argparse
-import copy
 import json
 import os
 import sys
@@ -30,37 +29,19 @@ import torch  # noqa: E402
 
 from distributed_pytorch_training_amd.config import parse_args  # noqa: E402
 from distributed_pytorch_training_amd.data import get_dataloaders  # noqa: E402
+from distributed_pytorch_training_amd.engine.graph import restore, snapshot  # noqa: E402
 from distributed_pytorch_training_amd.engine.trainer import Trainer  # noqa: E402
 from distributed_pytorch_training_amd.models import build_model  # noqa: E402
 from distributed_pytorch_training_amd.utils.dist import set_seed  # noqa: E402
 from distributed_pytorch_training_amd.utils.env import setup_miopen_env, setup_tunableop  # noqa: E402
 
 
-def _state_tensors(tr):
-    """Every tensor a training step reads and writes (restorable in place)."""
-    out = {"param": tr.ddp.arena.param_flat, "step": tr.optimizer._step, "metrics": tr.metrics}
-    mb = getattr(tr.optimizer, "momentum_buffer", None)
-    if mb is not None:
-        out["momentum"] = mb
-    for n, b in tr.module.named_buffers():
-        out["buf:" + n] = b
-    if tr.ddp.shadow_flat is not None:
-        out["shadow"] = tr.ddp.shadow_flat
-    for k in ("scale_tensor", "growth_tracker", "found_inf"):
-        t = getattr(tr.scaler, k, None)
-        if isinstance(t, torch.Tensor):
-            out["scaler:" + k] = t
-    return out
-
-
 def _snap(tr):
-    return {k: v.detach().clone() for k, v in _state_tensors(tr).items()}
+    return snapshot(tr)
 
 
 def _restore(tr, snap):
-    with torch.no_grad():
-        for k, v in _state_tensors(tr).items():
-            v.copy_(snap[k])
+    restore(tr, snap)
 
 
 def make(argv, dev):
@@ -71,7 +52,12 @@ def make(argv, dev):
     return args, Trainer(model, args, 0, 1, dev, log=print)
 
 
-def teacher(steps: int, extra):
+def _eager(G, tr, x, y):
+    with G._on_stream():
+        tr._native_step(x, y)
+
+
+def teacher(steps: int, extra, repeat: bool = False):
     dev = torch.device("cuda:0")
     args, tr = make(["--dataset", "synthetic", "--image-size", "32", "--num-classes", "10", *extra], dev)
     train, _, _ = get_dataloaders(args, 0, 1, dev)
@@ -83,6 +69,7 @@ def teacher(steps: int, extra):
         tr.train_step(x, y)
     torch.cuda.synchronize()
     assert G.graph is not None, f"capture failed (failed={G.failed})"
+    print(json.dumps({"validation": G.validation}), flush=True)
     names = [n for n in tr.ddp.arena.names] if hasattr(tr.ddp.arena, "names") else None
     worst = []
     rows = []
@@ -94,11 +81,22 @@ def teacher(steps: int, extra):
         sg = _snap(tr)
         gg = tr.ddp.arena.grad_flat.detach().clone()
         _restore(tr, s0)
-        with G._on_stream():
-            tr._native_step(x, y)           # eager, same stream, same state
+        _eager(G, tr, x, y)                 # eager, same stream, same state
         torch.cuda.synchronize()
         se = _snap(tr)
         ge = tr.ddp.arena.grad_flat.detach().clone()
+        rep = {}
+        if repeat:   # each path once more from S_k: is either one not deterministic by itself?
+            for name, again in (("replay", lambda: tr.train_step(x, y)), ("eager", lambda: _eager(G, tr, x, y))):
+                _restore(tr, s0)
+                again()
+                torch.cuda.synchronize()
+                g2 = tr.ddp.arena.grad_flat.detach().clone()
+                base = gg if name == "replay" else ge
+                rep[name] = (g2 - base).double().norm().item() / max(base.double().norm().item(), 1e-30)
+            _restore(tr, s0)
+            _eager(G, tr, x, y)
+            torch.cuda.synchronize()
         upd = (se["param"] - s0["param"]).double().norm().item()
         dp = (sg["param"] - se["param"]).double().norm().item()
         dg = (gg - ge).double().norm().item() / max(ge.double().norm().item(), 1e-30)
@@ -110,10 +108,13 @@ def teacher(steps: int, extra):
         # per-parameter gradient differences
         per = []
         for i, (gv_g, gv_e) in enumerate(zip(tr.ddp.arena.views(gg), tr.ddp.arena.views(ge))):
-            r = (gv_g - gv_e).double().norm().item() / max(gv_e.double().norm().item(), 1e-30)
-            per.append((r, names[i] if names else str(i)))
+            ne = gv_e.double().norm().item()
+            r = (gv_g - gv_e).double().norm().item() / max(ne, 1e-30)
+            per.append((r, names[i] if names else str(i), gv_g.double().norm().item(), ne))
         per.sort(reverse=True)
-        row["worst_grads"] = per[:5]
+        if rep:
+            row["self_rel_grad"] = rep
+        row["worst_grads"] = per[:5]   # (relative difference, name, |replayed grad|, |eager grad|)
         rows.append(row)
         print(json.dumps(row), flush=True)
     return rows
@@ -179,6 +180,8 @@ def main():
     ap.add_argument("--extra", default="", help="extra train_ddp flags, space separated")
     ap.add_argument("--arms", default="--cuda-graph,--no-cuda-graph",
                     help="free mode: comma-separated modes, repeats allowed (spread of the configuration)")
+    ap.add_argument("--repeat", action="store_true",
+                    help="teacher mode: also rerun each path from the same state (self-consistency)")
     ap.add_argument("--task", default="random", choices=["random", "prototypes"])
     a = ap.parse_args()
     setup_miopen_env()
@@ -186,7 +189,7 @@ def main():
     setup_tunableop()
     torch.backends.cudnn.benchmark = True
     extra = a.extra.split() if a.extra else []
-    {"teacher": lambda: teacher(a.steps, extra), "free": lambda: free(a.steps, extra, tuple(a.arms.split(",")), a.task),
+    {"teacher": lambda: teacher(a.steps, extra, a.repeat), "free": lambda: free(a.steps, extra, tuple(a.arms.split(",")), a.task),
      "startup": lambda: startup(extra)}[a.mode]()
 
 

@@ -21,6 +21,11 @@ Rules (checked or documented):
 * hyper-parameters are baked into the graph (constant LR, as in the reference);
 * the profiling timeline is incompatible (it reads events on the host) and disables replay;
 * any capture failure falls back to eager execution with a warning;
+* the first replay is validated (``validate``): from one saved training state the step runs
+  eagerly once and replayed twice, and every parameter's gradient must agree (replay vs eager
+  and replay vs replay) within ``VALIDATE_RTOL``, or the trainer falls back to eager with a
+  warning naming the parameter.  This is what caught MIOpen's graph-unsafe CK backward-weights
+  solver (utils/env.py ``GRAPH_UNSAFE_MIOPEN_SOLVERS``; excluded when the GraphedStep is built);
 * the communicator watchdog gets one completion marker per replay (``Collective.track``),
   since the captured collectives never pass through ``RcclComm::all_reduce``.
 
@@ -41,12 +46,52 @@ from __future__ import annotations
 
 import contextlib
 import gc
+import os
 import warnings
 
 import torch
 
 
 AUTO_GRAPH_MAX_PIXELS = 1 << 18
+# Replay validation threshold: per-parameter ||g_a - g_b|| / ||g_b||.  Run-to-run noise of one step
+# (atomic reduction order in the BN / wgrad kernels) measured 1e-6..5e-3; the graph-unsafe
+# solver's garbage measured 1e5..1e36.
+VALIDATE_RTOL = 5e-2
+
+
+def step_state(trainer) -> dict:
+    """Every tensor one native training step reads and writes, restorable in place: fp32 master
+    parameters, optimizer state and step counter, module buffers (BN running statistics), 16-bit
+    weight shadows, device-side AMP scaler state and the device metrics."""
+    t = trainer
+    out = {"param": t.ddp.arena.param_flat, "step": t.optimizer._step, "metrics": t.metrics}
+    for i, st in enumerate(t.optimizer.arena_state() if hasattr(t.optimizer, "arena_state") else []):
+        if st is not None:
+            out[f"opt{i}"] = st
+    for n, b in t.module.named_buffers():
+        out["buf:" + n] = b
+    if t.ddp.shadow_flat is not None:
+        out["shadow"] = t.ddp.shadow_flat
+    for k in ("scale_tensor", "growth_tracker", "found_inf"):
+        v = getattr(t.scaler, k, None)
+        if isinstance(v, torch.Tensor):
+            out["scaler:" + k] = v
+    return out
+
+
+def snapshot(trainer) -> dict:
+    return {k: v.detach().clone() for k, v in step_state(trainer).items()}
+
+
+def restore(trainer, snap: dict) -> None:
+    with torch.no_grad():
+        for k, v in step_state(trainer).items():
+            v.copy_(snap[k])
+
+
+def _has_randomness(module) -> bool:
+    """Dropout-like modules draw fresh random numbers per run: eager and replay differ legitimately."""
+    return any(isinstance(m, torch.nn.modules.dropout._DropoutNd) and m.p > 0 for m in module.modules())
 
 
 def auto_enabled(args, device, world_size: int = 1) -> bool:
@@ -61,9 +106,17 @@ def auto_enabled(args, device, world_size: int = 1) -> bool:
 
 
 class GraphedStep:
-    def __init__(self, trainer, warmup: int = 3) -> None:
+    def __init__(self, trainer, warmup: int = 3, validate: bool | None = None) -> None:
+        from ..utils.env import graph_safe_miopen
+        # effective only if no convolution has run in this process yet (MIOpen reads it once);
+        # engine/run.py and the GPU test session call it at process start
+        graph_safe_miopen()
         self.trainer = trainer
         self.warmup = warmup
+        if validate is None:
+            validate = os.environ.get("DPT_GRAPH_VALIDATE", "1") != "0"
+        self.validate = validate
+        self.validation = None     # {"ok", "replay_vs_eager", "replay_vs_replay", "worst"} once run
         self.graph = None
         self.failed = False
         self.calls = 0
@@ -105,6 +158,12 @@ class GraphedStep:
         if x.shape != self.static_x.shape or y.shape != self.static_y.shape:
             with self._on_stream():
                 return t._native_step(x, y)
+        if self.validate and self.validation is None:
+            return self._validated_first_replay(x, y)
+        return self._replay(x, y)
+
+    def _replay(self, x: torch.Tensor, y: torch.Tensor):
+        t = self.trainer
         with self._on_stream():
             self.static_x.copy_(x)
             self.static_y.copy_(y)
@@ -116,6 +175,64 @@ class GraphedStep:
         self.replays += 1
         t.global_step += 1
         return self.out, self.loss
+
+    def _validated_first_replay(self, x: torch.Tensor, y: torch.Tensor):
+        """From one saved state: an eager step, then two replays; compare every parameter's
+        gradient.  Leaves the state of the last replay (the step this call stands for)."""
+        t = self.trainer
+        views = t.ddp.arena.views
+        names = list(getattr(t.ddp.arena, "names", [])) or [str(i) for i in range(len(t.ddp.arena.params))]
+        if _has_randomness(t.module):
+            self.validation = {"ok": True, "skipped": "model draws random numbers (dropout)"}
+            return self._replay(x, y)
+        torch.cuda.synchronize()
+        s0 = snapshot(t)
+        gs = []
+        with self._on_stream():
+            t._native_step(x, y)
+        t.global_step -= 1
+        for k in range(2):
+            torch.cuda.synchronize()
+            gs.append(t.ddp.arena.grad_flat.detach().clone())
+            restore(t, s0)
+            out = self._replay(x, y)
+            if k == 0:
+                t.global_step -= 1
+                self.replays -= 1
+        torch.cuda.synchronize()
+        gs.append(t.ddp.arena.grad_flat)
+        eager, rep1, rep2 = gs
+
+        def worst(a, b):
+            # floor: a parameter whose gradient is ~0 compares against the arena's scale
+            floor = max(1e-6 * b.double().norm().item(), 1e-30)
+            w = (0.0, "")
+            for n, u, v in zip(names, views(a), views(b)):
+                r = (u - v).double().norm().item() / max(v.double().norm().item(), floor)
+                if r != r:                 # NaN anywhere is a failure
+                    return (float("inf"), n)
+                if r > w[0]:
+                    w = (r, n)
+            return w
+
+        ve, vr = worst(rep2, eager), worst(rep2, rep1)
+        ok = ve[0] <= VALIDATE_RTOL and vr[0] <= VALIDATE_RTOL
+        if t.world_size > 1:
+            ok = agree(ok, t.device)
+        self.validation = {"ok": ok, "replay_vs_eager": ve[0], "replay_vs_replay": vr[0],
+                           "worst": ve[1] if ve[0] >= vr[0] else vr[1]}
+        if not ok:
+            warnings.warn(
+                "hipGraph replay disagrees with eager execution (worst parameter gradient "
+                f"{self.validation['worst']}: replay-vs-eager {ve[0]:.3g}, replay-vs-replay {vr[0]:.3g}); "
+                "a kernel in the step is not replay-safe - running eagerly from now on")
+            self.failed = True
+            t.global_step -= 1
+            self.replays -= 1
+            restore(t, s0)
+            with self._on_stream():
+                return t._native_step(x, y)
+        return out
 
     def _capture(self, x: torch.Tensor, y: torch.Tensor) -> None:
         t = self.trainer

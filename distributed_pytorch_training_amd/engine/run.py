@@ -21,7 +21,7 @@ from ..data import get_dataloaders
 from ..models import build_model
 from ..utils.checkpoint import load_checkpoint, save_checkpoint
 from ..utils.dist import cleanup_distributed, init_distributed, set_seed
-from ..utils.env import setup_miopen_env, setup_tunableop
+from ..utils.env import graph_safe_miopen, setup_miopen_env, setup_tunableop
 from ..utils.fault import FaultSpec
 from .trainer import Trainer, format_epoch_line
 
@@ -41,6 +41,10 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     rank, world_size, device = info.rank, info.world_size, info.device
     if args.impl == "native" and device.type == "cuda":
         setup_tunableop()
+        from .graph import auto_enabled
+        cg = args.cuda_graph if args.cuda_graph is not None else auto_enabled(args, device, world_size)
+        if cg:
+            graph_safe_miopen()     # before the first convolution (utils/env.py)
     set_seed(args.seed, rank)
 
     if rank == 0:

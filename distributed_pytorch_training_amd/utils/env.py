@@ -17,6 +17,24 @@ REPO = Path(__file__).resolve().parents[2]
 SHIPPED_DB = REPO / "miopen_db"
 SHIPPED_GEMM_DB = REPO / "gemm_db" / "tunableop_results.csv"
 
+# MIOpen solvers whose kernels compute wrong results under hipGraph replay.  Measured on MIOpen
+# 3.5 / ROCm 7.2 (profiles/graph_replay_miopen_r4.md): the CK grouped backward-weights solver
+# (ConvHipImplicitGemmGroupWrwXdlops) returns weight gradients that are wrong by 1e5-1e36
+# relative on replays of a captured fp32 NHWC conv backward, while eager calls of the same
+# solver are correct.  Find mode picks it on timing (it wins some shapes by ~15%), so which
+# boxes hit it varies from run to run.  MIOpen reads these switches once, at the first
+# convolution of the process: graph_safe_miopen() must run before any MIOpen call.
+GRAPH_UNSAFE_MIOPEN_SOLVERS = ("MIOPEN_DEBUG_GROUP_CONV_IMPLICIT_GEMM_HIP_WRW_XDLOPS",)
+
+
+def graph_safe_miopen() -> bool:
+    """Exclude the graph-unsafe MIOpen solvers (unless the user set the switches explicitly).
+    True when all of them are excluded.  Processes that may capture a hipGraph call this before
+    their first convolution; eager-only processes keep the full solver set."""
+    for k in GRAPH_UNSAFE_MIOPEN_SOLVERS:
+        os.environ.setdefault(k, "0")
+    return all(os.environ.get(k) == "0" for k in GRAPH_UNSAFE_MIOPEN_SOLVERS)
+
 
 def setup_miopen_env(scratch: str | None = None) -> str:
     """Point MIOpen's user find-db / kernel cache at writable dirs seeded from the repo."""

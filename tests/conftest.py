@@ -11,6 +11,11 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP kernels, RCCL)")
     config.addinivalue_line("markers", "slow: multi-process or long CPU test")
+    # The session's GPU tests capture hipGraphs after other tests already ran MIOpen convolutions,
+    # and MIOpen reads its solver switches once per process: exclude the graph-unsafe solvers
+    # before anything runs (utils/env.py GRAPH_UNSAFE_MIOPEN_SOLVERS).
+    from distributed_pytorch_training_amd.utils.env import graph_safe_miopen
+    graph_safe_miopen()
 
 
 @pytest.fixture(autouse=True)
