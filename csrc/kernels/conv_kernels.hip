@@ -1979,6 +1979,7 @@ static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdAr
 static int g_splitk = 1;
 static int splitk_mode() { return g_splitk; }
 void conv_set_splitk(int mode) { g_splitk = mode; }
+int conv_get_splitk() { return g_splitk; }
 
 int conv_fwd_splits(int64_t M, int Cout, int64_t K, int* kps_out, hipStream_t s) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;

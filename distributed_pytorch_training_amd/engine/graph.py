@@ -22,10 +22,11 @@ Rules (checked or documented):
 * the profiling timeline is incompatible (it reads events on the host) and disables replay;
 * any capture failure falls back to eager execution with a warning;
 * the first replay is validated (``validate``): from one saved training state the step runs
-  eagerly once and replayed twice, and every parameter's gradient must agree (replay vs eager
-  and replay vs replay) within ``VALIDATE_RTOL``, or the trainer falls back to eager with a
-  warning naming the parameter.  This is what caught MIOpen's graph-unsafe CK backward-weights
-  solver (utils/env.py ``GRAPH_UNSAFE_MIOPEN_SOLVERS``; excluded when the GraphedStep is built);
+  eagerly once and replayed twice; the whole gradient must agree within ``VALIDATE_RTOL`` and
+  no single parameter's gradient may be off by more than ``VALIDATE_PARAM_RTOL`` (replay vs eager
+  and replay vs replay), or the trainer falls back to eager with a warning naming the parameter.
+  MIOpen's graph-unsafe CK backward-weights solver (utils/env.py ``GRAPH_UNSAFE_MIOPEN_SOLVERS``,
+  excluded when the GraphedStep is built) produced per-parameter errors of 1e5-1e37;
 * the communicator watchdog gets one completion marker per replay (``Collective.track``),
   since the captured collectives never pass through ``RcclComm::all_reduce``.
 
@@ -53,10 +54,13 @@ import torch
 
 
 AUTO_GRAPH_MAX_PIXELS = 1 << 18
-# Replay validation threshold: per-parameter ||g_a - g_b|| / ||g_b||.  Run-to-run noise of one step
-# (atomic reduction order in the BN / wgrad kernels) measured 1e-6..5e-3; the graph-unsafe
-# solver's garbage measured 1e5..1e36.
+# Replay validation thresholds, ||g_a - g_b|| / ||g_b|| over the whole arena and per parameter.
+# The whole gradient of a correct replay agrees with eager to 1e-6..5e-3 (atomic reduction order;
+# eager and captured steps may also split the conv K loops differently).  Single BatchNorm bias
+# gradients are near-cancelling sums and legitimately move by up to ~0.35 relative (bf16, 2 ranks,
+# tests/test_multirank_gpu.py); the graph-unsafe solver's garbage measured 1e5..1e37.
 VALIDATE_RTOL = 5e-2
+VALIDATE_PARAM_RTOL = 10.0
 
 
 def step_state(trainer) -> dict:
@@ -87,6 +91,27 @@ def restore(trainer, snap: dict) -> None:
     with torch.no_grad():
         for k, v in step_state(trainer).items():
             v.copy_(snap[k])
+
+
+@contextlib.contextmanager
+def _graph_splitk_policy():
+    """Run an eager step with the K-loop splits a capture chooses (ops/conv split-K policy, mode 2):
+    eager launches split fewer small grids than captured ones, which changes the summation order,
+    and bf16 steps of a small-batch network amplify that past any useful tolerance (24 % of the
+    gradient at batch 32, both paths equally far from fp32: profiles/graph_replay_miopen_r4.md).
+    With the same splits, eager and replay run the same kernels and must agree to rounding."""
+    from .. import ops
+    if not ops.native_available():
+        yield
+        return
+    C = ops.native()
+    old = C.conv_get_splitk()
+    if old == 1:
+        C.conv_set_splitk(2)
+    try:
+        yield
+    finally:
+        C.conv_set_splitk(old)
 
 
 def _has_randomness(module) -> bool:
@@ -188,9 +213,19 @@ class GraphedStep:
         torch.cuda.synchronize()
         s0 = snapshot(t)
         gs = []
-        with self._on_stream():
+        with self._on_stream(), _graph_splitk_policy():
             t._native_step(x, y)
         t.global_step -= 1
+        e2 = None
+        if os.environ.get("DPT_GRAPH_VALIDATE_DEBUG") == "1":   # eager self-consistency, diagnostics
+            torch.cuda.synchronize()
+            e1 = t.ddp.arena.grad_flat.detach().clone()
+            restore(t, s0)
+            with self._on_stream(), _graph_splitk_policy():
+                t._native_step(x, y)
+            t.global_step -= 1
+            torch.cuda.synchronize()
+            e2 = ((t.ddp.arena.grad_flat - e1).double().norm() / e1.double().norm()).item()
         for k in range(2):
             torch.cuda.synchronize()
             gs.append(t.ddp.arena.grad_flat.detach().clone())
@@ -215,17 +250,34 @@ class GraphedStep:
                     w = (r, n)
             return w
 
+        def whole(a, b):
+            r = (a - b).double().norm().item() / max(b.double().norm().item(), 1e-30)
+            return r if r == r else float("inf")
+
         ve, vr = worst(rep2, eager), worst(rep2, rep1)
-        ok = ve[0] <= VALIDATE_RTOL and vr[0] <= VALIDATE_RTOL
+        we, wr = whole(rep2, eager), whole(rep2, rep1)
+        ok = (we <= VALIDATE_RTOL and wr <= VALIDATE_RTOL and ve[0] <= VALIDATE_PARAM_RTOL
+              and vr[0] <= VALIDATE_PARAM_RTOL)
         if t.world_size > 1:
             ok = agree(ok, t.device)
-        self.validation = {"ok": ok, "replay_vs_eager": ve[0], "replay_vs_replay": vr[0],
+        self.validation = {"ok": ok, "replay_vs_eager": we, "replay_vs_replay": wr,
+                           "param_replay_vs_eager": ve[0], "param_replay_vs_replay": vr[0],
                            "worst": ve[1] if ve[0] >= vr[0] else vr[1]}
+        if e2 is not None:
+            self.validation["eager_vs_eager"] = e2
+            plan = t.ddp.plan
+            self.validation["bucket_replay_vs_eager"] = [
+                round(((rep2[o:o + n] - eager[o:o + n]).double().norm() /
+                       eager[o:o + n].double().norm().clamp_min(1e-30)).item(), 4)
+                for o, n in zip(plan.offsets, plan.numels)]
+            print(f"[graph validate] rank {t.rank}: {self.validation}", flush=True)
         if not ok:
             warnings.warn(
-                "hipGraph replay disagrees with eager execution (worst parameter gradient "
-                f"{self.validation['worst']}: replay-vs-eager {ve[0]:.3g}, replay-vs-replay {vr[0]:.3g}); "
-                "a kernel in the step is not replay-safe - running eagerly from now on")
+                f"hipGraph replay disagrees with eager execution (gradient replay-vs-eager {we:.3g}, "
+                f"replay-vs-replay {wr:.3g}; worst parameter {self.validation['worst']}: {ve[0]:.3g} / {vr[0]:.3g}); "
+                "a kernel in the step is not replay-safe - running eagerly from now on"
+                + (" (torch.backends.cudnn.deterministic is set: MIOpen then picks its CK grouped "
+                   "backward-data solver, which is wrong under replay)" if torch.backends.cudnn.deterministic else ""))
             self.failed = True
             t.global_step -= 1
             self.replays -= 1

@@ -19,11 +19,16 @@ SHIPPED_GEMM_DB = REPO / "gemm_db" / "tunableop_results.csv"
 
 # MIOpen solvers whose kernels compute wrong results under hipGraph replay.  Measured on MIOpen
 # 3.5 / ROCm 7.2 (profiles/graph_replay_miopen_r4.md): the CK grouped backward-weights solver
-# (ConvHipImplicitGemmGroupWrwXdlops) returns weight gradients that are wrong by 1e5-1e36
-# relative on replays of a captured fp32 NHWC conv backward, while eager calls of the same
-# solver are correct.  Find mode picks it on timing (it wins some shapes by ~15%), so which
-# boxes hit it varies from run to run.  MIOpen reads these switches once, at the first
-# convolution of the process: graph_safe_miopen() must run before any MIOpen call.
+# (ConvHipImplicitGemmGroupWrwXdlops) and the CK grouped backward-data solver (...GroupBwdXdlops)
+# return gradients wrong by up to 1e36 relative on replays of a captured conv backward, while
+# eager calls of the same solvers are correct (the CK grouped forward solver is replay-safe).
+# Find mode picks them on timing (they win some shapes by ~15%), so which boxes hit them varies
+# from run to run.  Only the backward-weights one honours a switch: neither
+# MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_HIP_GROUP_BWD_XDLOPS nor MIOPEN_DEBUG_GROUP_CONV_IMPLICIT_GEMM_HIP_BWD_XDLOPS
+# keeps the backward-data solver out of find (measured).  Against that one: the shipped find-db
+# pins the replay-safe ASM solver for the default fp32 ResNet-18 shapes, and engine/graph.py
+# validates the first replay and falls back to eager.  MIOpen reads these switches once, at the
+# first convolution of the process: graph_safe_miopen() must run before any MIOpen call.
 GRAPH_UNSAFE_MIOPEN_SOLVERS = ("MIOPEN_DEBUG_GROUP_CONV_IMPLICIT_GEMM_HIP_WRW_XDLOPS",)
 
 

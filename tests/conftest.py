@@ -19,6 +19,17 @@ def pytest_configure(config):
 
 
 @pytest.fixture(autouse=True)
+def _restore_cudnn_flags():
+    """Tests that set ``torch.backends.cudnn.deterministic`` (parity tests) must not leak it: in
+    deterministic mode MIOpen picks its CK grouped backward-data solver, which is wrong under
+    hipGraph replay (utils/env.py), so a later graph test would validate-and-fall-back."""
+    import torch
+    old = (torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic)
+    yield
+    torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic = old
+
+
+@pytest.fixture(autouse=True)
 def _collect_before_gpu_tests(request):
     """Collect the previous tests' garbage BEFORE a GPU test starts: a reference cycle collected in
     the middle of a later hipGraph capture runs destructors whose HIP calls are illegal there (one
