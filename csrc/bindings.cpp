@@ -1173,6 +1173,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         }, py::arg("M"), py::arg("Cout"), py::arg("K"), py::arg("graph") = false);
   m.def("conv_set_splitk", &dpt::conv_set_splitk, py::arg("mode"));
   m.def("conv_get_splitk", &dpt::conv_get_splitk);
+  m.def("conv_set_fwd_shape_policy", &dpt::conv_set_fwd_shape_policy, py::arg("bits"));
   m.def("conv_dgrad", &conv_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("pad"));
   m.def("conv_dgrad_bnstats", &conv_dgrad_bnstats, py::arg("grad_output"), py::arg("w"), py::arg("pad"),
         py::arg("bn_x"), py::arg("bn_mean"), py::arg("bn_coef"), py::arg("bn_y") = py::none(),

@@ -2168,6 +2168,25 @@ static bool conv_fwd_big(int v, ConvFwdArgs& a, hipStream_t s) {
   return true;
 }
 
+// Per-shape forward tile policy (variant 0 only; bits, conv_set_fwd_shape_policy):
+//   1: expanding 1x1 convs with the BN-statistics epilogue (C <= 128, Cout >= 2C) -> 256-row
+//      blocks with the LDS epilogue (variant 6): the statistics partials are summed over 256
+//      rows per block instead of 128 (64->256 @56: 0.155 -> 0.130 ms with statistics, MIOpen
+//      0.106 without; bench/conv_variant_sweep.py, profiles/conv_variant_sweep_r4.md);
+//   2: the 3x3 stride-2 256->256 conv (K = 2304, M >= 32768) -> the 8-wave 256x256 tile (variant
+//      9): 0.081 -> 0.069 ms, 1.05-1.08x MIOpen.
+static int g_fwd_shape_policy = 0;
+void conv_set_fwd_shape_policy(int bits) { g_fwd_shape_policy = bits; }
+static int fwd_shape_variant(const ConvFwdArgs& a, bool stats) {
+  if (a.f16) return 0;
+  if ((g_fwd_shape_policy & 1) && stats && a.R == 1 && a.S == 1 && a.stride == 1 && a.C <= 128 &&
+      a.Cout >= 2 * a.C)
+    return 6;
+  if ((g_fwd_shape_policy & 2) && a.R == 3 && a.stride == 2 && a.Cout == 256 && a.C == 256 && a.M >= 32768)
+    return 9;
+  return 0;
+}
+
 static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
                           int R, int S, int stride, int pad, float* psum, float* psq, bool bkn, hipStream_t s,
                           int Ho = 0, int Wo = 0, bool f16 = false, float* ws = nullptr) {
@@ -2185,8 +2204,9 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
   const bool wide = Cout % 128 == 0;
   a.n_tiles = Cout / (wide ? 128 : 64);
   a.mt256 = 0;
-  const int v = fwd_variant();
+  int v = fwd_variant();
   if (!bkn && maybe_split(a, ws, psum != nullptr, false, false, false, s)) return;
+  if (!bkn && v == 0) v = fwd_shape_variant(a, psum != nullptr);
   if (!bkn && !a.f16) {
     const int vb = (v >= 9 && v <= 13) ? v : v == 0 ? conv_big_auto(a.M, Cout, (int64_t)R * S * C) : 0;
     if (vb && conv_fwd_big(vb, a, s)) return;

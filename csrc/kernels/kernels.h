@@ -164,6 +164,7 @@ int conv_split_cols(int64_t M);
 void conv_set_splitk_policy(int tiles, int eager_tiles, int eager_min_k, int target);  // A/B knob
 void conv_set_splitk(int mode);  // 0 off / 1 auto (default, DPT_CONV_SPLITK) / 2 in-graph policy always
 int conv_get_splitk();
+void conv_set_fwd_shape_policy(int bits);  // per-shape forward tiles (conv_kernels.hip)
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
                      int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s, int Ho = 0,
                      int Wo = 0, bool f16 = false, float* ws = nullptr);

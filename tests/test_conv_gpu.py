@@ -911,3 +911,25 @@ def test_tail_relu_bitmask_matches_output_mask(cuda, shape):
     m = C_.conv_dgrad_bnstats(dy, wc, 0, x, mean, None, y, dres, bn_mask=mask)
     for u, v in zip(a[:3], m[:3]):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("shape,bits", [((4, 64, 20, 20, 256, 1, 1, 0), 1), ((2, 128, 28, 28, 512, 1, 1, 0), 1),
+                                        ((168, 256, 28, 28, 256, 3, 2, 1), 2)],
+                         ids=["1x1-64-256", "1x1-128-512", "3x3s2-256-big"])
+def test_fwd_shape_policy_matches_fp32(cuda, shape, bits):
+    """conv_set_fwd_shape_policy: the per-shape tiles (256-row blocks for expanding 1x1 convs with
+    statistics, the 8-wave 256x256 tile for the 3x3/2 256->256 conv) give the same output and BN
+    statistics partials as the fp32 reference."""
+    N, C, H, W, Cout, k, s, p = shape
+    x, w = _operands(cuda, N, C, H, W, Cout, k, seed=4)
+    C_ = ops.native()
+    C_.conv_set_fwd_shape_policy(bits)
+    try:
+        y, ps, pq = C_.conv_fwd(x, w, s, p, True)
+    finally:
+        C_.conv_set_fwd_shape_policy(0)
+    ref = F.conv2d(x.float(), w.float(), stride=s, padding=p)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+    yf = y.float()
+    torch.testing.assert_close(ps.sum(1), yf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(pq.sum(1), (yf * yf).sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
