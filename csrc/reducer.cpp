@@ -215,6 +215,16 @@ void Reducer::mark_ready(int64_t index) {
   }
 }
 
+// Same element order in memory: both dense, equal strides on every dimension longer than 1
+// (AccumulateGrad's layout contract ignores size-1 dimensions, so a 1x1 conv weight's gradient
+// may arrive with strides (C,1,1,1) for a channels_last (C,1,C,C) parameter - the same bytes).
+static bool same_dense_layout(const at::Tensor& g, const at::Tensor& v) {
+  if (!g.is_non_overlapping_and_dense() || !v.is_non_overlapping_and_dense()) return false;
+  for (int64_t d = 0; d < g.dim(); ++d)
+    if (g.size(d) > 1 && g.stride(d) != v.stride(d)) return false;
+  return true;
+}
+
 // Move the stolen gradients of bucket b into the arena (one launch per <= kGatherMax
 // tensors).  Gradients whose layout differs from their arena view (rare: a non-dense or
 // differently-strided gradient) go through a strided copy instead; parameters that got no
@@ -231,8 +241,7 @@ void Reducer::gather_bucket(int64_t b, hipStream_t s) {
     }
     const auto dt = g.scalar_type();
     const int kind = dt == at::kFloat ? 0 : dt == at::kBFloat16 ? 1 : dt == at::kHalf ? 2 : -1;
-    const bool same = kind >= 0 && g.is_cuda() && g.strides() == v.strides() && g.sizes() == v.sizes() &&
-                      g.is_non_overlapping_and_dense();
+    const bool same = kind >= 0 && g.is_cuda() && g.sizes() == v.sizes() && same_dense_layout(g, v);
     if (!same) {
       at::Tensor vv = v;  // strided / odd-dtype fallback on the current stream
       if (accumulate_) vv.add_(g.to(at::kFloat));
