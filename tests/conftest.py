@@ -18,6 +18,29 @@ def pytest_configure(config):
     graph_safe_miopen()
 
 
+# GPU suite order under ``-x``: cheap, deterministic kernel-numerics files first, then the engine
+# and comm tiers, and the long stochastic graph / training-parity runs last, so a failure there
+# can never hide the optimizer, scaler, reducer or kernel evidence.
+_FIRST = ("test_kernels_gpu.py", "test_bn_gpu.py", "test_conv_gpu.py", "test_attention_gpu.py",
+          "test_vit_gpu.py", "test_comm_gpu.py", "test_engine_gpu.py", "test_bench_contract.py",
+          "test_multirank_gpu.py", "test_serialized_gpu.py")
+_LAST = ("test_graph_replay_gpu.py", "test_graph_default_run_gpu.py", "test_bf16_parity_gpu.py",
+         "test_training_parity_gpu.py")
+
+
+def _order_key(item) -> int:
+    name = os.path.basename(str(item.fspath))
+    if name in _FIRST:
+        return _FIRST.index(name)
+    if name in _LAST:
+        return 1000 + _LAST.index(name)
+    return 500
+
+
+def pytest_collection_modifyitems(session, config, items):
+    items.sort(key=_order_key)        # stable: keeps the in-file order of each file
+
+
 @pytest.fixture(autouse=True)
 def _restore_cudnn_flags():
     """Tests that set ``torch.backends.cudnn.deterministic`` (parity tests) must not leak it: in
