@@ -90,6 +90,10 @@ def parse(argv=None):
                     help="testing: run as rank 0 of a --gpus-rank job on torch's fake process group (CPU)")
     ap.add_argument("--fail-rank", type=int, default=-1,
                     help="testing: this rank exits with status 17 right after the process group is up")
+    ap.add_argument("--allow-comm-fallback", action="store_true",
+                    help="N > 1: publish a record even when the framework RCCL communicator could not be "
+                         "created and the reducer fell back to torch's c10d communicator (default: exit 4 "
+                         "without measuring - a headline must come from the framework's RCCL reducer)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -388,6 +392,16 @@ def main(argv=None) -> int:
     model = build_model(args.model, args.num_classes, device, image_size=args.image_size,
                         channels_last=args.channels_last)
     trainer = Trainer(model, args, rank, ws, device, log=lambda s: None)
+    fallback = getattr(trainer.ddp, "comm_fallback_reason", None) if trainer.ddp is not None else None
+    if fallback and not a.allow_comm_fallback:
+        # fail closed: every rank took the same branch (parallel/comm.py agreement), so every rank
+        # exits here and the job's status is non-zero - no record of the wrong engine
+        print(f"bench: rank {rank}: --comm {a.comm} requested but the job fell back to torch's c10d "
+              f"communicator: {fallback} (pass --allow-comm-fallback to measure it anyway)", file=sys.stderr)
+        trainer.close()
+        if ws > 1:
+            dist.destroy_process_group()
+        return 4
     trainer.model.train()
     loader = SyntheticLoader(a.batch_size * 4, a.batch_size, args.image_size, args.num_classes, device,
                              channels_last=args.channels_last, pool=4, seed=rank)
@@ -497,7 +511,9 @@ def main(argv=None) -> int:
                                     else None,
                    "rccl_channels_opened": verify["rccl_channels_opened"] if verify else None,
                    "selftest_ok": verify["selftest_ok"] if verify else None,
-                   "rccl_version": _rccl_version()}
+                   "rccl_version": _rccl_version(),
+                   "requested": a.comm if a.impl == "native" and ws > 1 else None,
+                   "fallback_reason": fallback}
     rec["verify"] = verify
     rec["config"]["launcher"] = launcher
     rec["config"]["env"] = env_in_effect()

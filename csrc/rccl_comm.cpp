@@ -57,8 +57,8 @@ RcclComm::RcclComm(const std::string& unique_id, int rank, int world_size, int d
   // RCCL's init is collective and blocking: a peer that failed inside its own init leaves this
   // rank blocked in bootstrap forever.  Run it on a helper thread and give up after
   // init_timeout_s (the caller then agrees on a fallback with its peers, parallel/comm.py).  A
-  // thread that is still blocked is detached: its communicator is never used, and the process
-  // normally exits or falls back to torch's communicator.
+  // thread that is still blocked is detached and marked abandoned: if its init ever returns, it
+  // aborts the communicator it got (never used, and nobody else holds it to free it).
   auto st = std::make_shared<InitState>();
   std::thread worker([st, id, rank, world_size, device, min_ctas, max_ctas] {
     ncclComm_t c = nullptr;
@@ -77,6 +77,11 @@ RcclComm::RcclComm(const std::string& unique_id, int rank, int world_size, int d
       r = ncclCommInitRank(&c, world_size, id, rank);
     }
     std::lock_guard<std::mutex> lk(st->mu);
+    if (st->abandoned) {
+      // the caller gave up and already fell back: nobody will ever use or free this one
+      if (c != nullptr) ncclCommAbort(c);
+      c = nullptr;
+    }
     st->comm = c;
     st->result = r;
     st->done = true;
@@ -87,6 +92,7 @@ RcclComm::RcclComm(const std::string& unique_id, int rank, int world_size, int d
       ? (st->cv.wait(lk, [&] { return st->done; }), true)
       : st->cv.wait_for(lk, std::chrono::duration<double>(init_timeout_s), [&] { return st->done; });
   if (!finished) {
+    st->abandoned = true;   // under st->mu: the worker sees it when (if) its init returns
     lk.unlock();
     worker.detach();
     hipStreamDestroy(stream_);

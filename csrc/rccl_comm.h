@@ -76,6 +76,7 @@ class RcclComm : public Collective {
     std::mutex mu;
     std::condition_variable cv;
     bool done = false;
+    bool abandoned = false;   // the constructor timed out: a late-finishing worker aborts its comm
     ncclComm_t comm = nullptr;
     ncclResult_t result = ncclSuccess;
   };

@@ -76,9 +76,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="gradient bucket size cap in MiB")
     g.add_argument("--first-bucket-mb", default=1.0, type=float,
                    help="first (last-layer) bucket cap in MiB")
-    g.add_argument("--last-bucket-mb", default=1.0, type=float,
+    g.add_argument("--last-bucket-mb", default=0.0, type=float,
                    help="native impl: cap of the bucket that becomes ready last (its all-reduce can not "
-                        "overlap backward); 0 = torch DDP's plan, where it is whatever is left over")
+                        "overlap backward); 0 (default) = torch DDP's plan, where it is whatever is left "
+                        "over; bench.py passes 1.0")
     g.add_argument("--no-broadcast-buffers", dest="broadcast_buffers", action="store_false",
                    help="do not broadcast BN buffers from rank 0 before each forward")
     g.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],

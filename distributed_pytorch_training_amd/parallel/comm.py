@@ -38,6 +38,7 @@ RCCL's init log to check the communicator got what was asked.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -48,6 +49,23 @@ from .. import ops
 COMM_KINDS = ("rccl", "c10d", "host", "host-async")
 _HOST_GROUP = None
 _ASYNC_GROUP = None
+# Why the last ``make_comm(kind="rccl")`` of this process ended on the c10d fallback (None: it did
+# not).  NativeDDP copies it to ``comm_fallback_reason``; bench.py fails closed on it.
+LAST_FALLBACK_REASON: Optional[str] = None
+# Upper bound of the RCCL init wait; tied to the process-group timeout (``init_timeout_for``).
+MAX_INIT_TIMEOUT_S = 300.0
+
+
+def init_timeout_for(pg_timeout_s: Optional[float]) -> float:
+    """How long a rank waits inside ``ncclCommInitRank`` before giving up.
+
+    A rank whose own init failed goes straight to the post-init MIN agreement, a control-plane
+    collective bounded by the process-group timeout (``--dist-timeout``).  Its peers must reach
+    that agreement first, so their init wait has to end well inside that timeout: half of it,
+    capped at ``MAX_INIT_TIMEOUT_S``."""
+    if pg_timeout_s is None or pg_timeout_s <= 0:
+        return MAX_INIT_TIMEOUT_S
+    return min(MAX_INIT_TIMEOUT_S, 0.5 * float(pg_timeout_s))
 
 
 def _host_group():
@@ -77,9 +95,17 @@ def _host_broadcast(t: torch.Tensor, root: int) -> None:
 
 def make_comm(device: torch.device, rank: int, world_size: int, kind: str = "rccl",
               timeout_s: Optional[float] = None, rccl_channels: int = 0,
-              exit_grace_s: float = 30.0, init_timeout_s: float = 300.0):
-    """Create the device collective on ``device`` (GPU) or return None (CPU/gloo path)."""
+              exit_grace_s: float = 30.0, init_timeout_s: Optional[float] = None):
+    """Create the device collective on ``device`` (GPU) or return None (CPU/gloo path).
+
+    ``init_timeout_s`` defaults to ``init_timeout_for(timeout_s)``."""
+    global LAST_FALLBACK_REASON
+    LAST_FALLBACK_REASON = None
+    if init_timeout_s is None:
+        init_timeout_s = init_timeout_for(timeout_s)
     if device.type != "cuda":
+        if kind == "rccl" and world_size > 1 and "DPT_TEST_FAIL_COMM_INIT_RANK" in os.environ:
+            _cpu_rehearsal(rank, world_size)
         return None
     if kind not in COMM_KINDS:
         raise ValueError(f"unknown communicator kind {kind!r}; expected one of {COMM_KINDS}")
@@ -108,6 +134,16 @@ def make_comm(device: torch.device, rank: int, world_size: int, kind: str = "rcc
     return comm
 
 
+def _cpu_rehearsal(rank: int, world_size: int) -> None:
+    """Testing (``DPT_TEST_FAIL_COMM_INIT_RANK`` set, gloo ranks on the CPU): run the bootstrap
+    agreement of ``rccl_or_fallback`` with a stand-in unique id, so the fallback decision and
+    ``LAST_FALLBACK_REASON`` (what bench.py fails closed on) are exercised without a GPU.  The
+    CPU path has no device collective either way: the reducer keeps its gloo callback."""
+    rccl_or_fallback(new_uid=lambda: b"\0" * 128, create=lambda uid: "cpu-stand-in",
+                     fallback=lambda: None, rank=rank, world_size=world_size,
+                     flag_device=torch.device("cpu"))
+
+
 def _agree(ok: bool, flag_device) -> bool:
     on = flag_device if dist.get_backend() == "nccl" else "cpu"
     flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=on)
@@ -127,12 +163,13 @@ def rccl_or_fallback(new_uid, create, fallback, rank: int, world_size: int, flag
     2. before init, a MIN all-reduce of "ready" (the test hook ``DPT_TEST_FAIL_COMM_INIT_RANK``
        makes one rank not ready) - any rank not ready: nobody enters RCCL;
     3. after init, a MIN all-reduce of "created" - a communicator some ranks built and others did
-       not would hang the first collective, so the built ones are destroyed.
+       not would hang the first collective, so the built ones are aborted.
+
+    Every fallback records its reason in ``LAST_FALLBACK_REASON``.
 
     A failure INSIDE ``ncclCommInitRank`` on some ranks only is bounded by the communicator's
     init timeout (csrc/rccl_comm.cpp: the blocked ranks give up and reach step 3), then every
     rank takes the fallback.  ``world_size == 1`` skips the agreements."""
-    import os
     import warnings
 
     err = None
@@ -152,9 +189,9 @@ def rccl_or_fallback(new_uid, create, fallback, rank: int, world_size: int, flag
         elif not ready and err is None:
             err = RuntimeError("injected pre-init failure (DPT_TEST_FAIL_COMM_INIT_RANK)")
         if not _agree(ready, flag_device):
-            warnings.warn(f"framework RCCL communicator not created on any rank ({err or 'another rank was not ready'}); "
-                          "falling back to --comm c10d")
-            return fallback()
+            reason = f"framework RCCL communicator not created on any rank ({err or 'another rank was not ready'})"
+            warnings.warn(reason + "; falling back to --comm c10d")
+            return _fell_back(reason, fallback)
     else:
         uid = new_uid()
     comm = None
@@ -167,11 +204,19 @@ def rccl_or_fallback(new_uid, create, fallback, rank: int, world_size: int, flag
         ok = _agree(ok, flag_device)
     if not ok:
         if comm is not None:
-            comm.destroy()
-        warnings.warn(f"framework RCCL communicator unavailable on some rank "
-                      f"({err if err is not None else 'another rank'}); falling back to --comm c10d")
-        return fallback()
+            # its peers never finished (or gave up on) the collective init: ncclCommDestroy could
+            # block on them, ncclCommAbort does not
+            (comm.abort if hasattr(comm, "abort") else comm.destroy)()
+        reason = f"framework RCCL communicator unavailable on some rank ({err if err is not None else 'another rank'})"
+        warnings.warn(reason + "; falling back to --comm c10d")
+        return _fell_back(reason, fallback)
     return comm
+
+
+def _fell_back(reason: str, fallback):
+    global LAST_FALLBACK_REASON
+    LAST_FALLBACK_REASON = reason
+    return fallback()
 
 
 def _pg_comm(C, dev: int):

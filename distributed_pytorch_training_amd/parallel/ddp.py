@@ -33,6 +33,7 @@ import torch.nn as nn
 from .. import ops
 from ..ops import reference
 from .bucketing import BucketPlan, plan_for_arena
+from . import comm as comm_mod
 from .comm import broadcast_, make_comm
 from .flat import BufferArena, FlatArena
 
@@ -77,6 +78,10 @@ class NativeDDP(nn.Module):
         self.comm = comm if comm is not None else (
             make_comm(self.device, rank, world_size, kind=comm_kind, timeout_s=timeout_s,
                       rccl_channels=rccl_channels) if world_size > 1 else None)
+        # requested rccl, got torch's c10d communicator: why (None when nothing fell back)
+        self.comm_requested = comm_kind if comm is None and world_size > 1 else None
+        self.comm_fallback_reason = (comm_mod.LAST_FALLBACK_REASON
+                                     if comm is None and world_size > 1 and comm_kind == "rccl" else None)
         if world_size > 1:
             broadcast_(self.arena.param_flat, self.comm, 0)
             for t in self.buffers_arena.tensors():

@@ -144,6 +144,40 @@ def test_bench_launcher_world_size_mismatch_fails(tmp_path):
     assert not _json_lines(r.stdout)
 
 
+def _fallback_run(tmp_path, extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["DPT_TEST_FAIL_COMM_INIT_RANK"] = "1"      # rank 1 is never ready: every rank falls back
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *extra, *TINY],
+                          cwd=tmp_path, capture_output=True, text=True, timeout=600, env=env)
+
+
+def test_bench_fails_closed_on_comm_fallback(tmp_path):
+    """when the framework RCCL communicator cannot be created and the ranks
+    fall back to torch's communicator, the N > 1 bench exits non-zero and publishes no record."""
+    r = _fallback_run(tmp_path, [])
+    assert r.returncode == 4, (r.returncode, r.stderr[-3000:])
+    assert not _json_lines(r.stdout)
+    assert "fell back to torch's c10d communicator" in r.stderr
+    assert "DPT_TEST_FAIL_COMM_INIT_RANK" in r.stderr          # the reason travels with the error
+
+
+def test_bench_allowed_comm_fallback_is_recorded(tmp_path):
+    r = _fallback_run(tmp_path, ["--allow-comm-fallback"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    comm = lines[0]["comm"]
+    # rank 0 writes the record; its reason is that another rank was not ready
+    assert comm["requested"] == "rccl" and "not created on any rank" in comm["fallback_reason"]
+
+
+def test_bench_no_fallback_reason_without_fallback(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *TINY], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _json_lines(r.stdout)[0]["comm"]["fallback_reason"] is None
+
+
 @pytest.mark.gpu
 def test_bench_self_launch_two_ranks_on_one_gpu(tmp_path):
     """The self-launch path on a real GPU: ``bench.py --gpus 2 --rehearse-shared-gpu`` without

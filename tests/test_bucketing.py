@@ -88,3 +88,20 @@ def test_last_bucket_cap_resnet50_defaults():
     assert ref[-1] == pytest.approx(9.27, abs=0.02)
     assert got[-1] <= 1.0 and sum(got) == pytest.approx(sum(ref))
     assert got[:len(ref) - 1] == ref[:-1]
+
+
+@pytest.mark.parametrize("name,classes", [("resnet18", 10), ("resnet50", 1000)])
+def test_default_cli_plan_is_torch_ddp_plan(name, classes):
+    """additive defaults reproduce the reference.  The plan NativeDDP builds from the
+    default CLI (``--bucket-cap-mb 25 --first-bucket-mb 1 --last-bucket-mb 0``) is exactly
+    ``dist._compute_bucket_assignment_by_size`` with 1 MiB / 25 MiB caps (reference
+    train_ddp.py:305-310, DDP defaults)."""
+    from distributed_pytorch_training_amd.config import parse_args
+    args = parse_args([])
+    assert (args.bucket_cap_mb, args.first_bucket_mb, args.last_bucket_mb) == (25.0, 1.0, 0.0)
+    model = build_model(name, classes)
+    params = list(reversed(list(model.parameters())))
+    arena = FlatArena(params)
+    plan = plan_for_arena(arena, args.bucket_cap_mb, args.first_bucket_mb, args.last_bucket_mb)
+    ref, _ = dist._compute_bucket_assignment_by_size(params, [1 * MiB, 25 * MiB], [False] * len(params))
+    assert plan.members == [list(b) for b in ref]
