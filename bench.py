@@ -21,13 +21,17 @@ autocast, channels_last), loss, loss scaling, backward with the bucketed RCCL al
 fused SGD (lr 0.1, momentum 0.9, wd 5e-4) with the device-resident scaler, device metrics.
 W untimed warmup steps, then EXACTLY K steps bracketed by barrier + device synchronize on
 both sides; the MAX step time over ranks is reported.  Per-GPU batch is fixed as N grows
-(weak scaling).  ``vs_baseline`` divides by N x the stock-PyTorch-ROCm single-GPU number
-measured on MI355X with the same harness (``--impl torch``), since the
-reference publishes no numbers.
+(weak scaling).  The reference publishes no numbers, so the baseline is stock PyTorch-ROCm
+running the reference's mechanics (torch DDP, foreach SGD, torch.amp.GradScaler: ``--impl
+torch``) on the SAME box: after the native run, a fresh child job measures it with the same
+model, batch, dtype and steps (``--stock-baseline``), and ``vs_baseline`` = value / that number.
+The round-1 constant from another box stays in the record as
+``baseline.stock_reference_constant`` and is the divisor only when the child job fails.
 """
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import signal
@@ -94,6 +98,13 @@ def parse(argv=None):
                     help="N > 1: publish a record even when the framework RCCL communicator could not be "
                          "created and the reducer fell back to torch's c10d communicator (default: exit 4 "
                          "without measuring - a headline must come from the framework's RCCL reducer)")
+    ap.add_argument("--stock-baseline", default="auto", choices=["auto", "on", "off"],
+                    help="after the native run, measure stock PyTorch-ROCm (--impl torch: torch DDP, foreach "
+                         "SGD, torch.amp.GradScaler) with the same model/batch/dtype/steps in a FRESH child "
+                         "job on the same GPUs; vs_baseline is then value / that number (auto: on for the "
+                         "native engine on GPUs)")
+    ap.add_argument("--stock-timeout", type=float, default=420.0,
+                    help="seconds the stock child job may take before it is killed (then no same-box number)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -303,6 +314,56 @@ def _rank_devices(device, ws):
     return [mine]
 
 
+def _stock_argv(a, json_out: str) -> list:
+    """The same benchmark on the stock engine: same model, per-GPU batch, dtype, layout, steps."""
+    argv = ["--gpus", str(a.gpus), "--impl", "torch", "--steps", str(a.steps), "--warmup", str(a.warmup),
+            "--model", a.model, "--batch-size", str(a.batch_size), "--image-size", str(a.image_size),
+            "--num-classes", str(a.num_classes), "--amp-dtype", a.amp_dtype, "--optimizer", a.optimizer,
+            "--bucket-cap-mb", str(a.bucket_cap_mb), "--profile-steps", "0", "--stock-baseline", "off",
+            "--json-out", json_out]
+    for flag in ("no_amp", "no_channels_last", "find"):
+        if getattr(a, flag):
+            argv.append("--" + flag.replace("_", "-"))
+    return argv
+
+
+def run_stock_baseline(a) -> dict:
+    """Stock PyTorch-ROCm on the same box ("same MI355X box ... same harness"), in a
+    fresh child job started AFTER this job's GPU work is done and its memory released: a new
+    interpreter (this process keeps running; nothing is exec'd over a process that touched the
+    GPU) that self-launches ``--gpus`` ranks of ``--impl torch``.  Launcher variables of this
+    job are stripped so the child picks its own rendezvous.  Returns its record's numbers or
+    the reason there are none."""
+    import tempfile
+    fd, out = tempfile.mkstemp(prefix="dpt_stock_", suffix=".json")
+    os.close(fd)
+    drop = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
+            "MASTER_PORT", "GROUP_WORLD_SIZE", "ROLE_WORLD_SIZE", CHILD_MARK, "NCCL_DEBUG", "NCCL_DEBUG_FILE",
+            "NCCL_DEBUG_SUBSYS")
+    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
+    cmd = [sys.executable, os.path.abspath(__file__), *_stock_argv(a, out)]
+    t0 = time.time()
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.stock_timeout)
+        with open(out) as f:
+            lines = [json.loads(l) for l in f if l.startswith("{")]
+        if r.returncode != 0 or not lines:
+            return {"error": f"stock job exited {r.returncode}: {r.stderr[-400:]}", "wall_s": round(time.time() - t0, 1)}
+        rec = lines[-1]
+        return {"img_s": rec["value"], "ms_per_step": rec["ms_per_step"], "n_gpus": rec["n_gpus"],
+                "steps": rec["steps"], "warmup": rec["warmup"], "impl": rec["config"]["impl"],
+                "wall_s": round(time.time() - t0, 1), "cmd": "bench.py " + " ".join(_stock_argv(a, "<tmp>"))}
+    except subprocess.TimeoutExpired:
+        return {"error": f"stock job exceeded --stock-timeout {a.stock_timeout:.0f} s"}
+    except (OSError, ValueError, KeyError) as e:
+        return {"error": repr(e)[:400]}
+    finally:
+        try:
+            os.remove(out)
+        except OSError:
+            pass
+
+
 def train_args(a):
     from distributed_pytorch_training_amd.config import parse_args
 
@@ -457,15 +518,16 @@ def main(argv=None) -> int:
         prof_window = {"steps": a.profile_steps, "ms_per_step": round(1e3 * pdt / a.profile_steps, 3),
                        "value": round(a.batch_size * ws * a.profile_steps / pdt, 2)}
 
-    base = STOCK_TORCH_1GPU.get(a.batch_size) if (args.model == "resnet50" and args.amp and
-                                                  args.amp_dtype == "bf16" and args.image_size == 224) else None
+    const = STOCK_TORCH_1GPU.get(a.batch_size) if (args.model == "resnet50" and args.amp and
+                                                   args.amp_dtype == "bf16" and args.image_size == 224) else None
     rec = {
         "metric": "images/sec (whole node) ResNet-50 bf16 training" if args.model == "resnet50"
                   else f"images/sec (whole node) {args.model} training",
         "value": round(value, 2), "unit": "images/s", "n_gpus": ws, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(value / (base * ws), 4) if base else None,
+        "vs_baseline": round(value / (const * ws), 4) if const else None,   # replaced below when the
+                                                                            # same-box stock run succeeds
         "dtype": (args.amp_dtype if args.amp else "fp32"), "data": "synthetic",
         "config": {"model": args.model, "global_batch": a.batch_size * ws, "per_gpu_batch": a.batch_size,
                    "seq_len": None, "image_size": args.image_size, "parallelism": f"dp{ws}",
@@ -480,7 +542,9 @@ def main(argv=None) -> int:
                    "weight_shadow": bool(trainer.ddp is not None and trainer.ddp.shadow_flat is not None),
                    "cuda_graph": bool(a.cuda_graph and trainer.graphed is not None
                                       and trainer.graphed.graph is not None)},
-        "baseline": {"stock_torch_1gpu_img_s": base, "source": "BASELINE.md (MI355X, --impl torch)"},
+        "baseline": {"stock_reference_constant": (round(const * ws, 2) if const else None),
+                     "stock_reference_constant_source": "BASELINE.md round-1 stock run x N (another box)",
+                     "stock_same_box_img_s": None, "vs_baseline_source": "stock_reference_constant"},
         "warmup_seconds": round(warm_s, 1),
     }
     # BASELINE's second headline number, measured in the second (profiled) window; null when
@@ -517,6 +581,37 @@ def main(argv=None) -> int:
     rec["verify"] = verify
     rec["config"]["launcher"] = launcher
     rec["config"]["env"] = env_in_effect()
+    if ws > 1:
+        dist.barrier()
+    trainer.close()
+    stock_on = a.stock_baseline == "on" or (a.stock_baseline == "auto" and a.impl == "native"
+                                            and device.type == "cuda" and not a.rehearse_shared_gpu
+                                            and not a.fake_pg)
+    if stock_on:
+        # free this job's GPU memory, then rank 0 runs the stock job on the same GPUs while the
+        # other ranks wait on the TCPStore (host side: no collective kernel spinning on a GPU)
+        del trainer, model, batches, loader, ddp, comm
+        import gc
+        gc.collect()
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+            torch.cuda.empty_cache()
+        if ws > 1:
+            dist.barrier()
+        stock = run_stock_baseline(a) if rank == 0 else None
+        if ws > 1:
+            store = dist.distributed_c10d._get_default_store()
+            key = "dpt_bench_stock_done"
+            if rank == 0:
+                store.set(key, "1")
+            else:
+                store.wait([key], datetime.timedelta(seconds=a.stock_timeout + 120))
+        if rank == 0:
+            rec["baseline"]["stock_same_box"] = stock
+            if stock.get("img_s"):
+                rec["baseline"]["stock_same_box_img_s"] = stock["img_s"]
+                rec["baseline"]["vs_baseline_source"] = "stock_same_box (fresh child job, --impl torch)"
+                rec["vs_baseline"] = round(value / stock["img_s"], 4)
     if rank == 0:
         line = json.dumps(rec)
         print(line, flush=True)
@@ -525,8 +620,6 @@ def main(argv=None) -> int:
                 f.write(line + "\n")
     if ws > 1:
         dist.barrier()
-    trainer.close()
-    if ws > 1:
         dist.destroy_process_group()
     if verify is not None and verify["ok"] is False:
         print(f"bench: rank {rank}: self-verification FAILED: {json.dumps(verify)}", file=sys.stderr)

@@ -1263,7 +1263,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              return pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>()->getSize();
            })
       .def_property_readonly("async_mode", &dpt::HostBridgeComm::async_mode)
-      .def_property_readonly("completed", &dpt::HostBridgeComm::completed);
+      .def_property_readonly("completed", &dpt::HostBridgeComm::completed)
+      .def("release_graph_resources", &dpt::HostBridgeComm::release_graph_resources);
 
   // the Collective contract over a torch c10d group on device memory (RCCL through
   // ProcessGroupNCCL): the framework communicator's fallback and A/B arm (csrc/pg_comm.h)

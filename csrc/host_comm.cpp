@@ -1,5 +1,8 @@
 #include "host_comm.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 #include <torch/extension.h>  // at::Tensor <-> torch.Tensor caster for the callbacks
 
 #include <stdexcept>
@@ -70,10 +73,37 @@ void HostBridgeComm::destroy() {
     host_ = nullptr;
     host_bytes_ = 0;
   }
-  for (auto& kv : staging_) hipHostFree(kv.second);
+  if (!graph_jobs_.empty()) {
+    // A graph that captured these collectives may still exist (the caller did not reset it
+    // first).  Its host nodes point at the jobs and its copy nodes at the staging buffers, so
+    // neither is freed: the jobs are retired (self = nullptr, a replay aborts loudly in
+    // host_fn) and both are kept for the life of the process.
+    static std::mutex mu;
+    static std::vector<std::unique_ptr<Job>>* retired = new std::vector<std::unique_ptr<Job>>();
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& j : graph_jobs_) {
+      j->self = nullptr;
+      retired->push_back(std::move(j));
+    }
+    graph_jobs_.clear();
+  }
+  for (auto& kv : staging_)
+    if (!graph_staging_.count(kv.second)) hipHostFree(kv.second);
   staging_.clear();
   graph_staging_.clear();
-  graph_jobs_.clear();  // the device is drained above: no replay can still reference them
+}
+
+size_t HostBridgeComm::release_graph_resources() {
+  const size_t n = graph_jobs_.size();
+  if (n == 0) return 0;
+  {
+    std::unique_ptr<py::gil_scoped_release> rel;
+    if (PyGILState_Check()) rel = std::make_unique<py::gil_scoped_release>();
+    DPT_HIP_THROW(hipDeviceSynchronize());  // no replay still in flight
+  }
+  graph_jobs_.clear();
+  graph_staging_.clear();  // the buffers stay cached in staging_ for eager reuse; trim may free them
+  return n;
 }
 
 // Release the cached pinned buffers no captured graph references.  Only called outside capture;
@@ -131,6 +161,11 @@ void HostBridgeComm::host_fn(void* arg) {
   Job* j = static_cast<Job*>(arg);
   std::unique_ptr<Job> owned(j->persistent ? nullptr : j);  // graph jobs are reused per replay
   HostBridgeComm* self = j->self;
+  if (self == nullptr) {
+    std::fprintf(stderr, "HostBridgeComm: a hipGraph replayed a host collective whose communicator was "
+                         "destroyed (reset the graph before closing the trainer); aborting\n");
+    std::abort();
+  }
   try {
     if (self->aborted_.load()) throw std::runtime_error("aborted before the collective ran");
     std::vector<at::Tensor> v{

@@ -61,6 +61,10 @@ class HostBridgeComm : public Collective {
   bool async_mode() const { return async_; }
   // Host collectives the async host functions have completed.
   uint64_t completed() const { return completed_.load(); }
+  // Free the jobs and pinned staging buffers of collectives recorded into a hipGraph.  Call it
+  // once every graph that captured them is gone (engine/graph.py GraphedStep.reset); a later
+  // capture records new ones.  Returns the number of jobs released.
+  size_t release_graph_resources();
 
  private:
   struct Job {
@@ -71,7 +75,9 @@ class HostBridgeComm : public Collective {
     size_t count;
     WireType t;
     // Enqueued while a hipGraph was being captured: the host node runs once per REPLAY, so the
-    // job outlives every call (owned by graph_jobs_, freed at destroy()), never by host_fn.
+    // job outlives every call (owned by graph_jobs_, freed by release_graph_resources()), never
+    // by host_fn.  destroy() without that release retires the job with self = nullptr: a replay
+    // after destroy then aborts the process with a message instead of touching freed memory.
     bool persistent;
   };
   using StagingKey = std::tuple<void*, size_t, hipStream_t>;

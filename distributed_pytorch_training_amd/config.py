@@ -142,9 +142,9 @@ def build_parser() -> argparse.ArgumentParser:
                         "(the reference's step-line definition, train_ddp.py:196,224) instead of the "
                         "default sync-to-sync window, which has no per-step host sync")
     g.add_argument("--fault-inject", default=None, type=str, metavar="rank=R,step=S|rank=R,epoch=E",
-                   help="testing: rank R exits abruptly with status 17 before global optimizer step S, or at "
-                        "the start of 0-based epoch E; once per output dir (a marker file there lets a "
-                        "restarted job run through)")
+                   help="testing: rank R exits abruptly with status 17 before global optimizer step S (every "
+                        "run), or at the start of 0-based epoch E (once per output dir: a marker file there "
+                        "lets a restarted job run through)")
     g.add_argument("--cuda-graph", dest="cuda_graph", action="store_true", default=None,
                    help="capture the training step in a hipGraph (static shapes, native impl); "
                         "default: on when the step is launch-bound (per-GPU batch x pixels <= 2^18, "

@@ -187,6 +187,20 @@ class GraphedStep:
             return self._validated_first_replay(x, y)
         return self._replay(x, y)
 
+    def reset(self) -> None:
+        """Drop the captured graph, then free what the communicator kept alive for it (the
+        asynchronous host bridge's host-node jobs and pinned staging buffers).  Called when the
+        step falls back to eager and by ``Trainer.close`` (before the communicator is destroyed)."""
+        if self.graph is None:
+            return
+        torch.cuda.synchronize()
+        self.graph.reset()
+        self.graph = None
+        comm = self.trainer.ddp.comm if self.trainer.ddp is not None else None
+        release = getattr(comm, "release_graph_resources", None)
+        if release is not None:
+            release()
+
     def _replay(self, x: torch.Tensor, y: torch.Tensor):
         t = self.trainer
         with self._on_stream():
@@ -282,6 +296,7 @@ class GraphedStep:
             t.global_step -= 1
             self.replays -= 1
             restore(t, s0)
+            self.reset()
             with self._on_stream():
                 return t._native_step(x, y)
         return out

@@ -393,6 +393,8 @@ class Trainer:
             self.ddp.refresh_shadow()
 
     def close(self) -> None:
+        if self.graphed is not None:
+            self.graphed.reset()        # before the communicator its host nodes may reference
         if self.ddp is not None:
             self.ddp.close()
 

@@ -144,6 +144,26 @@ def test_bench_launcher_world_size_mismatch_fails(tmp_path):
     assert not _json_lines(r.stdout)
 
 
+@pytest.mark.parametrize("n", [1, 2])
+def test_bench_same_box_stock_baseline(tmp_path, n):
+    """the record carries a stock (--impl torch) number measured by a fresh
+    child job of the same shape right after the native run, and vs_baseline divides by it."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--stock-baseline", "on",
+                        *TINY], cwd=tmp_path, capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    rec = lines[0]
+    _check(rec, n)
+    b = rec["baseline"]
+    stock = b["stock_same_box"]
+    assert stock["impl"] == "torch" and stock["n_gpus"] == n and stock["steps"] == 2, stock
+    assert b["stock_same_box_img_s"] == stock["img_s"] > 0
+    assert rec["vs_baseline"] == pytest.approx(rec["value"] / stock["img_s"], rel=1e-2)
+    assert b["vs_baseline_source"].startswith("stock_same_box")
+
+
 def _fallback_run(tmp_path, extra):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["DPT_TEST_FAIL_COMM_INIT_RANK"] = "1"      # rank 1 is never ready: every rank falls back

@@ -35,3 +35,24 @@ def test_fire_exits_once_per_output_dir(tmp_path):
     assert first.returncode == FAULT_EXIT_CODE and "injected fault at epoch 1" in first.stdout
     again = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
     assert again.returncode == 0 and "survived" in again.stdout
+
+
+def test_step_faults_fire_every_run(tmp_path):
+    """a step fault leaves no marker - the same fault test run twice in one output
+    directory injects the fault both times (never a silent clean pass)."""
+    code = ("from distributed_pytorch_training_amd.utils.fault import FaultSpec; "
+            f"FaultSpec.parse('rank=0,step=3').fire({str(tmp_path)!r}); print('survived')")
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    for _ in range(2):
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+        assert r.returncode == FAULT_EXIT_CODE and "injected fault at step 3" in r.stdout
+    assert not list(tmp_path.iterdir())
+
+
+def test_suppressed_epoch_fault_warns_once(tmp_path):
+    spec = FaultSpec.parse("rank=0,epoch=1")
+    spec.marker(str(tmp_path)).touch()
+    logs = []
+    for _ in range(3):
+        spec.fire(str(tmp_path), logs.append)
+    assert len(logs) == 1 and "NOT injected" in logs[0]
