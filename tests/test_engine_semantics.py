@@ -5,6 +5,7 @@
 * ``--warmup-steps`` keeps the first steps out of the throughput windows;
 * ``--ref-throughput`` times each step after the loader yields (train_ddp.py:196,224).
 """
+import pytest
 import torch
 
 from distributed_pytorch_training_amd.config import parse_args
@@ -82,3 +83,51 @@ def test_step_state_snapshot_restore_round_trips_a_step():
     tr.train_step(x, y)
     for k, v in step_state(tr).items():
         assert torch.equal(v, after[k]), k
+
+
+def _grads(n=4, size=64, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    base = torch.randn(n * size, generator=g)
+    return base, (lambda flat: [flat[i * size:(i + 1) * size] for i in range(n)]), [f"p{i}" for i in range(n)]
+
+
+def test_replay_check_accepts_rounding_noise():
+    """engine/graph.py check_replay: replays within the measured eager noise pass."""
+    from distributed_pytorch_training_amd.engine.graph import check_replay
+    base, views, names = _grads()
+    noise = lambda k: base + 1e-7 * torch.randn(base.shape, generator=torch.Generator().manual_seed(k))
+    g = {"eager1": noise(1), "eager2": noise(2), "replay1": noise(3), "replay2": noise(4)}
+    v = check_replay(g, views, names, fp32=True)
+    assert v["ok"], v
+
+
+@pytest.mark.parametrize("err", [0.3, 0.05])
+def test_replay_check_rejects_a_wrong_parameter(err):
+    """A reproducible error on ONE parameter's replayed gradient (a replay-unsafe kernel) fails,
+    even when the whole-arena difference is small."""
+    from distributed_pytorch_training_amd.engine.graph import check_replay
+    base, views, names = _grads(n=64)
+    bad = base.clone()
+    views(bad)[5].mul_(1 + err)
+    g = {"eager1": base, "eager2": base.clone(), "replay1": bad, "replay2": bad.clone()}
+    v = check_replay(g, views, names, fp32=False)
+    assert not v["ok"] and v["worst"] == "p5", v
+
+
+def test_replay_check_rejects_irreproducible_replays():
+    """Replays that disagree with each other (a racy / stale read) fail even if one is close to eager."""
+    from distributed_pytorch_training_amd.engine.graph import check_replay
+    base, views, names = _grads()
+    other = base + 1e-2 * torch.randn(base.shape, generator=torch.Generator().manual_seed(9))
+    g = {"eager1": base, "eager2": base.clone(), "replay1": other, "replay2": base.clone()}
+    v = check_replay(g, views, names, fp32=True)
+    assert not v["ok"], v
+
+
+def test_replay_check_nan_fails():
+    from distributed_pytorch_training_amd.engine.graph import check_replay
+    base, views, names = _grads()
+    bad = base.clone()
+    bad[3] = float("nan")
+    g = {"eager1": base, "eager2": base.clone(), "replay1": bad, "replay2": bad.clone()}
+    assert not check_replay(g, views, names, fp32=True)["ok"]

@@ -101,3 +101,38 @@ def test_validation_rejects_a_step_that_is_not_replay_safe(cuda):
     assert G.replays == 0
     assert tr.global_step == G.warmup + 1
     assert tr.metrics[2].item() == 8 * (G.warmup + 1)    # the validated call still counts one step
+
+
+def test_validation_rejects_an_injected_30pct_error_on_one_parameter(cuda):
+    """a replay that is wrong by 30 % on ONE parameter - what a replay-unsafe kernel
+    that reads stale data produces - must fail the noise-relative validation and fall back."""
+    torch.manual_seed(0)
+    model = build_model("resnet18", 10, cuda, image_size=32, channels_last=True)
+    args = parse_args(["--dataset", "synthetic", "--image-size", "32", "--num-classes", "10", "--cuda-graph"])
+    tr = Trainer(model, args, 0, 1, cuda, log=lambda s: None)
+    G = tr.graphed
+    names = list(tr.ddp.arena.names)
+    target = names.index("layer3.0.conv1.weight")
+
+    def inject(grad_flat, arena):
+        arena.views(grad_flat)[target].mul_(1.3)
+
+    G.inject = inject
+    g = torch.Generator(device=cuda).manual_seed(5)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        for _ in range(G.warmup + 1):
+            x = torch.randn(128, 3, 32, 32, device=cuda, generator=g).contiguous(memory_format=torch.channels_last)
+            tr.train_step(x, torch.randint(0, 10, (128,), device=cuda, generator=g))
+    torch.cuda.synchronize()
+    v = G.validation
+    assert G.failed and not v["ok"] and v["worst"] == "layer3.0.conv1.weight", v
+    assert any("not replay-safe" in str(m.message) for m in w)
+    # without the injection the same configuration validates (the check is not simply strict)
+    tr2 = Trainer(build_model("resnet18", 10, cuda, image_size=32, channels_last=True), args, 0, 1, cuda,
+                  log=lambda s: None)
+    for _ in range(tr2.graphed.warmup + 1):
+        x = torch.randn(128, 3, 32, 32, device=cuda, generator=g).contiguous(memory_format=torch.channels_last)
+        tr2.train_step(x, torch.randint(0, 10, (128,), device=cuda, generator=g))
+    torch.cuda.synchronize()
+    assert tr2.graphed.validation["ok"] and not tr2.graphed.failed, tr2.graphed.validation
