@@ -29,13 +29,30 @@ SHIPPED_GEMM_DB = REPO / "gemm_db" / "tunableop_results.csv"
 # pins the replay-safe ASM solver for the default fp32 ResNet-18 shapes, and engine/graph.py
 # validates the first replay and falls back to eager.  MIOpen reads these switches once, at the
 # first convolution of the process: graph_safe_miopen() must run before any MIOpen call.
-GRAPH_UNSAFE_MIOPEN_SOLVERS = ("MIOPEN_DEBUG_GROUP_CONV_IMPLICIT_GEMM_HIP_WRW_XDLOPS",)
+#
+# The second switch is about determinism, not replay safety (round 5, profiles/replay_noise_r5.md):
+# the ASM implicit-GEMM forward solver for NHWC (ConvAsmImplicitGemmGTCDynamicFwdXdlopsNHWC, find's
+# choice for 7 of the 12 fp32 ResNet-18 convolutions) reduces over K with atomics, so two forwards
+# of the same input differ by ~1e-6.  That flips the ReLU mask of activations within 1e-6 of zero,
+# which moves a BatchNorm parameter's gradient by O(1/batch): eager-vs-eager (and replay-vs-eager)
+# differed by 3e-3 of the whole gradient on some steps (the round-4 driver failure of
+# tests/test_graph_replay_gpu.py).  Without it find picks the CK grouped forward solver (replay-
+# safe, deterministic: bench/determinism_probe.py, logits bitwise equal run to run), and the
+# remaining noise is the rounding of the backward solvers' atomics (~7e-7, no discrete step after
+# it).  Excluding the ASM backward-weights solver as well would leave only the naive one.
+GRAPH_MIOPEN_EXCLUDE = {
+    "MIOPEN_DEBUG_GROUP_CONV_IMPLICIT_GEMM_HIP_WRW_XDLOPS": "CK grouped backward-weights: wrong under replay",
+    "MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_FWD_GTC_XDLOPS_NHWC": "ASM NHWC forward: non-deterministic (atomics)",
+}
+GRAPH_UNSAFE_MIOPEN_SOLVERS = tuple(GRAPH_MIOPEN_EXCLUDE)
 
 
 def graph_safe_miopen() -> bool:
-    """Exclude the graph-unsafe MIOpen solvers (unless the user set the switches explicitly).
-    True when all of them are excluded.  Processes that may capture a hipGraph call this before
-    their first convolution; eager-only processes keep the full solver set."""
+    """Exclude the graph-unsafe and the non-deterministic-forward MIOpen solvers
+    (``GRAPH_MIOPEN_EXCLUDE``; unless the user set the switches explicitly).  True when all of
+    them are excluded.  Processes that may capture a hipGraph call this before their first
+    convolution (its first replay is validated against eager steps, which needs a reproducible
+    step); eager-only processes keep the full solver set."""
     for k in GRAPH_UNSAFE_MIOPEN_SOLVERS:
         os.environ.setdefault(k, "0")
     return all(os.environ.get(k) == "0" for k in GRAPH_UNSAFE_MIOPEN_SOLVERS)

@@ -131,3 +131,13 @@ def test_replay_check_nan_fails():
     bad[3] = float("nan")
     g = {"eager1": base, "eager2": base.clone(), "replay1": bad, "replay2": bad.clone()}
     assert not check_replay(g, views, names, fp32=True)["ok"]
+
+
+def test_replay_check_rejects_irreproducible_eager_steps():
+    """A forward that reads host state (a Python counter) makes even two eager steps from one
+    saved state differ: the inflated noise must not excuse the replay."""
+    from distributed_pytorch_training_amd.engine.graph import check_replay
+    base, views, names = _grads()
+    g = {"eager1": base, "eager2": base * 1.5, "replay1": base * 1.2, "replay2": base * 1.2}
+    v = check_replay(g, views, names, fp32=True)
+    assert not v["ok"] and not v["eager_reproducible"], v

@@ -24,16 +24,15 @@ def test_graph_unsafe_miopen_solvers_excluded_in_session():
     assert all(os.environ.get(k) == "0" for k in GRAPH_UNSAFE_MIOPEN_SOLVERS)
 
 
-def _per_param_worst(tr, a, b):
-    floor = 1e-6 * b.double().norm().item()
-    w = (0.0, "")
-    for n, u, v in zip(tr.ddp.arena.names, tr.ddp.arena.views(a), tr.ddp.arena.views(b)):
-        r = (u - v).double().norm().item() / max(v.double().norm().item(), floor, 1e-30)
-        w = max(w, (r, n))
-    return w
-
-
 def test_fp32_resnet18_replay_matches_eager_per_parameter(cuda):
+    """Teacher-forced: from one saved state, two replays and two eager steps.  Replay must agree
+    with eager as closely as eager agrees with itself: replay-vs-eager <= max(2 x eager-vs-eager,
+    1e-5) over the whole gradient, and every parameter within check_replay's noise-relative
+    tolerance.  Measured noise floor (bench/replay_noise.py, profiles/replay_noise_r5.md): with
+    the non-deterministic ASM forward solver excluded (utils/env.py) eager-vs-eager is ~7e-7 (the
+    backward solvers' atomics) and the forward is bitwise reproducible; with it, eager-vs-eager
+    reached 3e-3 on some steps (ReLU-mask flips) - the round-4 driver failure at 2.72e-3."""
+    from distributed_pytorch_training_amd.engine.graph import check_replay
     torch.backends.cudnn.benchmark = True
     torch.manual_seed(0)
     model = build_model("resnet18", 10, cuda, image_size=32, channels_last=True)
@@ -46,27 +45,32 @@ def test_fp32_resnet18_replay_matches_eager_per_parameter(cuda):
         x = torch.randn(128, 3, 32, 32, device=cuda, generator=g) * 4
         return x.contiguous(memory_format=torch.channels_last), torch.randint(0, 10, (128,), device=cuda, generator=g)
 
+    def eager(x, y):
+        with G._on_stream():
+            tr._native_step(x, y)
+        tr.global_step -= 1
+
     for _ in range(G.warmup + 1):       # warmup, capture, validated first replay
         tr.train_step(*batch())
     torch.cuda.synchronize()
     assert G.graph is not None and not G.failed, (G.failed, G.validation)
     assert G.validation["ok"], G.validation
-    # teacher-forced: three more steps, each replayed and run eagerly from the same state
-    for _ in range(3):
+    rel = lambda a, b: ((a - b).double().norm() / b.double().norm()).item()
+    for _ in range(6):
         x, y = batch()
         s0 = snapshot(tr)
-        tr.train_step(x, y)
-        torch.cuda.synchronize()
-        gr = tr.ddp.arena.grad_flat.clone()
-        restore(tr, s0)
-        with G._on_stream():
-            tr._native_step(x, y)
-        torch.cuda.synchronize()
-        ge = tr.ddp.arena.grad_flat
-        whole = ((gr - ge).double().norm() / ge.double().norm()).item()
-        worst = _per_param_worst(tr, gr, ge)
-        # fp32 rounding-level agreement overall; a single near-cancelling BN sum may move more
-        assert whole < 1e-3 and worst[0] < 0.1, (whole, worst)
+        gr = {}
+        for name, fn in (("replay1", lambda: tr.train_step(x, y)), ("replay2", lambda: tr.train_step(x, y)),
+                         ("eager1", lambda: eager(x, y)), ("eager2", lambda: eager(x, y))):
+            restore(tr, s0)
+            fn()
+            torch.cuda.synchronize()
+            gr[name] = tr.ddp.arena.grad_flat.clone()
+        ee, rr, re_ = rel(gr["eager2"], gr["eager1"]), rel(gr["replay2"], gr["replay1"]), rel(gr["replay1"], gr["eager1"])
+        bound = max(2 * ee, 1e-5)
+        assert re_ <= bound and rr <= bound, (re_, rr, ee)
+        v = check_replay(gr, tr.ddp.arena.views, tr.ddp.arena.names, fp32=True)
+        assert v["ok"], v
 
 
 class _HostScale(torch.nn.Module):
