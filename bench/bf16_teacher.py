@@ -48,8 +48,31 @@ def grouped(named: dict) -> dict:
     return {g: torch.cat(v) for g, v in out.items()}
 
 
+def pretrain(model, steps: int, batch: int, image_size: int, lr: float, dev, log=print):
+    """fp32 SGD on the learnable prototypes task (data/loader.py): at random init a ResNet-50's
+    gradient is chaotic - ReLU-mask flips from ANY rounding difference cascade through 50 BN
+    layers, so bf16 and fp32 gradients are nearly orthogonal in both engines (rel-L2 1.2-1.3,
+    profiles/bf16_teacher_r5.md) and the comparison has no power.  A briefly trained network is
+    out of that regime."""
+    from distributed_pytorch_training_amd.data import SyntheticLoader
+    if steps <= 0:
+        return
+    loader = SyntheticLoader(batch * steps, batch, image_size, 10, dev, channels_last=True, seed=7,
+                             task="prototypes", noise=2.0)
+    opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-4)
+    model.train()
+    for i, (x, y) in enumerate(loader):
+        opt.zero_grad(set_to_none=True)
+        loss = F.cross_entropy(model(x), y)
+        loss.backward()
+        opt.step()
+        if (i + 1) % 50 == 0:
+            log(json.dumps({"pretrain_step": i + 1, "loss": round(float(loss), 4)}))
+
+
 def run(steps: int = 5, batch: int = 64, image_size: int = 112, seed: int = 0, lr: float = 0.1,
-        wd: float = 5e-4, log=print) -> dict:
+        wd: float = 5e-4, log=print, pretrain_steps: int = 0, pretrain_lr: float = 0.05,
+        task: str = "random") -> dict:
     from distributed_pytorch_training_amd.config import parse_args
     from distributed_pytorch_training_amd.engine.graph import step_state
     from distributed_pytorch_training_amd.engine.trainer import Trainer
@@ -67,12 +90,22 @@ def run(steps: int = 5, batch: int = 64, image_size: int = 112, seed: int = 0, l
                        "--weight-decay", str(wd)])
     tr = Trainer(nat_model, args, 0, 1, dev, log=lambda s: None)
     pnames = [n for n, _ in ref.named_parameters()]
+    pretrain(ref, pretrain_steps, batch, image_size, pretrain_lr, dev, log)
     g = torch.Generator(device=dev).manual_seed(1000 + seed)
+    protos = None
+    if task == "prototypes":
+        from distributed_pytorch_training_amd.data.loader import class_prototypes
+        protos = class_prototypes(10, image_size, dev)
     rows = []
     for k in range(steps):
         state = {n: t.detach().clone() for n, t in ref.state_dict().items()}
-        x = torch.randn(batch, 3, image_size, image_size, device=dev, generator=g).contiguous(memory_format=cl)
-        y = torch.randint(0, 1000, (batch,), device=dev, generator=g)
+        if protos is None:
+            x = torch.randn(batch, 3, image_size, image_size, device=dev, generator=g).contiguous(memory_format=cl)
+            y = torch.randint(0, 1000, (batch,), device=dev, generator=g)
+        else:
+            y = torch.randint(0, 10, (batch,), device=dev, generator=g)
+            x = (protos.index_select(0, y) + 2.0 * torch.randn(batch, 3, image_size, image_size, device=dev,
+                                                             generator=g)).contiguous(memory_format=cl)
 
         # fp32 reference and stock bf16 autocast: plain autograd gradients
         grads = {}
@@ -112,12 +145,15 @@ def run(steps: int = 5, batch: int = 64, image_size: int = 112, seed: int = 0, l
             upd[name] = {n: -lr * (grads[name][n] + wd * state[n].float()) for n in pnames}
         upd["native"] = upd_native
 
-        row = {"step": k, "scale": scale, "found_inf": found_inf, "grad": {}, "update": {}}
+        row = {"step": k, "scale": scale, "found_inf": found_inf, "grad": {}, "update": {}, "cos": {}}
         gref = grouped(grads["ref"])
         for eng in ("stock", "native"):
             ge = grouped(grads[eng])
             row["grad"][eng] = {gname: rel(ge[gname], gref[gname]) for gname in gref}
             row["grad"][eng]["all"] = rel(torch.cat([ge[n] for n in gref]), torch.cat([gref[n] for n in gref]))
+            fa = torch.cat([ge[n] for n in gref])
+            fr = torch.cat([gref[n] for n in gref])
+            row["cos"][eng] = float((fa @ fr) / (fa.norm() * fr.norm()).clamp_min(1e-30))
             row["update"][eng] = rel(torch.cat([upd[eng][n].reshape(-1).double() for n in pnames]),
                                      torch.cat([upd["ref"][n].reshape(-1).double() for n in pnames]))
         rows.append(row)
@@ -138,7 +174,8 @@ def summarize(rows) -> dict:
     for gname in table:
         table[gname]["ratio"] = table[gname]["native"] / max(table[gname]["stock"], 1e-30)
     upd = {eng: sum(r["update"][eng] for r in rows) / len(rows) for eng in ("stock", "native")}
-    return {"steps": len(rows), "groups": table, "update": upd, "rows": rows}
+    cos = {eng: sum(r["cos"][eng] for r in rows) / len(rows) for eng in ("stock", "native")}
+    return {"steps": len(rows), "groups": table, "update": upd, "cos": cos, "rows": rows}
 
 
 def markdown(res: dict) -> str:
@@ -148,6 +185,9 @@ def markdown(res: dict) -> str:
         lines.append(f"| {gname} | {v['stock']:.4g} | {v['native']:.4g} | {v['ratio']:.3f} |")
     u = res["update"]
     lines.append(f"| **SGD update** | {u['stock']:.4g} | {u['native']:.4g} | {u['native'] / max(u['stock'], 1e-30):.3f} |")
+    c = res.get("cos")
+    if c:
+        lines.append(f"| gradient cosine vs fp32 | {c['stock']:.4f} | {c['native']:.4f} | |")
     return "\n".join(lines)
 
 
@@ -157,12 +197,14 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--image-size", type=int, default=112)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--pretrain-steps", type=int, default=0)
+    ap.add_argument("--task", default="random", choices=["random", "prototypes"])
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args()
     from distributed_pytorch_training_amd.utils.env import setup_miopen_env
     setup_miopen_env()
     torch.cuda.set_device(0)
-    res = run(a.steps, a.batch, a.image_size, a.seed)
+    res = run(a.steps, a.batch, a.image_size, a.seed, pretrain_steps=a.pretrain_steps, task=a.task)
     print(markdown(res))
     if a.json_out:
         with open(a.json_out, "w") as f:
