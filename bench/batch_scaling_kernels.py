@@ -11,14 +11,16 @@ images/s).
 from __future__ import annotations
 
 import argparse
-import csv
 import re
+import sys
 from collections import defaultdict
+
+sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.abspath(__file__)))
+from rocprof_rows import load_rows  # noqa: E402
 
 
 def per_step(path: str, steps: int):
-    with open(path) as f:
-        rows = sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"]))
+    rows = load_rows(path)
     opt = [i for i, r in enumerate(rows) if re.search(r"dpt::(sgd|adam)\w*_kernel", r["Kernel_Name"])]
     if len(opt) >= steps + 1:
         rows = rows[opt[-steps - 1] + 1: opt[-1] + 1]

@@ -19,11 +19,13 @@ the most frequent kernel when not given.
 from __future__ import annotations
 
 import argparse
-import csv
 import math
 import re
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.abspath(__file__)))
+from rocprof_rows import load_rows  # noqa: E402
 
 CUS = 256
 LDS_PER_CU = 160 * 1024
@@ -57,9 +59,7 @@ def main(argv=None):
     ap.add_argument("--filter", default="dpt::")
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args(argv)
-    with open(a.trace) as f:
-        rows = list(csv.DictReader(f))
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    rows = load_rows(a.trace)
     # the timed window: the last `steps` optimizer steps (one sgd/adam kernel per step)
     opt = [i for i, r in enumerate(rows) if re.search(r"dpt::(sgd|adam)\w*_kernel", r["Kernel_Name"])]
     if len(opt) >= a.steps + 1:

@@ -581,6 +581,74 @@ void conv_reduce_flush(PendingReducePtr p) {
 }
 
 // a = im2col(x) as a channels_last [N, Kp, Ho, Wo] bf16 tensor (x: channels_last fp32/bf16)
+// ---- fp32 convolutions (conv_f32_kernels.hip) ---------------------------------------------
+void check_cl_f32(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.dim() == 4, name, ": expected a 4-D CUDA fp32 tensor");
+  TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name, ": expected channels_last memory");
+}
+
+Tensor conv_f32_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad) {
+  check_cl_f32(x, "x");
+  check_cl_f32(w, "w");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int Co = w.size(0), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(w.size(1) == C, "conv_f32_fwd: channel mismatch");
+  TORCH_CHECK(C % 4 == 0 && Co % 4 == 0, "conv_f32_fwd: channels must be multiples of 4");
+  TORCH_CHECK(stride >= 1 && pad >= 0, "conv_f32_fwd: bad stride/pad");
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "conv_f32_fwd: empty output");
+  auto y = at::empty({N, Co, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t wsn = dpt::conv_f32_workspace((int64_t)N * Ho * Wo, Co, R * S * C);
+  Tensor ws = wsn > 0 ? at::empty({wsn}, x.options()) : Tensor();
+  dpt::launch_conv_f32(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(),
+                       ws.defined() ? ws.data_ptr<float>() : nullptr, false, N, H, W, C, Ho, Wo, Co, R, S,
+                       (int)stride, (int)pad, cur_stream(x));
+  return y;
+}
+
+// dx of a conv with input H x W: the transposed-conv gather of dy against the weight
+// transposed to [C][R][S][Co] (a copy of the small weight tensor).
+Tensor conv_f32_dgrad(Tensor dy, Tensor w, int64_t stride, int64_t pad, int64_t H, int64_t W) {
+  check_cl_f32(dy, "grad_output");
+  check_cl_f32(w, "w");
+  const int N = dy.size(0), Co = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  const int C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(w.size(0) == Co, "conv_f32_dgrad: channel mismatch");
+  TORCH_CHECK(C % 4 == 0 && Co % 4 == 0, "conv_f32_dgrad: channels must be multiples of 4");
+  TORCH_CHECK((H + 2 * pad - R) / stride + 1 == Ho && (W + 2 * pad - S) / stride + 1 == Wo,
+              "conv_f32_dgrad: input size does not match grad_output");
+  Tensor wt = w.permute({1, 2, 3, 0}).contiguous();  // logical [C, R, S, Co] from memory [Co][R][S][C]
+  auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(dy.device().index());
+  const int64_t wsn = dpt::conv_f32_workspace((int64_t)N * H * W, C, R * S * Co);
+  Tensor ws = wsn > 0 ? at::empty({wsn}, dy.options()) : Tensor();
+  dpt::launch_conv_f32(dy.data_ptr<float>(), wt.data_ptr<float>(), dx.data_ptr<float>(),
+                       ws.defined() ? ws.data_ptr<float>() : nullptr, true, N, (int)H, (int)W, C, Ho, Wo, Co, R, S,
+                       (int)stride, (int)pad, cur_stream(dy));
+  return dx;
+}
+
+Tensor conv_f32_wgrad(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stride, int64_t pad) {
+  check_cl_f32(dy, "grad_output");
+  check_cl_f32(x, "x");
+  TORCH_CHECK(wshape.size() == 4, "conv_f32_wgrad: weight shape must be [Co, C, R, S]");
+  const int Co = wshape[0], C = wshape[1], R = wshape[2], S = wshape[3];
+  const int N = x.size(0), H = x.size(2), W = x.size(3), Ho = dy.size(2), Wo = dy.size(3);
+  TORCH_CHECK(x.size(1) == C && dy.size(1) == Co && dy.size(0) == N, "conv_f32_wgrad: shape mismatch");
+  TORCH_CHECK(C % 4 == 0 && Co % 4 == 0, "conv_f32_wgrad: channels must be multiples of 4");
+  TORCH_CHECK((H + 2 * pad - R) / stride + 1 == Ho && (W + 2 * pad - S) / stride + 1 == Wo,
+              "conv_f32_wgrad: input size does not match grad_output");
+  auto dw = at::empty({Co, C, R, S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t wsn = dpt::conv_f32_wgrad_workspace(N, Ho, Wo, Co, R * S * C);
+  Tensor ws = wsn > 0 ? at::empty({wsn}, x.options()) : Tensor();
+  dpt::launch_conv_f32_wgrad(dy.data_ptr<float>(), x.data_ptr<float>(), dw.data_ptr<float>(),
+                             ws.defined() ? ws.data_ptr<float>() : nullptr, N, H, W, C, Ho, Wo, Co, R, S,
+                             (int)stride, (int)pad, cur_stream(x));
+  return dw;
+}
+
 Tensor im2col(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Kp) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
               "im2col: x must be a 4-d fp32/bf16 GPU tensor");
@@ -1154,6 +1222,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("space_to_depth2", &space_to_depth2, py::arg("x"), py::arg("out_f16") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("grad_output"), py::arg("x"), py::arg("weight_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("fp32_out"));
+  m.def("conv_f32_fwd", &conv_f32_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"));
+  m.def("conv_f32_dgrad", &conv_f32_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("stride"), py::arg("pad"),
+        py::arg("H"), py::arg("W"));
+  m.def("conv_f32_wgrad", &conv_f32_wgrad, py::arg("grad_output"), py::arg("x"), py::arg("weight_shape"),
+        py::arg("stride"), py::arg("pad"));
   m.def("im2col", &im2col, py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("Kp"));
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("heads"), py::arg("scale"));
   m.def("attn_set_bwd_split", &dpt::attn_set_bwd_split, py::arg("on"));

@@ -272,4 +272,15 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* ctx, float* lse2, int B, int
                      hipStream_t s);
 void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse2,
                      uint16_t* dqkv, int B, int S, int H, float scale, hipStream_t s);
+
+// conv_f32_kernels.hip: channels_last fp32 convolutions on v_mfma_f32_32x32x2_f32 (exact fp32,
+// deterministic split-K).  dgrad = true: a is dy [N,Ho,Wo,Co], b the transposed weight
+// [C][R][S][Co], out dx [N,H,W,C]; otherwise a is x, b the weight [Co][R][S][C], out y.
+// ws: conv_f32_workspace(...) floats when that is > 0 (split-K partial tiles).
+int64_t conv_f32_workspace(int64_t M, int ncols, int K, int* splits = nullptr);
+void launch_conv_f32(const float* a, const float* b, float* out, float* ws, bool dgrad, int N, int H, int W, int C,
+                     int Ho, int Wo, int Co, int R, int S, int stride, int pad, hipStream_t st);
+int64_t conv_f32_wgrad_workspace(int N, int Ho, int Wo, int Co, int J);
+void launch_conv_f32_wgrad(const float* dy, const float* x, float* dw, float* ws, int N, int H, int W, int C,
+                           int Ho, int Wo, int Co, int R, int S, int stride, int pad, hipStream_t st);
 }  // namespace dpt

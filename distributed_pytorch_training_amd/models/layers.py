@@ -18,6 +18,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import bn as fused_bn
+from ..ops.conv_f32 import NativeConv2d
 from ..ops import pool as fused_pool
 
 
@@ -173,8 +174,11 @@ class GemmConv1x1(nn.Conv2d):
 
 
 def set_conv_routing(model: nn.Module, native_conv: bool = True, min_pixels=None) -> None:
-    """Per-model conv routing: MFMA kernels (ops/conv.py) or MIOpen, stored on each conv."""
+    """Per-model conv routing: MFMA kernels (ops/conv.py, ops/conv_f32.py) or MIOpen, stored on
+    each conv; plain ``nn.Conv2d`` modules become ``NativeConv2d`` (same parameters)."""
     for m in model.modules():
+        if type(m) is nn.Conv2d:
+            m.__class__ = NativeConv2d
         if isinstance(m, nn.Conv2d):
             m.dpt_native_conv = bool(native_conv)
             m.dpt_min_pixels = min_pixels

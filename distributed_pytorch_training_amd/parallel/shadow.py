@@ -22,6 +22,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.conv_f32 import NativeConv2d
 from ..ops import conv as native_conv
 
 SHADOW_ATTR = "_dpt_shadow"
@@ -36,7 +37,7 @@ def active_shadow(mod: nn.Module, x: torch.Tensor):
     return sh
 
 
-class ShadowConv2d(nn.Conv2d):
+class ShadowConv2d(NativeConv2d):
     # set by fuse_native_layers on convs that feed a fused BatchNorm: the native conv's
     # epilogue then also emits the BN statistics partials
     dpt_bn_stats = False
@@ -47,10 +48,10 @@ class ShadowConv2d(nn.Conv2d):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         sh = active_shadow(self, x)
         if sh is None:
-            return super().forward(x)
+            return super().forward(x)          # NativeConv2d: the fp32 MFMA path, or nn.Conv2d
         w, b = sh["weight"], sh.get("bias", self.bias)
         if not self.dpt_native_conv:
-            return self._conv_forward(x, w, b)
+            return nn.Conv2d._conv_forward(self, x, w, b)
         if b is None and native_conv.supported(x, w, self.stride, self.padding, self.dilation, self.groups,
                                                self.dpt_min_pixels):
             return native_conv.conv2d(x, w, self.stride[0], self.padding[0], self.dpt_bn_stats)
@@ -78,7 +79,7 @@ def shadow_param(mod: nn.Module, name: str, x: torch.Tensor) -> torch.Tensor:
     return getattr(mod, name)
 
 
-_SWAP = {nn.Conv2d: ShadowConv2d, nn.Linear: ShadowLinear}
+_SWAP = {nn.Conv2d: ShadowConv2d, NativeConv2d: ShadowConv2d, nn.Linear: ShadowLinear}
 
 
 def install_shadows(module: nn.Module, arena, dtype: torch.dtype) -> Tuple[torch.Tensor, Dict[int, torch.Tensor]]:
