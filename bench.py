@@ -74,6 +74,8 @@ def parse(argv=None):
                          "for this config) and skips the search")
     ap.add_argument("--cuda-graph", action="store_true", help="replay the captured step as a hipGraph")
     ap.add_argument("--no-native-conv", action="store_true", help="A/B: MIOpen convolutions")
+    ap.add_argument("--native-conv-fp32", action="store_true",
+                    help="with --no-amp: the fp32 MFMA conv kernels instead of MIOpen's fp32 solvers")
     ap.add_argument("--no-weight-shadow", action="store_true",
                     help="A/B: autocast casts fp32 weights every forward (no optimizer-kept bf16 copy)")
     ap.add_argument("--profile-steps", type=int, default=8,
@@ -386,6 +388,8 @@ def train_args(a):
         argv.append("--no-weight-shadow")
     if a.no_native_conv:
         argv.append("--no-native-conv")
+    if a.native_conv_fp32:
+        argv.append("--native-conv-fp32")
     return parse_args(argv)
 
 

@@ -122,9 +122,44 @@ __global__ __launch_bounds__(cf32::kThreads, 2) void conv_f32_mk_kernel(ConvF32A
   const int ks0 = sp * p.kps;
   const int ks1 = min(nk, ks0 + p.kps);
 
+  // ca % 32 == 0 (every ResNet conv but the stem): a K-step is 32 channels of ONE tap, so the
+  // tap and channel block are wave-uniform (scalar) and a row's source offset is its base plus
+  // a per-step constant; only the bounds (and, strided dgrad, the parity) are per row.
+  const bool wide = p.ca % BK == 0;
+  const int cpk = p.ca / BK;
   auto stage = [&](int ks) {
     unsigned char* a = lds;
     unsigned char* b = lds + BM * kRowBytes;
+    if (wide) {
+      const int tap = ks / cpk, cb = ks - tap * cpk;
+      const int r = tap / p.S, s = tap - r * p.S;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        uint32_t off = kOOB;
+        if (rn[i] >= 0) {
+          int ys, xs;
+          bool ok;
+          if (DGRAD) {
+            const int t = ry[i] + p.pad - r, u = rx[i] + p.pad - s;
+            if (p.stride == 1) {
+              ys = t; xs = u; ok = true;
+            } else {
+              ok = t >= 0 && u >= 0 &&
+                   (p.stride == 2 ? ((t | u) & 1) == 0 : (t % p.stride) == 0 && (u % p.stride) == 0);
+              ys = p.stride == 2 ? t >> 1 : t / p.stride;
+              xs = p.stride == 2 ? u >> 1 : u / p.stride;
+            }
+          } else {
+            ys = ry[i] * p.stride - p.pad + r;
+            xs = rx[i] * p.stride - p.pad + s;
+            ok = true;
+          }
+          ok = ok && (unsigned)ys < (unsigned)Hs && (unsigned)xs < (unsigned)Ws;
+          if (ok) off = (uint32_t)((((int64_t)rn[i] * Hs + ys) * Ws + xs) * p.ca + cb * BK + achunk[i] * 4) * 4u;
+        }
+        cf32::glds16(ra, a + (wid * 4 + i) * 1024, off);
+      }
+    } else
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int k = ks * BK + achunk[i] * 4;  // 4 channels of one tap (ca % 4 == 0)

@@ -95,6 +95,10 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--no-native-conv", dest="native_conv", action="store_false",
                    help="native impl: run convolutions on MIOpen instead of the hand-written MFMA "
                         "implicit-GEMM kernels (which also fuse the BatchNorm statistics pass)")
+    g.add_argument("--native-conv-fp32", action="store_true",
+                   help="native impl, fp32 (no --amp): run the convolutions on the hand-written fp32 MFMA "
+                        "kernels (exact, bitwise deterministic, replay-safe) instead of MIOpen (faster on "
+                        "ResNet-50: profiles/conv_f32_r5.md)")
     g.add_argument("--no-weight-shadow", dest="weight_shadow", action="store_false",
                    help="native impl: let autocast cast fp32 weights every forward instead of keeping "
                         "16-bit weight shadows updated by the fused optimizer")

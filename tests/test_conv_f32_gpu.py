@@ -9,6 +9,12 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _enable_f32(monkeypatch):
+    from distributed_pytorch_training_amd.ops import conv_f32
+    monkeypatch.setattr(conv_f32, "ENABLED", True)
+
 CL = torch.channels_last
 
 # (N, C, H, W, Co, k, stride, pad)
