@@ -395,11 +395,13 @@ __global__ __launch_bounds__(kBlock) void conv_f32_reduce_kernel(const float4* _
 
 namespace {
 
-// split-K so that a small tile grid still fills the chip: ~4 blocks per CU, >= 4 K-steps each
+// split-K so that a small tile grid still fills the chip (>= 16 K-steps per split, at most
+// `target` blocks): every extra split costs a partial tile written and read back by the reduce
+// (measured on ResNet-50: a 1024-block target moved ~28 GB/step through conv_f32_reduce_kernel)
 void choose_splits(int tiles, int64_t nk, int target, int* splits, int* kps) {
   int sp = 1;
-  if (tiles < target && nk >= 8) {
-    sp = (int)std::min<int64_t>(nk / 4, (target + tiles - 1) / tiles);
+  if (tiles < target && nk >= 32) {
+    sp = (int)std::min<int64_t>(nk / 16, (target + tiles - 1) / tiles);
     sp = std::max(sp, 1);
   }
   int64_t k = (nk + sp - 1) / sp;
@@ -417,7 +419,7 @@ void check_bytes(int64_t bytes, const char* what) {
 int64_t conv_f32_workspace(int64_t M, int ncols, int K, int* splits_out) {
   const int tiles = (int)((M + cf32::BM - 1) / cf32::BM) * ((ncols + cf32::BN - 1) / cf32::BN);
   int sp, kps;
-  choose_splits(tiles, (K + cf32::BK - 1) / cf32::BK, 1024, &sp, &kps);
+  choose_splits(tiles, (K + cf32::BK - 1) / cf32::BK, 512, &sp, &kps);
   if (splits_out) *splits_out = sp;
   return sp > 1 ? (int64_t)sp * M * ncols : 0;
 }
@@ -442,7 +444,7 @@ void launch_conv_f32(const float* a, const float* b, float* out, float* ws, bool
   p.b_bytes = (uint32_t)b_bytes;
   p.m_tiles = (int)((p.M + cf32::BM - 1) / cf32::BM);
   p.n_tiles = (p.ncols + cf32::BN - 1) / cf32::BN;
-  choose_splits(p.m_tiles * p.n_tiles, (p.K + cf32::BK - 1) / cf32::BK, 1024, &p.splits, &p.kps);
+  choose_splits(p.m_tiles * p.n_tiles, (p.K + cf32::BK - 1) / cf32::BK, 512, &p.splits, &p.kps);
   if (p.splits > 1 && ws == nullptr) throw std::invalid_argument("conv_f32: split-K needs a workspace");
   p.out = p.splits > 1 ? ws : out;
   const dim3 grid(p.m_tiles * p.n_tiles * p.splits);
@@ -458,7 +460,7 @@ void launch_conv_f32(const float* a, const float* b, float* out, float* ws, bool
 int64_t conv_f32_wgrad_workspace(int N, int Ho, int Wo, int Co, int J) {
   const int tiles = ((Co + cf32::BM - 1) / cf32::BM) * ((J + cf32::BN - 1) / cf32::BN);
   int sp, kps;
-  choose_splits(tiles, ((int64_t)N * Ho * Wo + cf32::BK - 1) / cf32::BK, 1024, &sp, &kps);
+  choose_splits(tiles, ((int64_t)N * Ho * Wo + cf32::BK - 1) / cf32::BK, 512, &sp, &kps);
   return sp > 1 ? (int64_t)sp * Co * J : 0;
 }
 
@@ -479,7 +481,7 @@ void launch_conv_f32_wgrad(const float* dy, const float* x, float* dw, float* ws
   p.x_bytes = (uint32_t)x_bytes;
   p.m_tiles = (Co + cf32::BM - 1) / cf32::BM;
   p.n_tiles = (p.J + cf32::BN - 1) / cf32::BN;
-  choose_splits(p.m_tiles * p.n_tiles, (p.Q + cf32::BK - 1) / cf32::BK, 1024, &p.splits, &p.kps);
+  choose_splits(p.m_tiles * p.n_tiles, (p.Q + cf32::BK - 1) / cf32::BK, 512, &p.splits, &p.kps);
   if (p.splits > 1 && ws == nullptr) throw std::invalid_argument("conv_f32_wgrad: split-K needs a workspace");
   p.out = p.splits > 1 ? ws : dw;
   const dim3 grid(p.m_tiles * p.n_tiles * p.splits);
