@@ -5,7 +5,7 @@ From the same fp32 master weights, BatchNorm buffers and batch (ResNet-50, 112 p
 gradient is chaotic - bf16 and fp32 gradients are nearly orthogonal in BOTH engines, rel-L2 1.2-1.3,
 and nothing can be compared), one fp32 torch step is the reference; the native bf16 step's gradient (per
 parameter group: stage x {conv, bn, fc}) and its SGD update must be no further from it than
-1.25x what stock PyTorch's bf16 autocast step is, averaged over 8 teacher-forced steps
+1.25x what stock PyTorch's bf16 autocast step is, averaged over 16 teacher-forced steps
 (bench/bf16_teacher.py; committed numbers in profiles/bf16_teacher_r5.md).  This is the check
 with statistical power that free-running seed sweeps cannot give: an engine-level error of a few
 percent in one layer's gradient shows up here as a ratio far above 1.
@@ -28,10 +28,10 @@ ABS = 2e-3
 def test_native_bf16_step_is_as_close_to_fp32_as_stock_bf16(cuda):
     import bf16_teacher
 
-    res = bf16_teacher.run(steps=8, batch=64, image_size=112, seed=0, log=lambda s: None, pretrain_steps=200,
+    res = bf16_teacher.run(steps=16, batch=64, image_size=112, seed=0, log=lambda s: None, pretrain_steps=200,
                            task="prototypes")
     print(bf16_teacher.markdown(res))
-    assert res["steps"] == 8
+    assert res["steps"] == 16
     assert all(r["found_inf"] == 0.0 for r in res["rows"]), [r["found_inf"] for r in res["rows"]]
     bad = {g: v for g, v in res["groups"].items() if v["native"] > RATIO * v["stock"] + ABS}
     assert not bad, bad
