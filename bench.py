@@ -76,6 +76,9 @@ def parse(argv=None):
     ap.add_argument("--no-native-conv", action="store_true", help="A/B: MIOpen convolutions")
     ap.add_argument("--native-conv-fp32", action="store_true",
                     help="with --no-amp: the fp32 MFMA conv kernels instead of MIOpen's fp32 solvers")
+    ap.add_argument("--conv-streamk", choices=("off", "auto", "all"), default=None,
+                    help="stream-K grids for unevenly spread MFMA conv tile grids (default: the "
+                         "framework's, env DPT_CONV_STREAMK)")
     ap.add_argument("--no-weight-shadow", action="store_true",
                     help="A/B: autocast casts fp32 weights every forward (no optimizer-kept bf16 copy)")
     ap.add_argument("--profile-steps", type=int, default=8,
@@ -390,6 +393,8 @@ def train_args(a):
         argv.append("--no-native-conv")
     if a.native_conv_fp32:
         argv.append("--native-conv-fp32")
+    if a.conv_streamk:
+        argv += ["--conv-streamk", a.conv_streamk]
     return parse_args(argv)
 
 

@@ -1239,6 +1239,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eager_min_k"), py::arg("target"), "split-K thresholds (A/B knob; <= 0 keeps a value)");
   m.def("conv_set_big", &dpt::conv_set_big, py::arg("on"));
   m.def("conv_set_halo", &dpt::conv_set_halo, py::arg("on"));
+  m.def("conv_set_streamk", &dpt::conv_set_streamk, py::arg("mode"), py::arg("eff") = 0.0);
+  m.def("conv_get_streamk", &dpt::conv_get_streamk);
+  m.def("conv_sk_prepare", &dpt::conv_sk_prepare);
+  m.def("conv_sk_errors", &dpt::conv_sk_errors);
+  m.def("conv_sk_blocks", &dpt::conv_sk_blocks, py::arg("tiles"), py::arg("nk"), py::arg("bn"), py::arg("mode"));
   m.def("conv_set_wgrad_target", &dpt::conv_set_wgrad_target, py::arg("blocks"));
   m.def("conv_set_wgrad_halo", &dpt::conv_set_wgrad_halo, py::arg("mode"));
   m.def("conv_fwd_splits", [](int64_t M, int Cout, int64_t K, bool graph) {

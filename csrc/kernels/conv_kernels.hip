@@ -26,7 +26,9 @@
 // Blocks are numbered so the BN-tiles of one M-tile (which share the same A rows) are
 // consecutive and land on the same XCD (bijective XCD remap, cdna_hip_programming.md T1).
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
+#include <mutex>
 #include <stdexcept>
 
 #include "carry.h"
@@ -55,6 +57,11 @@ __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >>
 
 // Bijective XCD remap: consecutive logical ids share an XCD (MI355X: 8 XCDs, dispatch is
 // round-robin over them by hardware block id).
+__device__ __forceinline__ int opaque_v(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
@@ -87,6 +94,18 @@ __device__ __forceinline__ float cunpack(uint32_t u, int h) {
   if constexpr (F16) return (float)__builtin_bit_cast(_Float16, (uint16_t)(h ? (u >> 16) : (u & 0xffffu)));
   else return __uint_as_float(h ? (u & 0xffff0000u) : (u << 16));
 }
+
+// Stream-K workspace (one per device and stream, conv_sk_workspace): a contributing segment's
+// fp32 partial tile [G][float4 slot][thread], a published flag per block (set with an agent-scope
+// store after the sc1 payload drained; reset by the consuming block, so every launch starts from
+// zeros - hipGraph replays included), and a give-up counter of the bounded spin.
+struct ConvSk {
+  float* part = nullptr;
+  unsigned* flags = nullptr;
+  unsigned* err = nullptr;
+  int G = 0;
+  uint32_t part_bytes = 0;
+};
 
 struct ConvFwdArgs {
   const uint16_t* x;  // [N, H, W, C]
@@ -134,6 +153,10 @@ struct ConvFwdArgs {
   // split-K partials of a backward-weight launched just before (the same conv's) instead of
   // computing a conv tile (AttachWgradReduce, kernels.h).  red.blocks = 0: none.
   ReduceCarry red;
+  // Stream-K (conv_fwd_kernel<..., SK = true>): the first sk.G blocks split the tiles' K-steps
+  // evenly; a tile shared by several blocks is finished by the block holding its last K-step
+  // (see conv_fwd_kernel).  sk.G = 0: off.
+  ConvSk sk;
 };
 
 
@@ -189,8 +212,8 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 // tile is bound by what one CU can pull from L2 into LDS (docs/DESIGN.md 7.1).
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
           bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, bool F16 = false,
-          int NT = conv::kThreads, bool SPLIT = false, bool HALO = false, int HB = 1>
-__global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
+          int NT = conv::kThreads, bool SPLIT = false, bool HALO = false, int HB = 1, bool SK = false>
+__global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
   constexpr int BM = BMT;
   constexpr int NW = NT / 64;         // waves
@@ -202,6 +225,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   constexpr int A_PER_T = BM * 8 / NT;  // glds instructions per wave per K-step (A)
   constexpr int B_PER_T = BN * 8 / NT;  // (B)
   static_assert(!HALO || (BMT == 128 && STAGES == 1 && !BKN && !SPLIT && NT == conv::kThreads), "HALO config");
+  static_assert(!SK || (STAGES == 1 && !HALO && !SPLIT && LDSEPI && !BNR2 && NT == conv::kThreads), "SK config");
   constexpr int HROWS = 136;  // halo strip rows: 128 + 2, rounded up to whole 8-row glds instructions
   // HB (HALO): B taps staged per load phase - 1: one per K-step; 3: all three taps of the row
   // with the halo strip, one wait per three K-steps (more LDS: fewer resident blocks)
@@ -237,12 +261,19 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int tiles = (BM == 256 ? p.mt256 : p.m_tiles) * p.n_tiles;
-  const int nsplit = SPLIT ? p.splits : 1;
-  const int bid0 = conv::xcd_remap(blockIdx.x, tiles * nsplit);
-  // split-K: the splits of one tile are consecutive ids (one XCD, shared A/B rows in its L2)
-  const int sp = SPLIT ? bid0 % nsplit : 0;
-  const int bid = SPLIT ? bid0 / nsplit : bid0;
-  const int mt = bid / p.n_tiles, nt = bid % p.n_tiles;
+  const int nk_all = (int)((int64_t)p.R * p.S * p.C / BK);
+
+  // One output tile's K-steps [ks0, ks1) and its epilogue.  sk_role (stream-K only): 0 the whole
+  // tile; 1 a leading part of it - publish the partial accumulators in slot sk_slot and stop; 2 its
+  // trailing part - first add the partials of blocks sk_c0, sk_c0 + 8, .., sk_c1 (lower ids, one XCD).
+  auto tile_body = [&](const int mt, const int nt, const int sp, const int ks0, const int ks1, const int sk_role,
+                       const int sk_slot, const int sk_c0, const int sk_c1) {
+  // stream-K runs this body in a loop: recompute the lane-dependent values per tile (an opaque
+  // copy of the thread id), or the compiler hoists every per-lane address out of the loop and
+  // keeps them live across the K loop (~100 more VGPRs: half the resident blocks)
+  const int tid = SK ? conv::opaque_v((int)threadIdx.x) : (int)threadIdx.x, lane = tid & 63;
+  const int wid = SK ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
   const int64_t m0 = (int64_t)mt * BM;
   const int n0 = nt * BN;
 
@@ -303,9 +334,6 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
 
   const int cblocks = p.C >= BK ? p.C / BK : 1;
   const int tps = p.C >= BK ? 1 : BK / p.C;  // taps per K-step (narrow inputs)
-  const int nk_all = (int)(Kg / BK);
-  const int ks0 = SPLIT ? sp * p.kps : 0;
-  const int ks1 = SPLIT ? min(nk_all, ks0 + p.kps) : nk_all;
 
   // global -> LDS directly (no staging registers); wave-uniform LDS base per 1 KiB.
   auto stage = [&](int ks, int buf) {
@@ -528,6 +556,74 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
         }
       }
     return;
+  }
+
+  if constexpr (SK) {
+    // float4 q of thread tid in slot b: ((b * ACC4 + q) * NT + tid) - coalesced per float4
+    constexpr int ACC4 = MI * NI * 4;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) unsigned gu32;
+    // one VGPR offset per thread and slot; the float4 index q rides in the SGPR offset
+    const __amdgpu_buffer_rsrc_t rp =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.sk.part, 0, (int)p.sk.part_bytes, 0x00020000);
+    if (sk_role == 2) {
+      // consume: wave 0 polls each contributor's flag (relaxed, with sleeps, bounded), resets it for
+      // the next launch, ONE agent-scope acquire, then every wave reads the partials
+      if (wid == 0) {
+        for (int b = sk_c0; b <= sk_c1; b += 8) {
+          unsigned spins = 0;
+          while (__hip_atomic_load((gu32*)(p.sk.flags + b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 24)) {  // a contributor that never publishes: give up, count it
+              if (lane == 0) __hip_atomic_fetch_add((gu32*)p.sk.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+          }
+          if (lane == 0) __hip_atomic_store((gu32*)(p.sk.flags + b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+    }
+    if (sk_role != 0) {
+      // one pass over the accumulators, a float4 at a time, for both roles (keeps them in place:
+      // separate store and load-add passes need ~30 more VGPRs, below 4 waves per SIMD).
+      // role 1 publishes its slot (cdna_hip_programming.md Guideline 16, R1: write-through sc1
+      // payload, every storing wave drains, the block barrier, ONE agent-scope flag store);
+      // role 2 adds the contributors' slots in a fixed order (deterministic for a given grid)
+      const bool pub = sk_role == 1;
+      const int bfirst = pub ? sk_slot : sk_c0, blast = pub ? sk_slot : sk_c1;
+      for (int b = bfirst; b <= blast; b += 8) {
+        const int voff = (int)((((uint32_t)b * ACC4) * NT + tid) * 16u);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int e4 = 0; e4 < 4; ++e4) {
+              const int soff = ((i * NI + j) * 4 + e4) * NT * 16;
+              if (pub) {
+                const u32x4 v = {__float_as_uint(acc[i][j][4 * e4]), __float_as_uint(acc[i][j][4 * e4 + 1]),
+                                 __float_as_uint(acc[i][j][4 * e4 + 2]), __float_as_uint(acc[i][j][4 * e4 + 3])};
+                __builtin_amdgcn_raw_buffer_store_b128(v, rp, voff, soff, 16);
+              } else {
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rp, voff, soff, 0);
+                acc[i][j][4 * e4] += __uint_as_float(v.x);
+                acc[i][j][4 * e4 + 1] += __uint_as_float(v.y);
+                acc[i][j][4 * e4 + 2] += __uint_as_float(v.z);
+                acc[i][j][4 * e4 + 3] += __uint_as_float(v.w);
+              }
+            }
+      }
+      if (pub) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+          __hip_atomic_store((gu32*)(p.sk.flags + sk_slot), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+    }
   }
 
   // ---- epilogue: 16-bit rounding, BN partial sums, stores ----
@@ -787,6 +883,56 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs p) {
         }
       }
     }
+  }
+  };  // tile_body
+
+  if constexpr (SK) {
+    // Stream-K, per XCD: the tiles are cut into 8 contiguous groups (consecutive tiles share A
+    // rows: one L2) and group x = blockIdx & 7 is spread over its G/8 blocks x, x+8, x+16, ...
+    // (the dispatcher deals consecutive block ids round-robin over the XCDs).  Block i of a group
+    // owns iterations [I*i/g, I*(i+1)/g) of the group's tile-major (tile, K-step) space: its whole
+    // tiles first, then its last segment (stopping inside a tile: publish the partial), then its
+    // first segment (starting inside a tile: finish it with the partials of the group's lower
+    // blocks).  Every wait points at a lower block id, and lower ids never wait on higher ones,
+    // so the grid drains whatever the residency.
+    const uint32_t g = (uint32_t)p.sk.G >> 3, nk = (uint32_t)nk_all;
+    const uint32_t x = blockIdx.x & 7, i = blockIdx.x >> 3;
+    const uint32_t t_lo = (uint32_t)tiles * x / 8, t_hi = (uint32_t)tiles * (x + 1) / 8;
+    const uint32_t I = (t_hi - t_lo) * nk;  // I * g < 2^32 (conv_sk_blocks)
+    const uint32_t s0 = I * i / g, s1 = I * (i + 1) / g;
+    // segments in run order: those after the first (whole tiles, then the last), then the first
+    const uint32_t f1 = min(s1, (s0 / nk + 1) * nk);
+    const uint32_t nseg = s1 > s0 ? 1u + (s1 > f1 ? (s1 - 1) / nk - f1 / nk + 1 : 0u) : 0u;
+    for (uint32_t q = 0; q < nseg; ++q) {
+      const uint32_t b0 = q + 1 == nseg ? s0 : f1 + q * nk;  // f1 is a tile boundary when s1 > f1
+      const uint32_t tl = b0 / nk;
+      const uint32_t b1 = min(s1, (tl + 1) * nk);
+      const int k0 = (int)(b0 - tl * nk), k1 = (int)(b1 - tl * nk);
+      int role = 0, c0 = 0, c1 = -1;
+      if (k0 > 0 && k1 == nk_all) {
+        role = 2;
+        const uint32_t it0 = tl * nk;  // contributors: the blocks of the group holding [it0, b0)
+        uint32_t c = it0 * g / I;
+        while (c + 1 < i && I * (c + 1) / g <= it0) ++c;
+        while (c > 0 && I * c / g > it0) --c;
+        c0 = (int)(x + 8 * c);
+        c1 = (int)blockIdx.x - 8;
+      } else if (k1 < nk_all) {
+        role = 1;
+      }
+      if (q > 0) __syncthreads();  // the previous tile's epilogue is done with the LDS
+      const int t = (int)(t_lo + tl);
+      tile_body(t / p.n_tiles, t % p.n_tiles, 0, k0, k1, role, (int)blockIdx.x, c0, c1);
+    }
+  } else {
+    const int nsplit = SPLIT ? p.splits : 1;
+    const int bid0 = conv::xcd_remap(blockIdx.x, tiles * nsplit);
+    // split-K: the splits of one tile are consecutive ids (one XCD, shared A/B rows in its L2)
+    const int sp = SPLIT ? bid0 % nsplit : 0;
+    const int bid = SPLIT ? bid0 / nsplit : bid0;
+    const int ks0 = SPLIT ? sp * p.kps : 0;
+    const int ks1 = SPLIT ? min(nk_all, ks0 + p.kps) : nk_all;
+    tile_body(bid / p.n_tiles, bid % p.n_tiles, sp, ks0, ks1, 0, 0, 0, -1);
   }
 }
 
@@ -1929,6 +2075,88 @@ static bool halo_ok(const ConvFwdArgs& a) {
 }
 void conv_set_halo(int on) { g_conv_halo = on; }
 
+// ---- stream-K (conv_fwd_kernel<..., SK = true>) --------------------------------------------------
+// Grids whose 128 x BN tiles do not divide evenly over the 256 CUs lose the idle part of the last
+// round: 784 tiles of a ResNet-50 layer3 1x1 conv are 3 rounds on 240 CUs and 4 on 16, and the K loop
+// is bound by each CU's L2 -> LDS bandwidth, so the step takes 4 tile-times where 3.06 would do
+// (profiles/wave_efficiency_r5.md).  Stream-K spreads the (tile, K-step) iterations evenly over
+// 256 x k blocks; a tile cut between blocks costs one fp32 partial tile written and read back.
+// conv_set_streamk: 0 = off, 1 = auto (per-CU tile balance below kSkEff), 2 = every eligible grid.
+static int g_conv_sk = 0;
+static double kSkEff = 0.9;
+void conv_set_streamk(int mode, double eff) {
+  g_conv_sk = mode;
+  if (eff > 0) kSkEff = eff;
+}
+int conv_get_streamk() { return g_conv_sk; }
+
+namespace {
+struct SkWorkspace {
+  float* part = nullptr;
+  unsigned* flags = nullptr;  // kSkMaxBlocks publish flags, then the give-up counter
+  bool failed = false;
+};
+constexpr int kSkMaxBlocks = 256 * 6;
+constexpr size_t kSkPartBytes = 64ull << 20;  // 1024 blocks x 64 KiB (128 x 128 fp32 tile)
+std::mutex g_sk_mu;
+SkWorkspace g_sk_ws[64];
+}  // namespace
+
+// The device's stream-K workspace, allocated (and the flags zeroed) on first use outside a graph
+// capture; nullptr while capturing before that (the launch then runs the data-parallel grid).
+// One workspace per device: the engine issues its convolutions on one stream at a time.
+static SkWorkspace* sk_workspace(hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_sk_mu);
+  SkWorkspace& w = g_sk_ws[dev];
+  if (w.part != nullptr) return &w;
+  if (w.failed) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (s != nullptr && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) return nullptr;
+  void* part = nullptr;
+  void* flags = nullptr;
+  if (hipMalloc(&part, kSkPartBytes) != hipSuccess || hipMalloc(&flags, (kSkMaxBlocks + 64) * sizeof(unsigned)) != hipSuccess ||
+      hipMemset(flags, 0, (kSkMaxBlocks + 64) * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    if (part) (void)hipFree(part);
+    if (flags) (void)hipFree(flags);
+    (void)hipGetLastError();
+    w.failed = true;
+    return nullptr;
+  }
+  w.part = static_cast<float*>(part);
+  w.flags = static_cast<unsigned*>(flags);
+  return &w;
+}
+
+void conv_sk_prepare() { (void)sk_workspace(nullptr); }
+
+unsigned conv_sk_errors() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || g_sk_ws[dev].flags == nullptr) return 0;
+  unsigned e = 0;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(&e, g_sk_ws[dev].flags + kSkMaxBlocks, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess)
+    throw std::runtime_error("conv_sk_errors: device read failed");
+  return e;
+}
+
+// Blocks of the stream-K grid for this conv (0: run the data-parallel grid).  bpc = resident
+// blocks per CU of the variant (LDS-limited: 4 at BN = 128, 6 at BN = 64).
+int conv_sk_blocks(int64_t tiles, int nk, int bn, int mode) {
+  if (mode == 0 || nk < 2 || tiles < 256) return 0;
+  const double per_cu = (double)tiles / 256.0;
+  const double eff = per_cu / std::ceil(per_cu);
+  if (mode == 1 && eff >= kSkEff) return 0;
+  const int bpc = bn == 128 ? 4 : 6;
+  const int k = std::min<int>(bpc, (int)std::ceil(per_cu));
+  const int G = 256 * k;
+  // every block of every XCD group must hold at least one K-step (an empty block never publishes)
+  if ((tiles / 8) * nk < G / 8 + 1) return 0;
+  if ((tiles / 8 + 1) * (int64_t)nk * (G / 8) >= (1ll << 32)) return 0;  // 32-bit partition math
+  return G;
+}
+
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
           bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, int NT = conv::kThreads>
 static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdArgs& a0) {
@@ -1957,6 +2185,27 @@ static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdAr
     }
   }
   if constexpr (BMT == 128 && STAGES == 1 && LDSEPI && NT == conv::kThreads) {
+    // (not with BNR2: that epilogue spills at the 128-VGPR bound of 4 waves per SIMD)
+    if constexpr (!BNR2) {
+      if (g_conv_sk && !a.f16) {
+        const int64_t tiles = (int64_t)a.m_tiles * a.n_tiles;
+        const int G = conv_sk_blocks(tiles, (int)((int64_t)a.R * a.S * a.C / conv::BK), BN, g_conv_sk);
+        SkWorkspace* ws = G > 0 ? sk_workspace(s) : nullptr;
+        if (ws != nullptr && (size_t)G * (BN == 128 ? 65536u : 32768u) <= kSkPartBytes && G <= kSkMaxBlocks &&
+            a.n_tiles * BN == a.Cout) {
+          a.sk.part = ws->part;
+          a.sk.flags = ws->flags;
+          a.sk.err = ws->flags + kSkMaxBlocks;
+          a.sk.G = G;
+          a.sk.part_bytes = (uint32_t)kSkPartBytes;
+          const dim3 sgrid((unsigned)(G + a.red.blocks));
+          hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, 1, true, BKN, STATS, BNB, BNR, REMAP, ZSIB, BNR2, false,
+                                              conv::kThreads, false, false, 1, true>),
+                             sgrid, block, 0, s, a);
+          return;
+        }
+      }
+    }
     if (a.f16) {
       hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, STAGES, LDSEPI, BKN, STATS, BNB, BNR, REMAP, ZSIB, BNR2, true>),
                          grid, block, 0, s, a);

@@ -152,6 +152,13 @@ int conv_m_tiles(int64_t M);
 void conv_set_variant(int v);
 void conv_set_big(int on);  // 8-wave 256-row tiles where conv_big_auto picks them (default off)
 void conv_set_halo(int on);  // 3x3 / stride-1 halo K loop (default on, DPT_CONV_HALO)
+// stream-K conv_fwd_kernel grids (0 off, 1 auto below the per-CU balance eff, 2 every eligible
+// grid; eff <= 0 keeps the threshold), workspace preallocation, and the bounded-spin give-up count
+void conv_set_streamk(int mode, double eff);
+int conv_get_streamk();
+void conv_sk_prepare();
+unsigned conv_sk_errors();
+int conv_sk_blocks(int64_t tiles, int nk, int bn, int mode);
 void conv_set_wgrad_target(int blocks);  // split-K backward-weight block target (0 = policy)
 // Ho/Wo > 0: explicit output size (padding applied on top/left only beyond what it needs)
 // ws: split-K workspace of conv_fwd_splits(M, Cout, R*S*C) * M * Cout floats when that is > 1

@@ -10,6 +10,7 @@ path (HIP fused optimizer + device-resident scaler + RCCL reducer).
 from __future__ import annotations
 
 import argparse
+import os
 from typing import Optional, Sequence
 
 
@@ -99,6 +100,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="native impl, fp32 (no --amp): run the convolutions on the hand-written fp32 MFMA "
                         "kernels (exact, bitwise deterministic, replay-safe) instead of MIOpen (faster on "
                         "ResNet-50: profiles/conv_f32_r5.md)")
+    g.add_argument("--conv-streamk", choices=("off", "auto", "all"),
+                   default=os.environ.get("DPT_CONV_STREAMK", "off"),
+                   help="native impl: stream-K grids for the MFMA convs whose tiles spread unevenly over the "
+                        "256 CUs (auto), for every eligible conv (all), or never (off; env DPT_CONV_STREAMK)")
     g.add_argument("--no-weight-shadow", dest="weight_shadow", action="store_false",
                    help="native impl: let autocast cast fp32 weights every forward instead of keeping "
                         "16-bit weight shadows updated by the fused optimizer")

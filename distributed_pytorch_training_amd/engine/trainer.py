@@ -99,6 +99,12 @@ class Trainer:
         gpu_cl = self.device.type == "cuda" and bool(getattr(args, "channels_last", False))
         # MFMA convs need channels_last bf16/fp16 activations; routing is per model
         use_native_conv = gpu_cl and bool(getattr(args, "native_conv", True)) and native_conv.ENABLED
+        if use_native_conv:
+            from .. import ops
+            sk = {"off": 0, "auto": 1, "all": 2}[getattr(args, "conv_streamk", "off")]
+            ops.native().conv_set_streamk(sk)   # process-wide, like the other conv policies
+            if sk:
+                ops.native().conv_sk_prepare()  # workspace before any graph capture
         # every supported conv runs native: small tile grids split their K loop (split-K,
         # conv_kernels.hip), which made the MFMA path faster than MIOpen on ResNet-18 / 32x32
         # under hipGraph too; DPT_CONV_MIN_PIXELS still routes tiny convs to MIOpen
