@@ -110,6 +110,16 @@ def parse(argv=None):
                          "native engine on GPUs)")
     ap.add_argument("--stock-timeout", type=float, default=420.0,
                     help="seconds the stock child job may take before it is killed (then no same-box number)")
+    ap.add_argument("--extra-windows", default="auto", choices=["auto", "on", "off"],
+                    help="after the headline (and the stock job), fresh child jobs on the same GPUs for "
+                         "BASELINE.json configs 4 and 5: at 4 GPUs the fp32 ResNet-50 run (AMP vs FP32 with "
+                         "the sync profile), at 8 GPUs ViT-B/16 bf16 AdamW at several bucket caps; recorded "
+                         "under extra_windows, never part of the headline (auto: on for the native ResNet-50 "
+                         "bf16 engine on 4 or 8 GPUs)")
+    ap.add_argument("--extra-timeout", type=float, default=300.0,
+                    help="seconds each extra-window child job may take")
+    ap.add_argument("--vit-buckets", default="25,100,400",
+                    help="bucket caps (MB) of the 8-GPU ViT-B/16 extra windows")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -330,6 +340,73 @@ def _stock_argv(a, json_out: str) -> list:
         if getattr(a, flag):
             argv.append("--" + flag.replace("_", "-"))
     return argv
+
+
+def _run_child(argv: list, timeout: float) -> dict:
+    """A fresh child ``bench.py`` job (new interpreter, launcher variables stripped so it picks its
+    own rendezvous and self-launches its ranks); returns its JSON record or the reason there is
+    none."""
+    import tempfile
+    fd, out = tempfile.mkstemp(prefix="dpt_child_", suffix=".json")
+    os.close(fd)
+    drop = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
+            "MASTER_PORT", "GROUP_WORLD_SIZE", "ROLE_WORLD_SIZE", CHILD_MARK, "NCCL_DEBUG", "NCCL_DEBUG_FILE",
+            "NCCL_DEBUG_SUBSYS")
+    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
+    cmd = [sys.executable, os.path.abspath(__file__), *argv, "--json-out", out]
+    t0 = time.time()
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+        with open(out) as f:
+            lines = [json.loads(l) for l in f if l.startswith("{")]
+        if r.returncode != 0 or not lines:
+            return {"error": f"child job exited {r.returncode}: {r.stderr[-400:]}", "wall_s": round(time.time() - t0, 1)}
+        rec = lines[-1]
+        rec["wall_s"] = round(time.time() - t0, 1)
+        return rec
+    except subprocess.TimeoutExpired:
+        return {"error": f"child job exceeded {timeout:.0f} s"}
+    except (OSError, ValueError) as e:
+        return {"error": repr(e)[:400]}
+    finally:
+        try:
+            os.remove(out)
+        except OSError:
+            pass
+
+
+def _window(rec: dict, argv: list) -> dict:
+    """The fields of a child record that the extra windows keep."""
+    if "error" in rec:
+        return {"error": rec["error"], "cmd": "bench.py " + " ".join(argv)}
+    cfg = rec.get("config", {})
+    return {"value": rec.get("value"), "unit": rec.get("unit"), "ms_per_step": rec.get("ms_per_step"),
+            "n_gpus": rec.get("n_gpus"), "steps": rec.get("steps"), "dtype": rec.get("dtype"),
+            "model": cfg.get("model"), "per_gpu_batch": cfg.get("per_gpu_batch"),
+            "bucket_cap_mb": cfg.get("bucket_cap_mb"), "optimizer": cfg.get("optimizer"),
+            "pct_step_allreduce": rec.get("pct_step_allreduce"),
+            "pct_step_exposed_comm": rec.get("pct_step_exposed_comm"),
+            "sync_profile_window": rec.get("sync_profile_window"),
+            "comm_kind": rec.get("comm", {}).get("kind"), "buckets_mib": rec.get("comm", {}).get("buckets_mib"),
+            "wall_s": rec.get("wall_s"), "cmd": "bench.py " + " ".join(argv)}
+
+
+def extra_windows_plan(a, ws: int, forced: bool = False) -> list:
+    """(name, argv) of the extra windows for a ``ws``-GPU headline job (BASELINE.json configs 4/5);
+    ``forced`` (--extra-windows on) adds the fp32 window at any world size."""
+    common = ["--gpus", str(ws), "--stock-baseline", "off", "--extra-windows", "off", "--comm", a.comm]
+    plan = []
+    if (ws == 4 or forced) and not a.no_amp:
+        plan.append(("resnet50_fp32", common + ["--model", a.model, "--batch-size", str(a.batch_size),
+                                                "--image-size", str(a.image_size), "--no-amp", "--steps", "10",
+                                                "--warmup", "3", "--profile-steps", "6"]))
+    if ws == 8:
+        for cap in [c for c in a.vit_buckets.split(",") if c.strip()]:
+            plan.append((f"vit_b16_bucket{float(cap):g}mb",
+                         common + ["--model", "vit_b_16", "--batch-size", "128", "--optimizer", "adamw",
+                                   "--bucket-cap-mb", cap.strip(), "--steps", "10", "--warmup", "3",
+                                   "--profile-steps", "6"]))
+    return plan
 
 
 def run_stock_baseline(a) -> dict:
@@ -596,8 +673,13 @@ def main(argv=None) -> int:
     stock_on = a.stock_baseline == "on" or (a.stock_baseline == "auto" and a.impl == "native"
                                             and device.type == "cuda" and not a.rehearse_shared_gpu
                                             and not a.fake_pg)
-    if stock_on:
-        # free this job's GPU memory, then rank 0 runs the stock job on the same GPUs while the
+    extra_on = a.extra_windows == "on" or (a.extra_windows == "auto" and a.impl == "native"
+                                            and device.type == "cuda" and not a.rehearse_shared_gpu
+                                            and not a.fake_pg and a.model == "resnet50" and not a.no_amp
+                                            and ws in (4, 8))
+    extra_plan = extra_windows_plan(a, ws, forced=a.extra_windows == "on") if extra_on else []
+    if stock_on or extra_plan:
+        # free this job's GPU memory, then rank 0 runs the child jobs on the same GPUs while the
         # other ranks wait on the TCPStore (host side: no collective kernel spinning on a GPU)
         del trainer, model, batches, loader, ddp, comm
         import gc
@@ -607,15 +689,22 @@ def main(argv=None) -> int:
             torch.cuda.empty_cache()
         if ws > 1:
             dist.barrier()
-        stock = run_stock_baseline(a) if rank == 0 else None
+        stock = run_stock_baseline(a) if rank == 0 and stock_on else None
+        extra = {}
+        if rank == 0:
+            for name, argv in extra_plan:
+                extra[name] = _window(_run_child(argv, a.extra_timeout), argv)
         if ws > 1:
             store = dist.distributed_c10d._get_default_store()
             key = "dpt_bench_stock_done"
             if rank == 0:
                 store.set(key, "1")
             else:
-                store.wait([key], datetime.timedelta(seconds=a.stock_timeout + 120))
-        if rank == 0:
+                wait_s = (a.stock_timeout if stock_on else 0) + a.extra_timeout * len(extra_plan) + 120
+                store.wait([key], datetime.timedelta(seconds=wait_s))
+        if rank == 0 and extra_plan:
+            rec["extra_windows"] = extra
+        if rank == 0 and stock_on:
             rec["baseline"]["stock_same_box"] = stock
             if stock.get("img_s"):
                 rec["baseline"]["stock_same_box_img_s"] = stock["img_s"]
