@@ -1993,8 +1993,16 @@ void conv_set_variant(int v) { g_conv_variant = v; }
 // the neighbouring kernels) the per-shape wins did not show (11680/11521 vs 11659/11534 img/s,
 // same-box A/B).  conv_set_big(1) turns it on.
 static int g_conv_big = 0;
-static int conv_big_auto(int64_t M, int N, int64_t K) {
+// conv_set_big(2 / 3): the deep one-tap convs (K >= 1024 / >= 512, N a multiple of 256) on the
+// 8-wave 128 x 256 tile with the 3-stage pipelined K loop (variant 13): their grids are 392-784
+// 128 x 128 tiles of 16-32 K-steps, latency-bound at ~3 resident blocks per CU
+// (profiles/step_pmc_r5.md); in isolation v13 was 5-17 % faster there (profiles/conv_variants_r3_pipe3.md).
+static int conv_big_auto(int64_t M, int N, int64_t K, int taps) {
   if (!g_conv_big) return 0;
+  if (g_conv_big >= 2) {
+    const int64_t kmin = g_conv_big == 2 ? 1024 : 512;
+    return (taps == 1 && K >= kmin && N % 256 == 0) ? 13 : 0;
+  }
   if (N == 256 && K >= 1024 && M >= 32768) return 9;
   if (N == 512 && K >= 2048 && M <= 16384) return 10;
   return 0;
@@ -2457,7 +2465,7 @@ static void conv_fwd_impl(const uint16_t* x, const uint16_t* w, uint16_t* y, int
   if (!bkn && maybe_split(a, ws, psum != nullptr, false, false, false, s)) return;
   if (!bkn && v == 0) v = fwd_shape_variant(a, psum != nullptr);
   if (!bkn && !a.f16) {
-    const int vb = (v >= 9 && v <= 13) ? v : v == 0 ? conv_big_auto(a.M, Cout, (int64_t)R * S * C) : 0;
+    const int vb = (v >= 9 && v <= 13) ? v : v == 0 ? conv_big_auto(a.M, Cout, (int64_t)R * S * C, R * S) : 0;
     if (vb && conv_fwd_big(vb, a, s)) return;
   }
   if (wide) conv_fwd_dispatch<128>(v, bkn, a, s);
@@ -2498,7 +2506,7 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
   const int cv = fwd_variant();
   if (!f16 && (cv == 0 || (cv >= 9 && cv <= 13))) {
     // 8-wave tiles (conv_big_auto, or a forced variant): N = C, K = Cout*R*S
-    const int vb = cv ? cv : conv_big_auto(a.M, C, (int64_t)Cout * R * S);
+    const int vb = cv ? cv : conv_big_auto(a.M, C, (int64_t)Cout * R * S, R * S);
     if (vb && C % big_bn(vb) == 0) {
       const int bn = big_bn(vb), bm = big_bm(vb);
       a.n_tiles = C / bn;
