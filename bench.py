@@ -116,8 +116,11 @@ def parse(argv=None):
                          "the sync profile), at 8 GPUs ViT-B/16 bf16 AdamW at several bucket caps; recorded "
                          "under extra_windows, never part of the headline (auto: on for the native ResNet-50 "
                          "bf16 engine on 4 or 8 GPUs)")
-    ap.add_argument("--extra-timeout", type=float, default=300.0,
+    ap.add_argument("--extra-timeout", type=float, default=240.0,
                     help="seconds each extra-window child job may take")
+    ap.add_argument("--extra-budget", type=float, default=540.0,
+                    help="seconds all extra-window child jobs together may take (later windows are "
+                         "skipped and recorded as such once it is spent)")
     ap.add_argument("--vit-buckets", default="25,100,400",
                     help="bucket caps (MB) of the 8-GPU ViT-B/16 extra windows")
     ap.add_argument("--json-out", default=None)
@@ -692,15 +695,21 @@ def main(argv=None) -> int:
         stock = run_stock_baseline(a) if rank == 0 and stock_on else None
         extra = {}
         if rank == 0:
+            t_extra = time.time()
             for name, argv in extra_plan:
-                extra[name] = _window(_run_child(argv, a.extra_timeout), argv)
+                left = a.extra_budget - (time.time() - t_extra)
+                if left < 30:
+                    extra[name] = {"error": f"skipped: --extra-budget {a.extra_budget:.0f} s spent",
+                                   "cmd": "bench.py " + " ".join(argv)}
+                    continue
+                extra[name] = _window(_run_child(argv, min(a.extra_timeout, left)), argv)
         if ws > 1:
             store = dist.distributed_c10d._get_default_store()
             key = "dpt_bench_stock_done"
             if rank == 0:
                 store.set(key, "1")
             else:
-                wait_s = (a.stock_timeout if stock_on else 0) + a.extra_timeout * len(extra_plan) + 120
+                wait_s = (a.stock_timeout if stock_on else 0) + (a.extra_budget if extra_plan else 0) + 120
                 store.wait([key], datetime.timedelta(seconds=wait_s))
         if rank == 0 and extra_plan:
             rec["extra_windows"] = extra
