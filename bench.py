@@ -123,6 +123,9 @@ def parse(argv=None):
                          "skipped and recorded as such once it is spent)")
     ap.add_argument("--vit-buckets", default="25,100,400",
                     help="bucket caps (MB) of the 8-GPU ViT-B/16 extra windows")
+    ap.add_argument("--extra-rccl-channels", default="8,16",
+                    help="per-communicator RCCL channel bounds of the 8-GPU ResNet-50 extra windows (how many "
+                         "CUs RCCL's kernels take from the overlapped backward; the headline uses RCCL's choice)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -397,13 +400,19 @@ def _window(rec: dict, argv: list) -> dict:
 def extra_windows_plan(a, ws: int, forced: bool = False) -> list:
     """(name, argv) of the extra windows for a ``ws``-GPU headline job (BASELINE.json configs 4/5);
     ``forced`` (--extra-windows on) adds the fp32 window at any world size."""
-    common = ["--gpus", str(ws), "--stock-baseline", "off", "--extra-windows", "off", "--comm", a.comm]
+    common = ["--gpus", str(ws), "--stock-baseline", "off", "--extra-windows", "off", "--comm", a.comm,
+              "--bucket-cap-mb", str(a.bucket_cap_mb)]
     plan = []
     if (ws == 4 or forced) and not a.no_amp:
         plan.append(("resnet50_fp32", common + ["--model", a.model, "--batch-size", str(a.batch_size),
                                                 "--image-size", str(a.image_size), "--no-amp", "--steps", "10",
                                                 "--warmup", "3", "--profile-steps", "6"]))
     if ws == 8:
+        for ch in [c for c in a.extra_rccl_channels.split(",") if c.strip()]:
+            plan.append((f"resnet50_rccl_channels{int(ch)}",
+                         common + ["--model", a.model, "--batch-size", str(a.batch_size), "--image-size",
+                                   str(a.image_size), "--rccl-channels", ch.strip(), "--steps", "10",
+                                   "--warmup", "3", "--profile-steps", "6"]))
         for cap in [c for c in a.vit_buckets.split(",") if c.strip()]:
             plan.append((f"vit_b16_bucket{float(cap):g}mb",
                          common + ["--model", "vit_b_16", "--batch-size", "128", "--optimizer", "adamw",

@@ -258,9 +258,16 @@ def test_extra_windows_plan():
     assert "--no-amp" in argv and argv[argv.index("--gpus") + 1] == "4"
     assert argv[argv.index("--extra-windows") + 1] == "off" and argv[argv.index("--stock-baseline") + 1] == "off"
     plan8 = dict(bench.extra_windows_plan(bench.parse(["--gpus", "8"]), 8))
-    assert sorted(plan8) == ["vit_b16_bucket100mb", "vit_b16_bucket25mb", "vit_b16_bucket400mb"]
-    for argv in plan8.values():
-        assert argv[argv.index("--model") + 1] == "vit_b_16" and argv[argv.index("--optimizer") + 1] == "adamw"
+    assert sorted(plan8) == ["resnet50_rccl_channels16", "resnet50_rccl_channels8", "vit_b16_bucket100mb",
+                             "vit_b16_bucket25mb", "vit_b16_bucket400mb"]
+    for name, argv in plan8.items():
+        if name.startswith("vit"):
+            assert argv[argv.index("--model") + 1] == "vit_b_16" and argv[argv.index("--optimizer") + 1] == "adamw"
+            # the window's own cap is the last --bucket-cap-mb (argparse keeps the last)
+            caps = [argv[i + 1] for i, t in enumerate(argv) if t == "--bucket-cap-mb"]
+            assert caps[-1] == name[len("vit_b16_bucket"):-2]
+        else:
+            assert argv[argv.index("--rccl-channels") + 1] == name[len("resnet50_rccl_channels"):]
     assert bench.extra_windows_plan(bench.parse(["--gpus", "2"]), 2) == []
     assert bench.extra_windows_plan(bench.parse(["--gpus", "4", "--no-amp"]), 4) == []
 
