@@ -118,10 +118,10 @@ def parse(argv=None):
                          "bf16 engine on 4 or 8 GPUs)")
     ap.add_argument("--extra-timeout", type=float, default=240.0,
                     help="seconds each extra-window child job may take")
-    ap.add_argument("--extra-budget", type=float, default=540.0,
+    ap.add_argument("--extra-budget", type=float, default=300.0,
                     help="seconds all extra-window child jobs together may take (later windows are "
                          "skipped and recorded as such once it is spent)")
-    ap.add_argument("--vit-buckets", default="25,100,400",
+    ap.add_argument("--vit-buckets", default="25,400,100",
                     help="bucket caps (MB) of the 8-GPU ViT-B/16 extra windows")
     ap.add_argument("--extra-rccl-channels", default="8,16",
                     help="per-communicator RCCL channel bounds of the 8-GPU ResNet-50 extra windows (how many "
@@ -408,16 +408,17 @@ def extra_windows_plan(a, ws: int, forced: bool = False) -> list:
                                                 "--image-size", str(a.image_size), "--no-amp", "--steps", "10",
                                                 "--warmup", "3", "--profile-steps", "6"]))
     if ws == 8:
-        for ch in [c for c in a.extra_rccl_channels.split(",") if c.strip()]:
-            plan.append((f"resnet50_rccl_channels{int(ch)}",
-                         common + ["--model", a.model, "--batch-size", str(a.batch_size), "--image-size",
-                                   str(a.image_size), "--rccl-channels", ch.strip(), "--steps", "10",
-                                   "--warmup", "3", "--profile-steps", "6"]))
-        for cap in [c for c in a.vit_buckets.split(",") if c.strip()]:
-            plan.append((f"vit_b16_bucket{float(cap):g}mb",
-                         common + ["--model", "vit_b_16", "--batch-size", "128", "--optimizer", "adamw",
-                                   "--bucket-cap-mb", cap.strip(), "--steps", "10", "--warmup", "3",
-                                   "--profile-steps", "6"]))
+        vit = [(f"vit_b16_bucket{float(cap):g}mb",
+                common + ["--model", "vit_b_16", "--batch-size", "128", "--optimizer", "adamw",
+                          "--bucket-cap-mb", cap.strip(), "--steps", "10", "--warmup", "3", "--profile-steps", "6"])
+               for cap in a.vit_buckets.split(",") if cap.strip()]
+        r50 = [(f"resnet50_rccl_channels{int(ch)}",
+                common + ["--model", a.model, "--batch-size", str(a.batch_size), "--image-size", str(a.image_size),
+                          "--rccl-channels", ch.strip(), "--steps", "10", "--warmup", "3", "--profile-steps", "6"])
+               for ch in a.extra_rccl_channels.split(",") if ch.strip()]
+        # interleaved, the first two ViT caps first: what the time budget cuts is the least informative
+        order = vit[:2] + r50[:1] + vit[2:] + r50[1:]
+        plan.extend(order)
     return plan
 
 
