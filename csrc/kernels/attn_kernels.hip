@@ -31,6 +31,12 @@ constexpr int D = 64;     // head dim
 constexpr int RB = 128;   // LDS row bytes (64 bf16)
 }  // namespace attn
 
+// 2^x on the transcendental unit (v_exp_f32) without the denormal-range fix-up libm's exp2f adds
+// (compare, scale, ldexp, select: 4 more VALU per score).  It differs only where 2^x < 2^-126,
+// probabilities that vanish in the bf16 operands anyway; forward and backward use the same one,
+// so the recomputed P matches the forward's.
+__device__ __forceinline__ float attn_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // Stage rows [0, S) of a [S, ld]-strided bf16 matrix's 64-column slice into an LDS image of
 // SP rows (rows >= S zero).
 __device__ __forceinline__ void attn_stage(unsigned char* img, const uint16_t* src, int64_t ld, int S, int SP,
@@ -79,15 +85,21 @@ __global__ __launch_bounds__(NT * 64) void attn_fwd_kernel(const uint16_t* __res
     for (int s = 0; s < 4; ++s) sc[kt] = mfma32(row_frag<RB>(kimg, kt * 32 + r, 2 * s + h), qf[s], sc[kt]);
   }
   // softmax over keys (this lane's registers + the other lane half)
+  // padding keys exist only in the last tile(s): the per-element mask is a wave-uniform branch
+  // away everywhere else (it was 2 of the ~10 VALU per score)
   float m = -INFINITY;
 #pragma unroll
-  for (int kt = 0; kt < NT; ++kt)
+  for (int kt = 0; kt < NT; ++kt) {
+    if ((kt + 1) * 32 > S) {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int key = kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (key >= S) sc[kt][e] = -INFINITY;
-      m = fmaxf(m, sc[kt][e]);
+      for (int e = 0; e < 16; ++e) {
+        const int key = kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (key >= S) sc[kt][e] = -INFINITY;
+      }
     }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) m = fmaxf(m, sc[kt][e]);
+  }
   m = fmaxf(m, __shfl_xor(m, 32, 64));
   const float ms = m * scale_log2;
   float l = 0.f;
@@ -95,7 +107,7 @@ __global__ __launch_bounds__(NT * 64) void attn_fwd_kernel(const uint16_t* __res
   for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const float pv = exp2f(__builtin_fmaf(sc[kt][e], scale_log2, -ms));
+      const float pv = attn_exp2(__builtin_fmaf(sc[kt][e], scale_log2, -ms));
       sc[kt][e] = pv;
       l += pv;
     }
@@ -231,7 +243,7 @@ __global__ __launch_bounds__(NT * 64, PHASE == 1 ? DPT_ATTN_P1_WAVES : PHASE == 
 #pragma unroll
       for (int e = 0; e < 16; ++e) {  // rows = queries, column = this lane's key
         const int qq = qt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const float pv = key < S ? exp2f(__builtin_fmaf(sc[e], scale_log2, -ls[qq])) : 0.f;
+        const float pv = key < S ? attn_exp2(__builtin_fmaf(sc[e], scale_log2, -ls[qq])) : 0.f;
         sc[e] = pv;
         dp[e] = pv * (dp[e] - dd[qq]);
       }
@@ -291,7 +303,7 @@ __global__ __launch_bounds__(NT * 64, PHASE == 1 ? DPT_ATTN_P1_WAVES : PHASE == 
 #pragma unroll
       for (int e = 0; e < 16; ++e) {  // rows = keys, column = this lane's query
         const int key = kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const float pv = key < S ? exp2f(__builtin_fmaf(st[e], scale_log2, -lq)) : 0.f;
+        const float pv = key < S ? attn_exp2(__builtin_fmaf(st[e], scale_log2, -lq)) : 0.f;
         st[e] = pv * (dpt[e] - dq0);
       }
 #pragma unroll
