@@ -574,7 +574,7 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
           unsigned spins = 0;
           while (__hip_atomic_load((gu32*)(p.sk.flags + b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
             __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 24)) {  // a contributor that never publishes: give up, count it
+            if (++spins > (1u << 20)) {  // ~1 s: a contributor that never publishes - give up, count it
               if (lane == 0) __hip_atomic_fetch_add((gu32*)p.sk.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               break;
             }
