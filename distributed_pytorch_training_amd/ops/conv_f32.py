@@ -30,7 +30,20 @@ from . import native, native_available
 # solvers (which use Winograd for the 3x3s), and the fp32 ResNet-18 / 32x32 replay 41k against 66k
 # samples/s (profiles/conv_f32_r5.md) - so MIOpen stays the default fp32 path.
 ENABLED = os.environ.get("DPT_NATIVE_CONV_F32", "0") == "1"
+# Which convs the enabled path takes (A/B, DPT_NATIVE_CONV_F32_SCOPE): "all", "1x1" (one-tap,
+# stride 1), "1x1s" (one-tap, any stride), "kxk" (multi-tap convs only); the rest stay on MIOpen.
+SCOPE = os.environ.get("DPT_NATIVE_CONV_F32_SCOPE", "all")
 _CL = torch.channels_last
+
+
+def _in_scope(r: int, s: int, stride: int) -> bool:
+    if SCOPE == "1x1":
+        return r == 1 and s == 1 and stride == 1
+    if SCOPE == "1x1s":
+        return r == 1 and s == 1
+    if SCOPE == "kxk":
+        return r * s > 1
+    return True
 
 
 def supported(x: torch.Tensor, w: torch.Tensor, bias, stride, padding, dilation, groups) -> bool:
@@ -42,6 +55,8 @@ def supported(x: torch.Tensor, w: torch.Tensor, bias, stride, padding, dilation,
     if tuple(dilation) != (1, 1) or stride[0] != stride[1] or padding[0] != padding[1]:
         return False
     cout, cin, r, s = w.shape
+    if not _in_scope(r, s, stride[0]):
+        return False
     return (cout % 4 == 0 and x.shape[1] == cin and x.is_contiguous(memory_format=_CL)
             and (x.shape[2] + 2 * padding[0] - r) // stride[0] + 1 > 0
             and (x.shape[3] + 2 * padding[1] - s) // stride[1] + 1 > 0)
