@@ -118,6 +118,8 @@ def parse(argv=None):
                          "bf16 engine on 4 or 8 GPUs)")
     ap.add_argument("--extra-timeout", type=float, default=240.0,
                     help="seconds each extra-window child job may take")
+    ap.add_argument("--extra-steps", type=int, default=10,
+                    help="timed steps of each extra-window job (3 warm-up steps, a 6-step sync-profile window)")
     ap.add_argument("--extra-budget", type=float, default=300.0,
                     help="seconds all extra-window child jobs together may take (later windows are "
                          "skipped and recorded as such once it is spent)")
@@ -402,19 +404,17 @@ def extra_windows_plan(a, ws: int, forced: bool = False) -> list:
     ``forced`` (--extra-windows on) adds the fp32 window at any world size."""
     common = ["--gpus", str(ws), "--stock-baseline", "off", "--extra-windows", "off", "--comm", a.comm,
               "--bucket-cap-mb", str(a.bucket_cap_mb)]
+    steps = ["--steps", str(a.extra_steps), "--warmup", "3", "--profile-steps", "6"]
+    r50_shape = ["--model", a.model, "--batch-size", str(a.batch_size), "--image-size", str(a.image_size)]
     plan = []
     if (ws == 4 or forced) and not a.no_amp:
-        plan.append(("resnet50_fp32", common + ["--model", a.model, "--batch-size", str(a.batch_size),
-                                                "--image-size", str(a.image_size), "--no-amp", "--steps", "10",
-                                                "--warmup", "3", "--profile-steps", "6"]))
+        plan.append(("resnet50_fp32", common + r50_shape + ["--no-amp"] + steps))
     if ws == 8:
         vit = [(f"vit_b16_bucket{float(cap):g}mb",
                 common + ["--model", "vit_b_16", "--batch-size", "128", "--optimizer", "adamw",
-                          "--bucket-cap-mb", cap.strip(), "--steps", "10", "--warmup", "3", "--profile-steps", "6"])
+                          "--bucket-cap-mb", cap.strip()] + steps)
                for cap in a.vit_buckets.split(",") if cap.strip()]
-        r50 = [(f"resnet50_rccl_channels{int(ch)}",
-                common + ["--model", a.model, "--batch-size", str(a.batch_size), "--image-size", str(a.image_size),
-                          "--rccl-channels", ch.strip(), "--steps", "10", "--warmup", "3", "--profile-steps", "6"])
+        r50 = [(f"resnet50_rccl_channels{int(ch)}", common + r50_shape + ["--rccl-channels", ch.strip()] + steps)
                for ch in a.extra_rccl_channels.split(",") if ch.strip()]
         # interleaved, the first two ViT caps first: what the time budget cuts is the least informative
         order = vit[:2] + r50[:1] + vit[2:] + r50[1:]

@@ -272,13 +272,29 @@ def test_extra_windows_plan():
     assert bench.extra_windows_plan(bench.parse(["--gpus", "4", "--no-amp"]), 4) == []
 
 
+def test_bench_extra_window_two_ranks(tmp_path):
+    """N = 2: rank 0 runs the extra-window child job (itself two ranks) while rank 1 waits on the
+    store; the record carries it and the job exits cleanly."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--extra-windows", "on",
+                        "--extra-steps", "2", "--stock-baseline", "off", *TINY], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    _check(lines[0], 2)
+    w = lines[0]["extra_windows"]["resnet50_fp32"]
+    assert "error" not in w, w
+    assert w["n_gpus"] == 2 and w["dtype"] == "fp32"
+
+
 def test_bench_extra_window_record(tmp_path):
     """--extra-windows on: the fp32 child job runs after the headline and lands under
     extra_windows, outside the headline fields."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--extra-windows", "on",
-                        "--stock-baseline", "off", *TINY], cwd=tmp_path, capture_output=True, text=True,
-                       timeout=900, env=env)
+                        "--extra-steps", "2", "--stock-baseline", "off", *TINY], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1
@@ -286,5 +302,5 @@ def test_bench_extra_window_record(tmp_path):
     _check(rec, 1)
     w = rec["extra_windows"]["resnet50_fp32"]
     assert "error" not in w, w
-    assert w["dtype"] == "fp32" and w["n_gpus"] == 1 and w["value"] > 0 and w["steps"] == 10
+    assert w["dtype"] == "fp32" and w["n_gpus"] == 1 and w["value"] > 0 and w["steps"] == 2
     assert rec["dtype"] == "bf16"
