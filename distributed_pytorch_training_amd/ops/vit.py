@@ -23,6 +23,8 @@ one path.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional, Tuple
 
 import torch
@@ -189,10 +191,31 @@ def _wgrad_splits(n_out: int, n_in: int, T: int) -> int:
     return s
 
 
+# dW = dY^T X on the native MFMA backward-weight kernel of the 1x1 convolutions (a [1, 1, T, C]
+# channels-last "image"; split-K with fp32 partials and a fixed-order reduce, deterministic) for
+# inputs up to this many features; hipBLASLt's split-K batched GEMM above it.  ViT-B/16 at
+# batch 128 (bench/vit_wgrad_ab.py, profiles/vit_wgrad_ab_r5.md): qkv 126 vs 138 us, proj 53 vs
+# 64, fc1 150 vs 153 - but fc2 (3,072 inputs) 155 vs 141.  0 disables.
+NATIVE_WGRAD_MAX_IN = int(os.environ.get("DPT_VIT_NATIVE_WGRAD_MAX_IN", "1024"))
+
+
+def _native_wgrad_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
+    n_out, n_in = dy.shape[1], x.shape[1]
+    return (dy.is_cuda and native_available() and dy.dtype == x.dtype and dy.dtype in _KIND
+            and n_in <= NATIVE_WGRAD_MAX_IN and n_out % 64 == 0 and n_in % 64 == 0 and dy.shape[0] < (1 << 31))
+
+
 def wgrad_splitk(dy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
     """dY^T X ([T, n_out], [T, n_in] -> [n_out, n_in]) as split-K with fp32 partials."""
     T, n_out = dy.shape
     n_in = x.shape[1]
+    if _native_wgrad_ok(dy, x) and out_dtype in (torch.float32, dy.dtype):
+        cl = torch.channels_last
+        dy4 = dy.view(1, 1, T, n_out).permute(0, 3, 1, 2)      # [1, n_out, 1, T], channels_last
+        x4 = x.view(1, 1, T, n_in).permute(0, 3, 1, 2)
+        if dy4.is_contiguous(memory_format=cl) and x4.is_contiguous(memory_format=cl):
+            dw = native().conv_wgrad(dy4, x4, [n_out, n_in, 1, 1], 1, 0, out_dtype == torch.float32)
+            return dw.view(n_out, n_in)
     s = _wgrad_splits(n_out, n_in, T)
     if s == 1:
         return (dy.t() @ x).to(out_dtype)
