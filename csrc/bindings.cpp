@@ -1113,6 +1113,32 @@ std::vector<Tensor> gelu_bwd(Tensor gh, Tensor u, c10::optional<Tensor> bias, bo
   return {gu, db};
 }
 
+// A Linear's backward-data with the GELU backward fused (conv_fwd_kernel DGELU epilogue):
+// gu = (dy @ wt^T) * gelu'(u + bias) and part [n_in][tiles] (the column sums of gu per 128-row
+// tile: bias gradient = part.sum(1)).  dy [T, n_out], wt [n_in, n_out] (the weight transposed),
+// u [T, n_in] 16-bit and contiguous; bias fp32 [n_in].
+std::vector<Tensor> linear_dgrad_dgelu(Tensor dy, Tensor wt, Tensor u, Tensor bias) {
+  const int kind = act16_kind(u, "linear_dgrad_dgelu: u");
+  TORCH_CHECK(act16_kind(dy, "linear_dgrad_dgelu: grad") == kind && act16_kind(wt, "linear_dgrad_dgelu: wt") == kind,
+              "linear_dgrad_dgelu: grad, wt and u must share one 16-bit dtype");
+  TORCH_CHECK(dy.dim() == 2 && wt.dim() == 2 && u.dim() == 2 && dy.is_contiguous() && wt.is_contiguous() &&
+                  u.is_contiguous(), "linear_dgrad_dgelu: contiguous 2-D operands");
+  const int64_t T = dy.size(0), n_out = dy.size(1), n_in = wt.size(0);
+  TORCH_CHECK(wt.size(1) == n_out && u.size(0) == T && u.size(1) == n_in, "linear_dgrad_dgelu: shape mismatch");
+  TORCH_CHECK(n_in % 128 == 0 && n_out % 64 == 0, "linear_dgrad_dgelu: n_in % 128 == 0 and n_out % 64 == 0");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.is_contiguous() && bias.numel() == n_in && bias.is_cuda(),
+              "linear_dgrad_dgelu: fp32 bias of n_in elements on the device");
+  TORCH_CHECK(T * n_out < (1ll << 31) && T * n_in < (1ll << 31), "linear_dgrad_dgelu: too many elements");
+  auto gu = at::empty_like(u);
+  auto part = at::empty({n_in, (int64_t)dpt::linear_dgrad_dgelu_tiles(T)}, u.options().dtype(at::kFloat));
+  c10::hip::HIPGuard guard(u.device().index());
+  dpt::launch_linear_dgrad_dgelu(static_cast<const uint16_t*>(dy.data_ptr()), static_cast<const uint16_t*>(wt.data_ptr()),
+                                 static_cast<const uint16_t*>(u.data_ptr()), bias.data_ptr<float>(),
+                                 static_cast<uint16_t*>(gu.data_ptr()), part.data_ptr<float>(), T, (int)n_out,
+                                 (int)n_in, kind == 2, cur_stream(u));
+  return {gu, part};
+}
+
 // Column sums of a 16-bit [.., F] gradient (a Linear's bias gradient) in out_dtype's kind.
 Tensor bias_grad16(Tensor gy, int64_t out_kind) {
   const int kind = act16_kind(gy, "bias_grad16: grad");
@@ -1207,6 +1233,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gamma"), py::arg("want_ga"), py::arg("bias_like"), py::arg("want_dparams"));
   m.def("gelu_fwd", &gelu_fwd, py::arg("u"), py::arg("bias"));
   m.def("gelu_bwd", &gelu_bwd, py::arg("grad"), py::arg("u"), py::arg("bias"), py::arg("want_dbias"));
+  m.def("linear_dgrad_dgelu", &linear_dgrad_dgelu, py::arg("grad"), py::arg("wt"), py::arg("u"), py::arg("bias"));
   m.def("copy_rows16", &copy_rows16, py::arg("src"), py::arg("dst"));
   m.def("bias_grad16", &bias_grad16, py::arg("grad"), py::arg("out_kind"));
   m.def("sum_partials", &sum_partials, py::arg("part"), py::arg("out_kind"));

@@ -32,6 +32,7 @@
 #include <stdexcept>
 
 #include "carry.h"
+#include "gelu.h"
 #include "common.h"
 #include "kernels.h"
 #include "mfma.h"
@@ -212,7 +213,8 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 // tile is bound by what one CU can pull from L2 into LDS (docs/DESIGN.md 7.1).
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
           bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, bool F16 = false,
-          int NT = conv::kThreads, bool SPLIT = false, bool HALO = false, int HB = 1, bool SK = false>
+          int NT = conv::kThreads, bool SPLIT = false, bool HALO = false, int HB = 1, bool SK = false,
+          bool DGELU = false>
 __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
   constexpr int BM = BMT;
@@ -226,6 +228,10 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
   constexpr int B_PER_T = BN * 8 / NT;  // (B)
   static_assert(!HALO || (BMT == 128 && STAGES == 1 && !BKN && !SPLIT && NT == conv::kThreads), "HALO config");
   static_assert(!SK || (STAGES == 1 && !HALO && !SPLIT && LDSEPI && !BNR2 && NT == conv::kThreads), "SK config");
+  // DGELU (with BNB, a Linear's backward-data: ViT's fc2): the output is gu = g * gelu'(u + b)
+  // with u = bnx (the fc1 GEMM output before its bias) and b = bn_mean (fp32 bias); bp1 gets the
+  // per-tile column sums of gu (fc1's bias gradient), bp2 is not written
+  static_assert(!DGELU || (BNB && !BNR && !STATS && !REMAP && LDSEPI && !SK), "DGELU config");
   constexpr int HROWS = 136;  // halo strip rows: 128 + 2, rounded up to whole 8-row glds instructions
   // HB (HALO): B taps staged per load phase - 1: one per K-step; 3: all three taps of the row
   // with the halo strip, one wait per three K-steps (more LDS: fewer resident blocks)
@@ -707,8 +713,8 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int c = n0 + oc * 8 + k;
-        ba[k] = BNR ? 0.f : p.bn_coef[c];
-        bb[k] = BNR ? 0.f : p.bn_coef[p.Cout + c];
+        ba[k] = (BNR || DGELU) ? 0.f : p.bn_coef[c];
+        bb[k] = (BNR || DGELU) ? 0.f : p.bn_coef[p.Cout + c];
         bm[k] = p.bn_mean[c];
         bm2[k] = two ? p.bn_mean2[c] : 0.f;
         s1[k] = 0.f;
@@ -794,7 +800,9 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
                 const float g = cunpack<F16>(gu[k2], h);
                 const float x = cunpack<F16>(xu[k2], h);
                 float dz;
-                if (BNR) {
+                if (DGELU) {
+                  dz = g * gelu_grad(x + bm[k]);
+                } else if (BNR) {
                   const bool pos = p.bnmask != nullptr ? ((mv[q] >> k) & 1u) != 0u : cunpack<F16>(yu[k2], h) > 0.0f;
                   const float rr = cunpack<F16>(ru[k2], h);
                   dz = pos ? g + rr : 0.0f;
@@ -803,18 +811,18 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
                 }
                 dzp[h] = dz;
                 s1[k] += dz;
-                s2[k] = __builtin_fmaf(dz, x - bm[k], s2[k]);
+                if (!DGELU) s2[k] = __builtin_fmaf(dz, x - bm[k], s2[k]);
                 if (two) {
                   const float x2 = cunpack<F16>(x2u[k2], h);
                   s3[k] = __builtin_fmaf(dz, x2 - bm2[k], s3[k]);
                 }
               }
-              if (BNR) {
+              if (BNR || DGELU) {
                 const f32x2_t d2 = {dzp[0], dzp[1]};
                 du[k2] = cpack<F16>(d2);
               }
             }
-            if (BNR) v = make_uint4(du[0], du[1], du[2], du[3]);
+            if (BNR || DGELU) v = make_uint4(du[0], du[1], du[2], du[3]);
           }
           if (REMAP) {
             const int64_t gr = grow(m);
@@ -845,7 +853,7 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
 #pragma unroll
         for (int off = CPR; off < 64; off <<= 1) {
           s1[k] += __shfl_xor(s1[k], off, 64);
-          s2[k] += __shfl_xor(s2[k], off, 64);
+          if (!DGELU) s2[k] += __shfl_xor(s2[k], off, 64);
           if (two) s3[k] += __shfl_xor(s3[k], off, 64);
         }
       }
@@ -874,11 +882,11 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
         constexpr int SUBB = BM / 128;
         const int64_t pc = (int64_t)(n0 + tid) * p.bp_ld + p.bp_off + (int64_t)mt * SUBB;
         p.bp1[pc] = a;
-        p.bp2[pc] = b;
+        if (!DGELU) p.bp2[pc] = b;
         if (two) p.bp3[pc] = c3;
         if (SUBB == 2 && ((int64_t)mt * 2 + 1) * 128 < p.M) {
           p.bp1[pc + 1] = 0.f;
-          p.bp2[pc + 1] = 0.f;
+          if (!DGELU) p.bp2[pc + 1] = 0.f;
           if (two) p.bp3[pc + 1] = 0.f;
         }
       }
@@ -2546,6 +2554,38 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
     else fwd_launch<128, 64, 1, true, false, false, true>(grid, block, s, a);
   }
 }
+
+// A Linear's backward-data with the exact-GELU backward of its input fused into the epilogue
+// (ViT's fc2 -> GELU -> fc1 chain): gu[t, i] = (sum_o dy[t, o] wt[i, o]) * gelu'(u[t, i] + bias[i])
+// and bp1[i][mt] = the column sums of gu over 128-row tile mt (the bias gradient's partials).
+// dy [T, n_out], wt [n_in, n_out] (the weight transposed), u / gu [T, n_in] 16-bit, bias fp32.
+void launch_linear_dgrad_dgelu(const uint16_t* dy, const uint16_t* wt, const uint16_t* u, const float* bias,
+                               uint16_t* gu, float* bp1, int64_t T, int n_out, int n_in, bool f16, hipStream_t s) {
+  if (n_in % 128 != 0 || n_out % 64 != 0) throw std::runtime_error("linear_dgrad_dgelu: n_in % 128, n_out % 64");
+  ConvFwdArgs a;
+  a.part = nullptr; a.splits = 1; a.kps = 0;
+  a.f16 = f16 ? 1 : 0;
+  a.x = dy; a.w = wt; a.y = gu; a.psum = nullptr; a.psq = nullptr;
+  a.N = 1; a.H = 1; a.W = (int)T; a.C = n_out; a.Cout = n_in; a.R = 1; a.S = 1; a.stride = 1; a.pad = 0;
+  a.Ho = 1; a.Wo = (int)T;
+  a.M = T;
+  a.m_tiles = conv_m_tiles(a.M);
+  a.mt256 = 0;
+  a.n_tiles = n_in / 128;
+  a.bnx = u; a.bn_mean = bias; a.bn_coef = nullptr; a.bp1 = bp1; a.bp2 = nullptr;
+  a.bny = nullptr; a.bnres = nullptr; a.bnmask = nullptr; a.bnx2 = nullptr; a.bn_mean2 = nullptr; a.bp3 = nullptr;
+  a.bp_ld = a.m_tiles; a.bp_off = 0;
+  conv_check_offsets(a, false);
+  const dim3 grid((unsigned)(a.m_tiles * a.n_tiles)), block(conv::kThreads);
+  if (f16)
+    hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, false, false, true, false, false, false, false, true,
+                                        conv::kThreads, false, false, 1, false, true>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, true, false, false, true, false, false, false, false, false,
+                                        conv::kThreads, false, false, 1, false, true>), grid, block, 0, s, a);
+}
+
+int linear_dgrad_dgelu_tiles(int64_t T) { return conv_m_tiles(T); }
 
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int C, int Cout,
                      int R, int S, int stride, int pad, float* psum, float* psq, hipStream_t s, int Ho, int Wo,

@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.vit import (add_bias_layer_norm16, bias_gelu16, layer_norm16, linear16, ln_fusable, merge_heads,
+from ..ops.vit import (add_bias_layer_norm16, gelu_linear16, layer_norm16, linear16, ln_fusable, merge_heads,
                        split_heads)
 from ..ops import attention as fused_attn
 from ..parallel.shadow import shadow_param
@@ -131,8 +131,8 @@ class Encoder(nn.Module):
             x, h2 = add_bias_layer_norm16(x, a, ab, blk.ln_2)
             fc1, fc2 = blk.mlp[0], blk.mlp[3]
             u = linear16(h2, shadow_param(fc1, "weight", h2))
-            g = bias_gelu16(u, shadow_param(fc1, "bias", h2))
-            pending = (linear16(g, shadow_param(fc2, "weight", g)), shadow_param(fc2, "bias", g))
+            z = gelu_linear16(u, shadow_param(fc1, "bias", h2), shadow_param(fc2, "weight", h2))
+            pending = (z, shadow_param(fc2, "bias", h2))
         return add_bias_layer_norm16(x, pending[0], pending[1], self.ln)[1]
 
 

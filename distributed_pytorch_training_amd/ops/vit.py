@@ -256,6 +256,48 @@ class _Linear16(torch.autograd.Function):
         return dx, dw, db
 
 
+# fc2's backward-data and GELU's backward in one launch (conv_fwd_kernel's DGELU epilogue):
+# gu = (dz W2) * gelu'(u + b1) with the bias-gradient column sums, instead of a hipBLASLt GEMM
+# writing gh and a GELU pass re-reading it.  DPT_VIT_FUSED_DGELU=0 keeps the two launches (A/B).
+FUSED_DGELU = os.environ.get("DPT_VIT_FUSED_DGELU", "1") != "0"
+
+
+class _GeluLinear16(torch.autograd.Function):
+    """z = gelu(u + b1) W2^T on 16-bit operands (ViT's MLP after fc1), with the fused backward."""
+
+    @staticmethod
+    def forward(ctx, u, b1, w2):
+        w16 = w2 if w2.dtype == u.dtype else w2.to(u.dtype)
+        h = native().gelu_fwd(u, b1)
+        ctx.save_for_backward(u, b1, h, w16)
+        ctx.w_dtype = w2.dtype
+        return F.linear(h, w16)
+
+    @staticmethod
+    def backward(ctx, gz):
+        u, b1, h, w16 = ctx.saved_tensors
+        n_in, n_out = u.shape[-1], gz.shape[-1]
+        gz2 = gz.reshape(-1, n_out).contiguous()
+        u2 = u.reshape(-1, n_in)
+        dw2 = wgrad_splitk(gz2, h.reshape(-1, n_in), ctx.w_dtype) if ctx.needs_input_grad[2] else None
+        gu = db1 = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            gu, part = native().linear_dgrad_dgelu(gz2, w16.t().contiguous(), u2, b1.float().contiguous())
+            gu = gu.view(u.shape)
+            if ctx.needs_input_grad[1]:
+                db1 = part.sum(1).to(b1.dtype)
+        return gu, db1, dw2
+
+
+def gelu_linear16(u: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
+    """linear16(bias_gelu16(u, b1), w2) with fc2's backward-data and GELU's backward fused."""
+    n_in, n_out = u.shape[-1], w2.shape[0]
+    if (FUSED_DGELU and u.is_cuda and native_available() and u.dtype in _KIND and u.is_contiguous()
+            and b1 is not None and n_in % 128 == 0 and n_out % 64 == 0):
+        return _GeluLinear16.apply(u, b1, w2)
+    return linear16(bias_gelu16(u, b1), w2)
+
+
 def linear16(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
     """F.linear for 16-bit activations (autocast region) with the split-K weight gradient."""
     if x.is_cuda and x.dtype in _KIND and x.is_contiguous():

@@ -195,3 +195,53 @@ def test_linear16_splitk_wgrad(cuda, n_out, n_in, bias):
     _close(x.grad, xr.grad, 1e-2, 1e-2, "dx")
     if bias:
         _close(b.grad, br.grad, 1e-3, 1e-1, "db")
+
+
+@pytest.mark.parametrize("T", [2 * 197, 1000])
+def test_linear_dgrad_dgelu_matches_fp32(cuda, T):
+    """fc2's backward-data with GELU's backward fused (conv_fwd_kernel DGELU epilogue) against fp32:
+    gu = (dz W2) * gelu'(u + b1), and the per-tile column sums that make fc1's bias gradient.
+    T = 1000 leaves a partial last 128-row tile."""
+    from distributed_pytorch_training_amd.ops import native
+    torch.manual_seed(4)
+    n_in, n_out = 3072, 768
+    u = (torch.randn(T, n_in, device=cuda) * 2).to(torch.bfloat16)
+    b = torch.randn(n_in, device=cuda) * 0.5
+    w = (torch.randn(n_out, n_in, device=cuda) / n_in ** 0.5).to(torch.bfloat16)
+    dz = torch.randn(T, n_out, device=cuda).to(torch.bfloat16)
+    gu, part = native().linear_dgrad_dgelu(dz, w.t().contiguous(), u, b)
+    assert part.shape == (n_in, (T + 127) // 128)
+    # the kernel rounds g = dz W2 to bf16 before the GELU derivative, as the unfused path's GEMM
+    # output does: the reference does too (otherwise the column sums of T values carry
+    # sqrt(T) bf16 roundings of difference)
+    gh = (dz.float() @ w.float()).to(torch.bfloat16).float()
+    ur = (u.float() + b).requires_grad_(True)
+    F.gelu(ur).backward(gh)
+    _close(gu, ur.grad, 2e-2, 2e-2, "gu")
+    _close(part.sum(1), ur.grad.sum(0), 1e-2, 5e-2, "dbias")
+
+
+def test_gelu_linear16_fused_matches_unfused(cuda):
+    """The fused MLP tail (gelu_linear16) against the two-launch composition it replaces: same
+    forward bits, gradients within the bf16 rounding of gh."""
+    from distributed_pytorch_training_amd.ops import vit as vops
+    torch.manual_seed(5)
+    T, n_in, n_out = 4 * 197, 3072, 768
+    u0 = (torch.randn(T, n_in, device=cuda) * 2).to(torch.bfloat16)
+    b0 = (torch.randn(n_in, device=cuda) * 0.5).to(torch.bfloat16)
+    w0 = (torch.randn(n_out, n_in, device=cuda) / n_in ** 0.5)
+    gz = torch.randn(T, n_out, device=cuda).to(torch.bfloat16)
+    outs = {}
+    for fused in (True, False):
+        u, b, w = (t.clone().requires_grad_(True) for t in (u0, b0, w0))
+        old = vops.FUSED_DGELU
+        vops.FUSED_DGELU = fused
+        try:
+            z = vops.gelu_linear16(u, b, w)
+            z.backward(gz)
+        finally:
+            vops.FUSED_DGELU = old
+        outs[fused] = (z.detach(), u.grad, b.grad, w.grad)
+    assert torch.equal(outs[True][0], outs[False][0])
+    for name, a, r in zip(("du", "db", "dw"), outs[True][1:], outs[False][1:]):
+        _close(a, r, 2e-2, 5e-2, name)
