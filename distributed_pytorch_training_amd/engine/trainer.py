@@ -96,6 +96,8 @@ class Trainer:
         if getattr(args, "native_conv_fp32", False):
             from ..ops import conv_f32
             conv_f32.ENABLED = True          # process-wide: fp32 convs on the MFMA kernels
+        from ..models.vit import set_native as vit_set_native
+        vit_set_native(model, self.device.type == "cuda")   # fused ViT encoder (no-op for other models)
         gpu_cl = self.device.type == "cuda" and bool(getattr(args, "channels_last", False))
         # MFMA convs need channels_last bf16/fp16 activations; routing is per model
         use_native_conv = gpu_cl and bool(getattr(args, "native_conv", True)) and native_conv.ENABLED

@@ -35,6 +35,10 @@ from ..parallel.shadow import shadow_param
 
 class SelfAttention(nn.Module):
     dpt_shadow_names = ("in_proj_weight", "in_proj_bias")  # 16-bit weight shadows (parallel/shadow.py)
+    # False: stock PyTorch ops (F.linear, scaled_dot_product_attention) - what torchvision's
+    # nn.MultiheadAttention runs, and what the stock engine (--impl torch) must measure.  The
+    # native engine turns it on (set_native): split-K linear backward, the gfx950 attention kernels.
+    dpt_native = False
 
     def __init__(self, dim: int, heads: int, dropout: float = 0.0) -> None:
         super().__init__()
@@ -48,6 +52,11 @@ class SelfAttention(nn.Module):
 
     def _context(self, x: torch.Tensor) -> torch.Tensor:
         b, s, d = x.shape
+        if not self.dpt_native:
+            qkv = F.linear(x, self.in_proj_weight, self.in_proj_bias)
+            q, k, v = qkv.view(b, s, 3, self.heads, d // self.heads).permute(2, 0, 3, 1, 4).unbind(0)
+            y = F.scaled_dot_product_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0)
+            return y.transpose(1, 2).reshape(b, s, d)
         qkv = linear16(x, shadow_param(self, "in_proj_weight", x), shadow_param(self, "in_proj_bias", x))
         if (not self.training or self.dropout == 0.0) and fused_attn.supported(qkv, self.heads):
             return fused_attn.attention(qkv, self.heads)  # heads split/merged inside the kernels
@@ -92,6 +101,8 @@ class EncoderBlock(nn.Module):
 
 
 class Encoder(nn.Module):
+    dpt_native = False   # the fused encoder path (set_native); stock module-by-module otherwise
+
     def __init__(self, seq_len: int, layers: int, heads: int, dim: int, mlp_dim: int,
                  dropout: float, attn_dropout: float) -> None:
         super().__init__()
@@ -108,6 +119,8 @@ class Encoder(nn.Module):
         return self.ln(self.layers(self.dropout(x + self.pos_embedding)))
 
     def _fused_ok(self, x: torch.Tensor) -> bool:
+        if not self.dpt_native:
+            return False
         if not (x.is_cuda and torch.is_autocast_enabled("cuda")
                 and torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16)):
             return False
@@ -162,6 +175,17 @@ class VisionTransformer(nn.Module):
         x = torch.cat([self.class_token.expand(n, -1, -1), x], dim=1)
         x = self.encoder(x)
         return self.heads(x[:, 0])
+
+
+def set_native(model: nn.Module, on: bool = True) -> int:
+    """Route a ViT's encoder through the native fused path (on) or stock PyTorch ops (off, the
+    default of a freshly built model); returns how many modules were switched."""
+    n = 0
+    for m in model.modules():
+        if isinstance(m, (SelfAttention, Encoder)):
+            m.dpt_native = bool(on)
+            n += 1
+    return n
 
 
 def vit_b_16(num_classes: int = 1000, image_size: int = 224, **kw) -> VisionTransformer:

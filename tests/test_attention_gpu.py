@@ -36,7 +36,10 @@ def test_attention_fwd_bwd_matches_fp32(cuda, B, S, H):
 def test_vit_uses_fused_attention(cuda):
     from distributed_pytorch_training_amd.models import build_model
 
+    from distributed_pytorch_training_amd.models.vit import set_native
+
     m = build_model("vit_b_16", 10, cuda, image_size=32).train()
+    assert set_native(m) > 0
     x = torch.randn(2, 3, 32, 32, device=cuda)
     with torch.autocast("cuda", dtype=torch.bfloat16):
         y1 = m(x)

@@ -119,7 +119,11 @@ def test_vit_fused_encoder_matches_unfused(cuda):
             Encoder._fused_ok = orig
         return loss.detach(), {n: p.grad.detach().float().clone() for n, p in model.named_parameters()}
 
+    from distributed_pytorch_training_amd.models.vit import set_native
+
     fused_m, unf_m, ref_m = (copy.deepcopy(base) for _ in range(3))
+    set_native(fused_m)
+    set_native(unf_m)      # native module-by-module (the fused encoder switched off below)
     lf, gf = run(fused_m, True, True)
     lu, gu = run(unf_m, True, False)
     lr, gr = run(ref_m, False, False)
