@@ -26,6 +26,8 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tokens", type=int, default=128 * 197)
+    ap.add_argument("--targets", default="", help="comma list of conv_set_wgrad_target block counts to time "
+                                                  "the native kernel at (0 = the shipped policy)")
     a = ap.parse_args(argv)
     from distributed_pytorch_training_amd.ops import native
     from distributed_pytorch_training_amd.ops.vit import wgrad_splitk
@@ -42,11 +44,14 @@ def main(argv=None):
         dy4 = dy.view(1, 1, T, n_out).permute(0, 3, 1, 2)   # [1, n_out, 1, T] channels_last view
         x4 = x.view(1, 1, T, n_in).permute(0, 3, 1, 2)
         assert dy4.is_contiguous(memory_format=torch.channels_last)
-        fns = {"splitk_hipblaslt": lambda: wgrad_splitk(dy, x, torch.float32),
-               "native_conv_wgrad": lambda: C.conv_wgrad(dy4, x4, [n_out, n_in, 1, 1], 1, 0, True)}
+        fns = {"splitk_hipblaslt": (0, lambda: wgrad_splitk(dy, x, torch.float32)),
+               "native_conv_wgrad": (0, lambda: C.conv_wgrad(dy4, x4, [n_out, n_in, 1, 1], 1, 0, True))}
+        for t in [int(v) for v in a.targets.split(",") if v.strip()]:
+            fns[f"native_target{t}"] = (t, lambda: C.conv_wgrad(dy4, x4, [n_out, n_in, 1, 1], 1, 0, True))
         res = {}
         outs = {}
-        for name, fn in fns.items():
+        for name, (target, fn) in fns.items():
+            C.conv_set_wgrad_target(target)
             outs[name] = fn().reshape(n_out, n_in).float()
             torch.cuda.synchronize()
             ts = []
@@ -59,6 +64,7 @@ def main(argv=None):
                 torch.cuda.synchronize()
                 ts.append(e0.elapsed_time(e1) * 1000 / a.reps)
             res[name] = statistics.median(ts)
+            C.conv_set_wgrad_target(0)
         ref = (dy[:, :256].double().t() @ x[:, :256].double())
         err = {k: ((v[:256, :256].double() - ref).norm() / ref.norm()).item() for k, v in outs.items()}
         flop = 2.0 * T * n_out * n_in

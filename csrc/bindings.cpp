@@ -528,7 +528,7 @@ std::vector<Tensor> conv_dgrad_flip(Tensor dy, Tensor w, int64_t pad, PendingRed
 // dw = conv2d backward-weight (fp32 or bf16 output, KRSC = channels_last [Cout, C, R, S]).
 // pending != nullptr: a split-K reduce is left for a backward-data launch (conv_wgrad_deferred).
 Tensor conv_wgrad_impl(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stride, int64_t pad, bool fp32_out,
-                       PendingReduce* pending) {
+                       PendingReduce* pending, int64_t target_blocks = 0) {
   check_cl_bf16(dy, "grad_output");
   check_cl_bf16(x, "x");
   same_16(dy, x, "conv_wgrad");
@@ -542,7 +542,8 @@ Tensor conv_wgrad_impl(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t
   TORCH_CHECK(dy.size(2) >= 1 && dy.size(2) <= Hs && dy.size(3) >= 1 && dy.size(3) <= Ws,
               "conv_wgrad: grad_output spatial mismatch");
   // the output size comes from dy (covers asymmetric padding)
-  auto pl = dpt::conv_wgrad_plan(N, H, W, C, Cout, R, S, (int)stride, (int)pad, (int)dy.size(2), (int)dy.size(3));
+  auto pl = dpt::conv_wgrad_plan(N, H, W, C, Cout, R, S, (int)stride, (int)pad, (int)dy.size(2), (int)dy.size(3),
+                                 (int)target_blocks);
   TORCH_CHECK((int64_t)N * pl.Ho * pl.Wo < (1ll << 31), "conv_wgrad: too many pixels");
   auto dw = at::empty({Cout, C, R, S}, x.options().dtype(fp32_out ? at::kFloat : x.scalar_type())
                                           .memory_format(at::MemoryFormat::ChannelsLast));
@@ -559,8 +560,9 @@ Tensor conv_wgrad_impl(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t
   return dw;
 }
 
-Tensor conv_wgrad(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stride, int64_t pad, bool fp32_out) {
-  return conv_wgrad_impl(dy, x, wshape, stride, pad, fp32_out, nullptr);
+Tensor conv_wgrad(Tensor dy, Tensor x, std::vector<int64_t> wshape, int64_t stride, int64_t pad, bool fp32_out,
+                  int64_t target_blocks) {
+  return conv_wgrad_impl(dy, x, wshape, stride, pad, fp32_out, nullptr, target_blocks);
 }
 
 // (dw, pending): the backward-weight kernel is launched, its split-K reduce (if the plan needs
@@ -1248,7 +1250,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_h") = 0, py::arg("out_w") = 0);
   m.def("space_to_depth2", &space_to_depth2, py::arg("x"), py::arg("out_f16") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("grad_output"), py::arg("x"), py::arg("weight_shape"), py::arg("stride"),
-        py::arg("pad"), py::arg("fp32_out"));
+        py::arg("pad"), py::arg("fp32_out"), py::arg("target_blocks") = 0);
   m.def("conv_f32_fwd", &conv_f32_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"));
   m.def("conv_f32_dgrad", &conv_f32_dgrad, py::arg("grad_output"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("H"), py::arg("W"));

@@ -2755,7 +2755,7 @@ static int wgrad_target(int R, int S, int stride, int steps) {
 }
 
 ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad, int Ho,
-                              int Wo) {
+                              int Wo, int target_blocks) {
   ConvWgradPlan pl;
   pl.Ho = Ho > 0 ? Ho : (H + 2 * pad - R) / stride + 1;
   pl.Wo = Wo > 0 ? Wo : (W + 2 * pad - S) / stride + 1;
@@ -2794,7 +2794,7 @@ ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S
   // (BMW x BNW x 4 B, written once and read once by the reduce) then costs < 1/8 of the
   // operand bytes it streams.  Small problems that cannot fill the chip that way (ResNet-18 on
   // 32x32 images: 2-128 K-steps) are K-loop-latency-bound instead: down to 2 K-steps per split.
-  int splits = (wgrad_target(R, S, stride, steps) + tiles - 1) / tiles;
+  int splits = ((target_blocks > 0 ? target_blocks : wgrad_target(R, S, stride, steps)) + tiles - 1) / tiles;
   const int min_steps = (int64_t)tiles * (steps / 32) >= 512 ? 32 : 2;
   splits = std::max(1, std::min(splits, steps / min_steps));
   pl.steps_per_split = (steps + splits - 1) / splits;

@@ -189,8 +189,10 @@ struct ConvWgradPlan {
   int halo = 0;  // 3x3 / stride-1: the three taps of a tap row share one x strip (conv_wgrad_halo_kernel)
 };
 void conv_set_wgrad_halo(int mode);  // 0 off, 1-4 forced, 5 auto (default, DPT_WGRAD_HALO)
+// target_blocks > 0: the split-K block target for this call (ViT's long-K linears want 768,
+// profiles/vit_wgrad_ab_r5.md); 0: the shape policy (wgrad_target) or conv_set_wgrad_target
 ConvWgradPlan conv_wgrad_plan(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad, int Ho = 0,
-                              int Wo = 0);
+                              int Wo = 0, int target_blocks = 0);
 // The split-K reduce of a backward-weight (partials [splits][n4 float4s] -> out, kind as dw_kind).
 struct WgradReduce {
   const float* part;

@@ -193,10 +193,13 @@ def _wgrad_splits(n_out: int, n_in: int, T: int) -> int:
 
 # dW = dY^T X on the native MFMA backward-weight kernel of the 1x1 convolutions (a [1, 1, T, C]
 # channels-last "image"; split-K with fp32 partials and a fixed-order reduce, deterministic) for
-# inputs up to this many features; hipBLASLt's split-K batched GEMM above it.  ViT-B/16 at
-# batch 128 (bench/vit_wgrad_ab.py, profiles/vit_wgrad_ab_r5.md): qkv 126 vs 138 us, proj 53 vs
-# 64, fc1 150 vs 153 - but fc2 (3,072 inputs) 155 vs 141.  0 disables.
+# inputs up to this many features; hipBLASLt's split-K batched GEMM above it.  ViT-B/16 at batch
+# 128 (bench/vit_wgrad_ab.py, profiles/vit_wgrad_ab_r5.md): qkv 126 vs 138 us, proj 53 vs 64, fc1
+# 150 vs 153, fc2 155 vs 141; step 23.65 vs 23.88 ms.  0 disables.  NATIVE_WGRAD_BLOCKS > 0 aims
+# the split-K at that many blocks instead of the 1x1-conv policy's 512: 768 is 2-15 % faster per
+# product in isolation but level in the step (profiles/vit_wgrad_ab_r5.md), so it stays 0.
 NATIVE_WGRAD_MAX_IN = int(os.environ.get("DPT_VIT_NATIVE_WGRAD_MAX_IN", "1024"))
+NATIVE_WGRAD_BLOCKS = 0
 
 
 def _native_wgrad_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
@@ -214,7 +217,8 @@ def wgrad_splitk(dy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype) -> t
         dy4 = dy.view(1, 1, T, n_out).permute(0, 3, 1, 2)      # [1, n_out, 1, T], channels_last
         x4 = x.view(1, 1, T, n_in).permute(0, 3, 1, 2)
         if dy4.is_contiguous(memory_format=cl) and x4.is_contiguous(memory_format=cl):
-            dw = native().conv_wgrad(dy4, x4, [n_out, n_in, 1, 1], 1, 0, out_dtype == torch.float32)
+            dw = native().conv_wgrad(dy4, x4, [n_out, n_in, 1, 1], 1, 0, out_dtype == torch.float32,
+                                     NATIVE_WGRAD_BLOCKS)
             return dw.view(n_out, n_in)
     s = _wgrad_splits(n_out, n_in, T)
     if s == 1:
