@@ -240,12 +240,21 @@ __global__ __launch_bounds__(NT * 64, PHASE == 1 ? DPT_ATTN_P1_WAVES : PHASE == 
         sc = mfma32(row_frag<RB>(qimg, qt * 32 + r, 2 * s + h), kf[s], sc);   // S = Q K^T
         dp = mfma32(row_frag<RB>(oimg, qt * 32 + r, 2 * s + h), vf[s], dp);   // dP = dO V^T
       }
+      // rows = queries, column = this lane's key: rows (e & 3) of group e >> 2 are 4 consecutive
+      // queries, so their lse2 / D values come in one 16-byte LDS read each (8 reads, not 32)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {  // rows = queries, column = this lane's key
-        const int qq = qt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const float pv = key < S ? attn_exp2(__builtin_fmaf(sc[e], scale_log2, -ls[qq])) : 0.f;
-        sc[e] = pv;
-        dp[e] = pv * (dp[e] - dd[qq]);
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const int q4 = qt * 32 + 8 * e4 + 4 * h;
+        const float4 l4 = *reinterpret_cast<const float4*>(ls + q4);
+        const float4 d4 = *reinterpret_cast<const float4*>(dd + q4);
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int e = 4 * e4 + j;
+          const float pv = key < S ? attn_exp2(__builtin_fmaf(sc[e], scale_log2, -lv[j])) : 0.f;
+          sc[e] = pv;
+          dp[e] = pv * (dp[e] - dv4[j]);
+        }
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
