@@ -1236,6 +1236,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_fwd", &gelu_fwd, py::arg("u"), py::arg("bias"));
   m.def("gelu_bwd", &gelu_bwd, py::arg("grad"), py::arg("u"), py::arg("bias"), py::arg("want_dbias"));
   m.def("linear_dgrad_dgelu", &linear_dgrad_dgelu, py::arg("grad"), py::arg("wt"), py::arg("u"), py::arg("bias"));
+  m.def("vit_set_gelu_blocks_per_cu", &dpt::vit_set_gelu_blocks_per_cu, py::arg("n"));
   m.def("copy_rows16", &copy_rows16, py::arg("src"), py::arg("dst"));
   m.def("bias_grad16", &bias_grad16, py::arg("grad"), py::arg("out_kind"));
   m.def("sum_partials", &sum_partials, py::arg("part"), py::arg("out_kind"));

@@ -122,6 +122,7 @@ void launch_gather(const GatherBatch& batch, bool accumulate, hipStream_t s);
 bool ln_supported(int64_t D);
 int ln_bwd_blocks(int64_t T);
 int gelu_bwd_chunks(int64_t T, int64_t F);
+void vit_set_gelu_blocks_per_cu(int n);  // A/B: 2-wave blocks per CU of the GELU passes (default 6)
 void launch_ln_fwd(int kind, const float* x, const uint16_t* a, const void* bias, int bias_kind, const float* gamma,
                    const float* beta, float* s_out, uint16_t* h_out, float* mean, float* rstd, int64_t T, int64_t D,
                    float eps, hipStream_t s);

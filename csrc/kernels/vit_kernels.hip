@@ -499,17 +499,34 @@ void launch_ln_bwd(int kind, const float* gs, const uint16_t* gh, const float* s
     launch_colsum(part, nb, D, db ? 3 : 2, dgamma, 0, dbeta, 0, db, dbias_kind, s);
 }
 
-int gelu_bwd_chunks(int64_t T, int64_t F) {
-  // ~12 waves per CU in total: (F/8/128 column blocks) x chunks of 2-wave blocks.
+// 2-wave blocks per CU of the GELU passes (bench/gelu_ab.py, ViT-B/16's [25216, 3072] at batch
+// 128): the forward 73 -> 58 us going 6 -> 12 per CU (more 16-byte rows in flight), the backward
+// best at 8 (105 vs 113 us; its per-chunk column-sum partials grow with the chunk count).
+// A/B knob: vit_set_gelu_blocks_per_cu (0 = these defaults).
+constexpr int kGeluFwdBlocksPerCu = 12, kGeluBwdBlocksPerCu = 8;
+static int g_gelu_blocks_per_cu = 0;
+void vit_set_gelu_blocks_per_cu(int n) { g_gelu_blocks_per_cu = n > 0 ? n : 0; }
+
+static int gelu_chunks(int64_t T, int64_t F, int blocks_per_cu) {
   const int64_t colblocks = (F / 8 + 127) / 128;
-  int64_t c = (256 * 6) / (colblocks > 0 ? colblocks : 1);
+  const int per_cu = g_gelu_blocks_per_cu > 0 ? g_gelu_blocks_per_cu : blocks_per_cu;
+  int64_t c = (256 * (int64_t)per_cu) / (colblocks > 0 ? colblocks : 1);
+  if (c > T / 8) c = T / 8;
+  return (int)(c < 1 ? 1 : c);
+}
+
+int gelu_bwd_chunks(int64_t T, int64_t F) {
+  // (F/8/128 column blocks) x chunks of 2-wave blocks
+  const int64_t colblocks = (F / 8 + 127) / 128;
+  int64_t c = (256 * (int64_t)(g_gelu_blocks_per_cu > 0 ? g_gelu_blocks_per_cu : kGeluBwdBlocksPerCu)) /
+              (colblocks > 0 ? colblocks : 1);
   if (c > T / 8) c = T / 8;
   return (int)(c < 1 ? 1 : c);
 }
 
 void launch_gelu_fwd(int kind, const uint16_t* u, const void* bias, int bias_kind, uint16_t* h, int64_t T, int64_t F,
                      hipStream_t s) {
-  const int chunks = gelu_bwd_chunks(T, F);
+  const int chunks = gelu_chunks(T, F, kGeluFwdBlocksPerCu);
   const int64_t rpc = (T + chunks - 1) / chunks;
   dim3 gr((unsigned)((F / 8 + 127) / 128), (unsigned)chunks), bl(128);
   if (kind == 1) hipLaunchKernelGGL(gelu_fwd_kernel<1>, gr, bl, 0, s, u, bias, bias_kind, h, T, (int)F, rpc);
