@@ -201,24 +201,24 @@ def test_linear16_splitk_wgrad(cuda, n_out, n_in, bias):
         _close(b.grad, br.grad, 1e-3, 1e-1, "db")
 
 
-@pytest.mark.parametrize("T", [2 * 197, 1000])
-def test_linear_dgrad_dgelu_matches_fp32(cuda, T):
+@pytest.mark.parametrize("T,dt", [(2 * 197, torch.bfloat16), (1000, torch.bfloat16), (2 * 197, torch.float16)])
+def test_linear_dgrad_dgelu_matches_fp32(cuda, T, dt):
     """fc2's backward-data with GELU's backward fused (conv_fwd_kernel DGELU epilogue) against fp32:
     gu = (dz W2) * gelu'(u + b1), and the per-tile column sums that make fc1's bias gradient.
     T = 1000 leaves a partial last 128-row tile."""
     from distributed_pytorch_training_amd.ops import native
     torch.manual_seed(4)
     n_in, n_out = 3072, 768
-    u = (torch.randn(T, n_in, device=cuda) * 2).to(torch.bfloat16)
+    u = (torch.randn(T, n_in, device=cuda) * 2).to(dt)
     b = torch.randn(n_in, device=cuda) * 0.5
-    w = (torch.randn(n_out, n_in, device=cuda) / n_in ** 0.5).to(torch.bfloat16)
-    dz = torch.randn(T, n_out, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(n_out, n_in, device=cuda) / n_in ** 0.5).to(dt)
+    dz = torch.randn(T, n_out, device=cuda).to(dt)
     gu, part = native().linear_dgrad_dgelu(dz, w.t().contiguous(), u, b)
     assert part.shape == (n_in, (T + 127) // 128)
     # the kernel rounds g = dz W2 to bf16 before the GELU derivative, as the unfused path's GEMM
     # output does: the reference does too (otherwise the column sums of T values carry
     # sqrt(T) bf16 roundings of difference)
-    gh = (dz.float() @ w.float()).to(torch.bfloat16).float()
+    gh = (dz.float() @ w.float()).to(dt).float()
     ur = (u.float() + b).requires_grad_(True)
     F.gelu(ur).backward(gh)
     _close(gu, ur.grad, 2e-2, 2e-2, "gu")
