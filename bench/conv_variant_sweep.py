@@ -2,10 +2,11 @@
 
 For each shape: MIOpen's forward (cudnn.benchmark off: immediate mode, as conv_bench.py), then
 every conv_fwd_kernel tiling the dispatcher can launch - 4 (128x128, default), 5/6 (256-row
-blocks), 9..13 (8-wave 256x256 / 256x128 / 128x256, 2- and 3-stage) - with and without the
-BN-statistics epilogue the training step uses.  Mean of 20 timed repeats per cell (conv_roofline.time_ms).
+blocks), 9..13 (8-wave 256x256 / 256x128 / 128x256, 2- and 3-stage), 7 / 8 / 14 (BK = 32
+pipelined K loop, 3 / 4 / 2 stages) - with and without the BN-statistics epilogue the training
+step uses.  Mean of 20 timed repeats per cell (conv_roofline.time_ms).
 
-    python bench/conv_variant_sweep.py [--batch 256] [--all]
+    python bench/conv_variant_sweep.py [--batch 256] [--all | --small-1x1] [--variants 4,14,7]
 """
 from __future__ import annotations
 
@@ -27,7 +28,11 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--all", action="store_true", help="every ResNet-50 shape, not just the four behind MIOpen")
+    ap.add_argument("--small-1x1", action="store_true",
+                    help="the stride-1 1x1 shapes whose 128 x 128 grid is under 1,024 tiles")
+    ap.add_argument("--variants", default=",".join(map(str, VARIANTS)))
     a = ap.parse_args(argv)
+    variants = [int(v) for v in a.variants.split(",")]
     from distributed_pytorch_training_amd import ops
     from distributed_pytorch_training_amd.utils.env import setup_miopen_env
 
@@ -37,20 +42,24 @@ def main(argv=None):
     dev = torch.device("cuda")
     cl = torch.channels_last
     print(f"# forward tile variants vs MIOpen, ResNet-50 batch {a.batch}, bf16 channels_last (ms; +s = with BN statistics)\n")
-    print("| conv | MIOpen | " + " | ".join(f"v{v} / +s" for v in VARIANTS) + " | best+s vs MIOpen |")
-    print("|---|---|" + "---|" * len(VARIANTS) + "---|")
+    print("| conv | MIOpen | " + " | ".join(f"v{v} / +s" for v in variants) + " | best+s vs MIOpen |")
+    print("|---|---|" + "---|" * len(variants) + "---|")
     for (cin_hw, cout, k, s, p), count in resnet50_convs(a.batch, 224).items():
         cin, h, w = cin_hw
         if cin % 64 or cout % 64:
             continue
-        if not a.all and (cin, h, cout, k[0], s[0]) not in BEHIND:
+        if a.small_1x1:
+            tiles = -(-a.batch * h * w // 128) * (cout // (128 if cout % 128 == 0 else 64))
+            if k[0] != 1 or s[0] != 1 or tiles >= 1024:
+                continue
+        elif not a.all and (cin, h, cout, k[0], s[0]) not in BEHIND:
             continue
         x = torch.randn(a.batch, cin, h, w, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
         wt = (torch.randn(cout, cin, *k, device=dev, dtype=torch.bfloat16) * 0.05).contiguous(memory_format=cl)
         ref = F.conv2d(x.float(), wt.float(), stride=s, padding=p)
         t_m = time_ms(lambda: F.conv2d(x, wt, stride=s, padding=p))
         cells, best = [], None
-        for v in VARIANTS:
+        for v in variants:
             C_.conv_set_variant(v)
             out = C_.conv_fwd(x, wt, s[0], p[0], False)
             y = out[0] if isinstance(out, (tuple, list)) else out

@@ -2374,9 +2374,12 @@ static void conv_fwd_dispatch(int variant, bool bkn, ConvFwdArgs a, hipStream_t 
   }
   const dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
   const int nk32 = a.R * a.S * (a.C / 32);
-  if (!bkn && (variant == 7 || variant == 8)) {
+  if (!bkn && (variant == 7 || variant == 8 || variant == 14)) {
     const bool st = a.psum != nullptr;
-    if (variant == 7) {
+    if (variant == 14) {  // 2-stage BK = 32 ring: the same 32 KiB of operand LDS as the 1-stage tile
+      if (st) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN, 2, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN, 2, false>), grid, block, 0, s, a);
+    } else if (variant == 7) {
       if (st) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN, 3, true>), grid, block, 0, s, a);
       else hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN, 3, false>), grid, block, 0, s, a);
     } else {
@@ -2440,6 +2443,10 @@ static bool conv_fwd_big(int v, ConvFwdArgs& a, hipStream_t s) {
 //      0.106 without; bench/conv_variant_sweep.py, profiles/conv_variant_sweep_r4.md);
 //   2: the 3x3 stride-2 256->256 conv (K = 2304, M >= 32768) -> the 8-wave 256x256 tile (variant
 //      9): 0.081 -> 0.069 ms, 1.05-1.08x MIOpen.
+//   4 / 8: 1x1 stride-1 convs with the statistics epilogue on grids under 1,024 tiles (the deep
+//      reducing convs at 14x14 / 7x7, latency-bound with ~3 resident blocks per CU:
+//      profiles/step_pmc_r5.md) -> the BK = 32 pipelined K loop, 2 stages (variant 14, 4 blocks
+//      per CU) / 3 stages (variant 7).
 static int g_fwd_shape_policy = 0;
 void conv_set_fwd_shape_policy(int bits) { g_fwd_shape_policy = bits; }
 static int fwd_shape_variant(const ConvFwdArgs& a, bool stats) {
@@ -2449,6 +2456,9 @@ static int fwd_shape_variant(const ConvFwdArgs& a, bool stats) {
     return 6;
   if ((g_fwd_shape_policy & 2) && a.R == 3 && a.stride == 2 && a.Cout == 256 && a.C == 256 && a.M >= 32768)
     return 9;
+  if ((g_fwd_shape_policy & 12) && stats && a.R == 1 && a.S == 1 && a.stride == 1 && a.C % 32 == 0 &&
+      (int64_t)a.m_tiles * a.n_tiles < 1024)
+    return (g_fwd_shape_policy & 4) ? 14 : 7;
   return 0;
 }
 

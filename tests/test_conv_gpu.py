@@ -30,9 +30,9 @@ def _operands(cuda, N, C, H, W, Cout, k, seed=0):
     return x, w.contiguous(memory_format=CL)
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8],
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 14],
                 ids=["2stage-ldsepi", "2stage-regepi", "1stage-regepi", "1stage-ldsepi", "bm256-regepi",
-                     "bm256-ldsepi", "pipe3", "pipe4"])
+                     "bm256-ldsepi", "pipe3", "pipe4", "pipe2"])
 def variant(request):
     ops.native().conv_set_variant(request.param)
     yield request.param
