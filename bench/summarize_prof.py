@@ -20,6 +20,7 @@ FAMILIES = [
     ("native: MFMA convolutions (fwd/dgrad/wgrad + reduce/flip)", r"dpt::conv_"),
     ("native: fused BatchNorm(+add)(+ReLU)", r"dpt::bn_"),
     ("native: ViT block kernels", r"dpt::(ln_|gelu|rows_copy|colsum|sum_partials)"),
+    ("native: flash attention (fwd / bwd phases)", r"dpt::attn"),
     ("native: metrics/augment/comm/pool kernels", r"dpt::"),
     ("RCCL", r"nccl|rccl|AllReduce|Broadcast"),
     ("conv (MIOpen/CK igemm, xdlops)", r"igemm|Conv|conv|xdlops|gridwise_gemm|DeviceGroupedConv|naive_conv|ImplicitGemm|kernel_grouped_conv"),

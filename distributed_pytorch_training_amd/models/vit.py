@@ -21,6 +21,7 @@ MI355X notes
 from __future__ import annotations
 
 import math
+import os
 from collections import OrderedDict
 
 import torch
@@ -39,6 +40,7 @@ class SelfAttention(nn.Module):
     # nn.MultiheadAttention runs, and what the stock engine (--impl torch) must measure.  The
     # native engine turns it on (set_native): split-K linear backward, the gfx950 attention kernels.
     dpt_native = False
+    native_patch = os.environ.get("DPT_VIT_NATIVE_PATCH", "1") != "0"   # A/B knob
 
     def __init__(self, dim: int, heads: int, dropout: float = 0.0) -> None:
         super().__init__()
@@ -150,6 +152,14 @@ class Encoder(nn.Module):
 
 
 class VisionTransformer(nn.Module):
+    # native path (set_native): the patch embedding as one GEMM over the patch rows.  The conv
+    # has stride == kernel, so its im2col is a pure reshape; MIOpen runs it as an implicit-GEMM
+    # conv in both directions (~0.29 ms per B128 step, plus a find-mode search over naive
+    # solvers on the first step); here a patch copy, a hipBLASLt forward GEMM and the native
+    # split-K weight gradient of linear16.
+    dpt_native = False
+    native_patch = os.environ.get("DPT_VIT_NATIVE_PATCH", "1") != "0"   # A/B knob
+
     def __init__(self, image_size: int = 224, patch_size: int = 16, layers: int = 12,
                  heads: int = 12, dim: int = 768, mlp_dim: int = 3072, num_classes: int = 1000,
                  dropout: float = 0.0, attn_dropout: float = 0.0) -> None:
@@ -169,9 +179,24 @@ class VisionTransformer(nn.Module):
         nn.init.zeros_(self.heads.head.weight)
         nn.init.zeros_(self.heads.head.bias)
 
+    def patch_embed(self, x: torch.Tensor) -> torch.Tensor:
+        """[N, 3, H, W] images -> [N, patches, dim] tokens (conv_proj's output, row-major)."""
+        if not (self.dpt_native and self.native_patch):
+            return self.conv_proj(x).flatten(2).transpose(1, 2)
+        n, c, hh, ww = x.shape
+        p = self.patch_size
+        if torch.is_autocast_enabled(x.device.type):
+            x = x.to(torch.get_autocast_dtype(x.device.type))   # cast before the patch copy
+        rows = (x.reshape(n, c, hh // p, p, ww // p, p).permute(0, 2, 4, 1, 3, 5)
+                .reshape(n * (hh // p) * (ww // p), c * p * p))    # (c, kh, kw): the weight's order
+        w = shadow_param(self.conv_proj, "weight", rows)
+        # linear16: split-K / native weight gradient (K = patch rows, 25,088 at B128)
+        y = linear16(rows, w.reshape(self.dim, -1), shadow_param(self.conv_proj, "bias", rows))
+        return y.view(n, (hh // p) * (ww // p), self.dim)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         n = x.shape[0]
-        x = self.conv_proj(x).flatten(2).transpose(1, 2)          # [N, 196, 768]
+        x = self.patch_embed(x)                                    # [N, 196, 768]
         x = torch.cat([self.class_token.expand(n, -1, -1), x], dim=1)
         x = self.encoder(x)
         return self.heads(x[:, 0])
@@ -182,7 +207,7 @@ def set_native(model: nn.Module, on: bool = True) -> int:
     default of a freshly built model); returns how many modules were switched."""
     n = 0
     for m in model.modules():
-        if isinstance(m, (SelfAttention, Encoder)):
+        if isinstance(m, (SelfAttention, Encoder, VisionTransformer)):
             m.dpt_native = bool(on)
             n += 1
     return n

@@ -44,3 +44,28 @@ def test_wgrad_split_choice():
     assert _wgrad_splits(768, 768, T) == 16
     assert _wgrad_splits(768, 768, 1000) == 1          # too few rows per split
     assert _wgrad_splits(768, 768, 197 * 3) == 1       # odd token count: no even split
+
+
+def test_native_patch_embed_matches_conv():
+    """set_native's patch embedding (patch rows x one GEMM) against conv_proj: values and the
+    conv weight / bias gradients."""
+    from distributed_pytorch_training_amd.models import build_model
+    from distributed_pytorch_training_amd.models.vit import set_native
+
+    torch.manual_seed(0)
+    m = build_model("vit_b_16", 10, torch.device("cpu"), image_size=64)
+    with torch.no_grad():
+        m.conv_proj.bias.normal_()
+    x = torch.randn(3, 3, 64, 64)
+    ref = m.patch_embed(x)
+    gw = torch.randn_like(ref)
+    ref.backward(gw)
+    g_ref = (m.conv_proj.weight.grad.clone(), m.conv_proj.bias.grad.clone())
+    m.zero_grad()
+    assert set_native(m) > 0 and m.dpt_native
+    out = m.patch_embed(x)
+    assert out.shape == (3, 16, 768)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    out.backward(gw)
+    torch.testing.assert_close(m.conv_proj.weight.grad, g_ref[0], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(m.conv_proj.bias.grad, g_ref[1], rtol=1e-4, atol=1e-4)
