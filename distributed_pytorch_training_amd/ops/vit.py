@@ -286,11 +286,20 @@ class _GeluLinear16(torch.autograd.Function):
         dw2 = wgrad_splitk(gz2, h.reshape(-1, n_in), ctx.w_dtype) if ctx.needs_input_grad[2] else None
         gu = db1 = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            gu, part = native().linear_dgrad_dgelu(gz2, w16.t().contiguous(), u2, b1.float().contiguous())
+            gu, part = native().linear_dgrad_dgelu(gz2, _transpose16(w16), u2, b1.float().contiguous())
             gu = gu.view(u.shape)
             if ctx.needs_input_grad[1]:
                 db1 = part.sum(1).to(b1.dtype)
         return gu, db1, dw2
+
+
+def _transpose16(w: torch.Tensor) -> torch.Tensor:
+    """W^T of a contiguous 16-bit [n_out, n_in] weight through the tiled weight-flip kernel (a 1x1
+    conv weight's [Cout, C] -> [C, Cout]): ~3x faster than the strided copy of .t().contiguous()."""
+    n_out, n_in = w.shape
+    if w.is_contiguous() and w.data_ptr() % 16 == 0 and n_out % 8 == 0:
+        return native().conv_wt_flip_multi([w.view(n_out, n_in, 1, 1)])[0].view(n_in, n_out)
+    return w.t().contiguous()
 
 
 def gelu_linear16(u: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:

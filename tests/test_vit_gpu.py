@@ -249,3 +249,11 @@ def test_gelu_linear16_fused_matches_unfused(cuda):
     assert torch.equal(outs[True][0], outs[False][0])
     for name, a, r in zip(("du", "db", "dw"), outs[True][1:], outs[False][1:]):
         _close(a, r, 2e-2, 5e-2, name)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_transpose16_is_exact(cuda, dt):
+    """fc2's weight transpose for the DGELU backward-data (tiled weight-flip kernel) == .t()."""
+    from distributed_pytorch_training_amd.ops.vit import _transpose16
+    w = torch.randn(768, 3072, device=cuda).to(dt)
+    assert torch.equal(_transpose16(w), w.t().contiguous())
