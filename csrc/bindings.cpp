@@ -1117,7 +1117,7 @@ std::vector<Tensor> gelu_bwd(Tensor gh, Tensor u, c10::optional<Tensor> bias, bo
 
 // A Linear's backward-data with the GELU backward fused (conv_fwd_kernel DGELU epilogue):
 // gu = (dy @ wt^T) * gelu'(u + bias) and part [n_in][tiles] (the column sums of gu per 128-row
-// tile: bias gradient = part.sum(1)).  dy [T, n_out], wt [n_in, n_out] (the weight transposed),
+// tile, [tiles][n_in]: bias gradient = part.sum(0)).  dy [T, n_out], wt [n_in, n_out] (the weight transposed),
 // u [T, n_in] 16-bit and contiguous; bias fp32 [n_in].
 std::vector<Tensor> linear_dgrad_dgelu(Tensor dy, Tensor wt, Tensor u, Tensor bias) {
   const int kind = act16_kind(u, "linear_dgrad_dgelu: u");
@@ -1132,7 +1132,7 @@ std::vector<Tensor> linear_dgrad_dgelu(Tensor dy, Tensor wt, Tensor u, Tensor bi
               "linear_dgrad_dgelu: fp32 bias of n_in elements on the device");
   TORCH_CHECK(T * n_out < (1ll << 31) && T * n_in < (1ll << 31), "linear_dgrad_dgelu: too many elements");
   auto gu = at::empty_like(u);
-  auto part = at::empty({n_in, (int64_t)dpt::linear_dgrad_dgelu_tiles(T)}, u.options().dtype(at::kFloat));
+  auto part = at::empty({(int64_t)dpt::linear_dgrad_dgelu_tiles(T), n_in}, u.options().dtype(at::kFloat));
   c10::hip::HIPGuard guard(u.device().index());
   dpt::launch_linear_dgrad_dgelu(static_cast<const uint16_t*>(dy.data_ptr()), static_cast<const uint16_t*>(wt.data_ptr()),
                                  static_cast<const uint16_t*>(u.data_ptr()), bias.data_ptr<float>(),
@@ -1164,6 +1164,18 @@ Tensor sum_partials(Tensor part, int64_t out_kind) {
                        part.options().dtype(out_kind == 0 ? at::kFloat : kind_dtype((int)out_kind)));
   c10::hip::HIPGuard guard(part.device().index());
   dpt::launch_sum_partials(part.data_ptr<float>(), n, (int)S, out.data_ptr(), (int)out_kind, cur_stream(part));
+  return out;
+}
+
+// Column sums of a [n, D] fp32 partials array (many rows: 16 waves per 64 columns) into out_kind.
+Tensor colsum_rows(Tensor part, int64_t out_kind) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 2,
+              "colsum_rows: contiguous fp32 [n, D]");
+  TORCH_CHECK(out_kind >= 0 && out_kind <= 2, "colsum_rows: kind 0..2");
+  auto out = at::empty({part.size(1)}, part.options().dtype(out_kind == 0 ? at::kFloat : kind_dtype((int)out_kind)));
+  c10::hip::HIPGuard guard(part.device().index());
+  dpt::launch_colsum_rows(part.data_ptr<float>(), part.size(0), part.size(1), out.data_ptr(), (int)out_kind,
+                          cur_stream(part));
   return out;
 }
 
@@ -1240,6 +1252,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("copy_rows16", &copy_rows16, py::arg("src"), py::arg("dst"));
   m.def("bias_grad16", &bias_grad16, py::arg("grad"), py::arg("out_kind"));
   m.def("sum_partials", &sum_partials, py::arg("part"), py::arg("out_kind"));
+  m.def("colsum_rows", &colsum_rows, py::arg("part"), py::arg("out_kind"));
   m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("stride"), py::arg("pad"),
         py::arg("bn_coef") = py::none());
   m.def("gap_bwd", &gap_bwd, py::arg("g"), py::arg("H"), py::arg("W"), py::arg("dtype"));

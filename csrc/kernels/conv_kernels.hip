@@ -880,7 +880,9 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
         // partials stay one column per 128-row sub-tile whatever BM is: a 256-row block
         // writes its sum in its first column and zero in the second
         constexpr int SUBB = BM / 128;
-        const int64_t pc = (int64_t)(n0 + tid) * p.bp_ld + p.bp_off + (int64_t)mt * SUBB;
+        // DGELU: [m_tiles][Cout] rows (the bias gradient is then one sum_partials pass)
+        const int64_t pc = DGELU ? (int64_t)mt * p.Cout + n0 + tid
+                                 : (int64_t)(n0 + tid) * p.bp_ld + p.bp_off + (int64_t)mt * SUBB;
         p.bp1[pc] = a;
         if (!DGELU) p.bp2[pc] = b;
         if (two) p.bp3[pc] = c3;

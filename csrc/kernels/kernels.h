@@ -140,6 +140,9 @@ void launch_bias_grad16(int kind, const uint16_t* gy, float* part, void* dbias, 
                         hipStream_t s);
 // out[i] = sum over S of part[s][i], n % 4 == 0; out kind 0 f32 / 1 bf16 / 2 f16
 void launch_sum_partials(const float* part, int64_t n, int S, void* out, int out_kind, hipStream_t s);
+// out[c] = sum_r part[r][c] over an [n][D] fp32 array (fp64 accumulation, fixed order), out of kind
+// 0 f32 / 1 bf16 / 2 f16: many short rows (sum_partials walks S serially per column)
+void launch_colsum_rows(const float* part, int64_t n, int64_t D, void* out, int out_kind, hipStream_t s);
 // dst[i0..i3, :L] = src[i0..i3, :L] (16-bit elements, strides in elements, L % 8 == 0, rows 16-B aligned)
 void launch_rows_copy16(const uint16_t* src, uint16_t* dst, const int n[4], const int64_t ss[4], const int64_t ds[4],
                         int L, hipStream_t s);

@@ -572,6 +572,10 @@ __global__ __launch_bounds__(kBlock) void sum_partials_kernel(const float4* __re
   }
 }
 
+void launch_colsum_rows(const float* part, int64_t n, int64_t D, void* out, int out_kind, hipStream_t s) {
+  launch_colsum(part, n, D, 1, out, out_kind, nullptr, 0, nullptr, 0, s);
+}
+
 void launch_sum_partials(const float* part, int64_t n, int S, void* out, int out_kind, hipStream_t s) {
   const int64_t n4 = n / 4;
   hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(n4, 2)), dim3(kBlock), 0, s,

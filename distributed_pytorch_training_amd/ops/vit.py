@@ -289,7 +289,7 @@ class _GeluLinear16(torch.autograd.Function):
             gu, part = native().linear_dgrad_dgelu(gz2, _transpose16(w16), u2, b1.float().contiguous())
             gu = gu.view(u.shape)
             if ctx.needs_input_grad[1]:
-                db1 = part.sum(1).to(b1.dtype)
+                db1 = native().colsum_rows(part, _PKIND[b1.dtype])     # sum over tiles + cast, one pass
         return gu, db1, dw2
 
 

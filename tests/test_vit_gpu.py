@@ -214,7 +214,7 @@ def test_linear_dgrad_dgelu_matches_fp32(cuda, T, dt):
     w = (torch.randn(n_out, n_in, device=cuda) / n_in ** 0.5).to(dt)
     dz = torch.randn(T, n_out, device=cuda).to(dt)
     gu, part = native().linear_dgrad_dgelu(dz, w.t().contiguous(), u, b)
-    assert part.shape == (n_in, (T + 127) // 128)
+    assert part.shape == ((T + 127) // 128, n_in)
     # the kernel rounds g = dz W2 to bf16 before the GELU derivative, as the unfused path's GEMM
     # output does: the reference does too (otherwise the column sums of T values carry
     # sqrt(T) bf16 roundings of difference)
@@ -222,7 +222,7 @@ def test_linear_dgrad_dgelu_matches_fp32(cuda, T, dt):
     ur = (u.float() + b).requires_grad_(True)
     F.gelu(ur).backward(gh)
     _close(gu, ur.grad, 2e-2, 2e-2, "gu")
-    _close(part.sum(1), ur.grad.sum(0), 1e-2, 5e-2, "dbias")
+    _close(part.sum(0), ur.grad.sum(0), 1e-2, 5e-2, "dbias")
 
 
 def test_gelu_linear16_fused_matches_unfused(cuda):
@@ -257,3 +257,13 @@ def test_transpose16_is_exact(cuda, dt):
     from distributed_pytorch_training_amd.ops.vit import _transpose16
     w = torch.randn(768, 3072, device=cuda).to(dt)
     assert torch.equal(_transpose16(w), w.t().contiguous())
+
+
+@pytest.mark.parametrize("n,D,dt", [(197, 3072, torch.bfloat16), (5, 64, torch.float32), (1000, 768, torch.float16)])
+def test_colsum_rows_matches_fp64(cuda, n, D, dt):
+    from distributed_pytorch_training_amd.ops import native
+    part = torch.randn(n, D, device=cuda)
+    kind = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[dt]
+    out = native().colsum_rows(part, kind)
+    assert out.dtype == dt and out.shape == (D,)
+    torch.testing.assert_close(out, part.double().sum(0).float().to(dt), rtol=0, atol=0)
