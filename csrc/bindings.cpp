@@ -1118,7 +1118,7 @@ std::vector<Tensor> gelu_bwd(Tensor gh, Tensor u, c10::optional<Tensor> bias, bo
 // A Linear's backward-data with the GELU backward fused (conv_fwd_kernel DGELU epilogue):
 // gu = (dy @ wt^T) * gelu'(u + bias) and part [n_in][tiles] (the column sums of gu per 128-row
 // tile, [tiles][n_in]: bias gradient = part.sum(0)).  dy [T, n_out], wt [n_in, n_out] (the weight transposed),
-// u [T, n_in] 16-bit and contiguous; bias fp32 [n_in].
+// u [T, n_in] 16-bit and contiguous; bias [n_in] fp32 or u's dtype.
 std::vector<Tensor> linear_dgrad_dgelu(Tensor dy, Tensor wt, Tensor u, Tensor bias) {
   const int kind = act16_kind(u, "linear_dgrad_dgelu: u");
   TORCH_CHECK(act16_kind(dy, "linear_dgrad_dgelu: grad") == kind && act16_kind(wt, "linear_dgrad_dgelu: wt") == kind,
@@ -1128,14 +1128,17 @@ std::vector<Tensor> linear_dgrad_dgelu(Tensor dy, Tensor wt, Tensor u, Tensor bi
   const int64_t T = dy.size(0), n_out = dy.size(1), n_in = wt.size(0);
   TORCH_CHECK(wt.size(1) == n_out && u.size(0) == T && u.size(1) == n_in, "linear_dgrad_dgelu: shape mismatch");
   TORCH_CHECK(n_in % 128 == 0 && n_out % 64 == 0, "linear_dgrad_dgelu: n_in % 128 == 0 and n_out % 64 == 0");
-  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.is_contiguous() && bias.numel() == n_in && bias.is_cuda(),
-              "linear_dgrad_dgelu: fp32 bias of n_in elements on the device");
+  const bool b16 = bias.scalar_type() == u.scalar_type();
+  TORCH_CHECK((b16 || bias.scalar_type() == at::kFloat) && bias.is_contiguous() && bias.numel() == n_in &&
+                  bias.is_cuda(), "linear_dgrad_dgelu: fp32 or u-typed bias of n_in elements on the device");
   TORCH_CHECK(T * n_out < (1ll << 31) && T * n_in < (1ll << 31), "linear_dgrad_dgelu: too many elements");
   auto gu = at::empty_like(u);
   auto part = at::empty({(int64_t)dpt::linear_dgrad_dgelu_tiles(T), n_in}, u.options().dtype(at::kFloat));
   c10::hip::HIPGuard guard(u.device().index());
   dpt::launch_linear_dgrad_dgelu(static_cast<const uint16_t*>(dy.data_ptr()), static_cast<const uint16_t*>(wt.data_ptr()),
-                                 static_cast<const uint16_t*>(u.data_ptr()), bias.data_ptr<float>(),
+                                 static_cast<const uint16_t*>(u.data_ptr()),
+                                 b16 ? nullptr : bias.data_ptr<float>(),
+                                 b16 ? static_cast<const uint16_t*>(bias.data_ptr()) : nullptr,
                                  static_cast<uint16_t*>(gu.data_ptr()), part.data_ptr<float>(), T, (int)n_out,
                                  (int)n_in, kind == 2, cur_stream(u));
   return {gu, part};

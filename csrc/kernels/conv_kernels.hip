@@ -131,6 +131,8 @@ struct ConvFwdArgs {
   // the same ReLU mask as 1 bit per element, [M][Cout/8] bytes written by the tail's forward
   // apply (bn_kernels.hip): read instead of bny when set - 1/16 of y's bytes
   const uint8_t* bnmask = nullptr;
+  // DGELU: the Linear's bias in the operands' 16-bit type (read instead of bn_mean when set)
+  const uint16_t* bias16 = nullptr;
   // BNR with a downsample branch: the block's identity path was BN2(x2) (folded into the tail,
   // ops/bn.py _BN2AddReLUPair): also sum s3 = sum dz*(x2 - mean2) for that BatchNorm
   const uint16_t* bnx2;
@@ -715,7 +717,7 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
         const int c = n0 + oc * 8 + k;
         ba[k] = (BNR || DGELU) ? 0.f : p.bn_coef[c];
         bb[k] = (BNR || DGELU) ? 0.f : p.bn_coef[p.Cout + c];
-        bm[k] = p.bn_mean[c];
+        bm[k] = (DGELU && p.bias16 != nullptr) ? cunpack<F16>((uint32_t)p.bias16[c], 0) : p.bn_mean[c];
         bm2[k] = two ? p.bn_mean2[c] : 0.f;
         s1[k] = 0.f;
         s2[k] = 0.f;
@@ -2572,7 +2574,8 @@ void launch_conv_dgrad_bnstats(const uint16_t* dy, const uint16_t* wt, uint16_t*
 // and bp1[i][mt] = the column sums of gu over 128-row tile mt (the bias gradient's partials).
 // dy [T, n_out], wt [n_in, n_out] (the weight transposed), u / gu [T, n_in] 16-bit, bias fp32.
 void launch_linear_dgrad_dgelu(const uint16_t* dy, const uint16_t* wt, const uint16_t* u, const float* bias,
-                               uint16_t* gu, float* bp1, int64_t T, int n_out, int n_in, bool f16, hipStream_t s) {
+                               const uint16_t* bias16, uint16_t* gu, float* bp1, int64_t T, int n_out, int n_in,
+                               bool f16, hipStream_t s) {
   if (n_in % 128 != 0 || n_out % 64 != 0) throw std::runtime_error("linear_dgrad_dgelu: n_in % 128, n_out % 64");
   ConvFwdArgs a;
   a.part = nullptr; a.splits = 1; a.kps = 0;
@@ -2584,7 +2587,7 @@ void launch_linear_dgrad_dgelu(const uint16_t* dy, const uint16_t* wt, const uin
   a.m_tiles = conv_m_tiles(a.M);
   a.mt256 = 0;
   a.n_tiles = n_in / 128;
-  a.bnx = u; a.bn_mean = bias; a.bn_coef = nullptr; a.bp1 = bp1; a.bp2 = nullptr;
+  a.bnx = u; a.bn_mean = bias; a.bias16 = bias16; a.bn_coef = nullptr; a.bp1 = bp1; a.bp2 = nullptr;
   a.bny = nullptr; a.bnres = nullptr; a.bnmask = nullptr; a.bnx2 = nullptr; a.bn_mean2 = nullptr; a.bp3 = nullptr;
   a.bp_ld = a.m_tiles; a.bp_off = 0;
   conv_check_offsets(a, false);

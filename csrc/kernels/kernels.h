@@ -159,9 +159,11 @@ void conv_set_halo(int on);  // 3x3 / stride-1 halo K loop (default on, DPT_CONV
 // stream-K conv_fwd_kernel grids (0 off, 1 auto below the per-CU balance eff, 2 every eligible
 // grid; eff <= 0 keeps the threshold), workspace preallocation, and the bounded-spin give-up count
 // Linear backward-data with the exact-GELU backward fused (conv_fwd_kernel DGELU epilogue):
-// gu = (dy wt^T) * gelu'(u + bias), bp1 [n_in][linear_dgrad_dgelu_tiles(T)] column-sum partials
+// gu = (dy wt^T) * gelu'(u + bias), bp1 [linear_dgrad_dgelu_tiles(T)][n_in] column-sum partials;
+// the bias is fp32 (bias) or the operands' 16-bit type (bias16, used when non-null)
 void launch_linear_dgrad_dgelu(const uint16_t* dy, const uint16_t* wt, const uint16_t* u, const float* bias,
-                               uint16_t* gu, float* bp1, int64_t T, int n_out, int n_in, bool f16, hipStream_t s);
+                               const uint16_t* bias16, uint16_t* gu, float* bp1, int64_t T, int n_out, int n_in,
+                               bool f16, hipStream_t s);
 int linear_dgrad_dgelu_tiles(int64_t T);
 void conv_set_streamk(int mode, double eff);
 int conv_get_streamk();

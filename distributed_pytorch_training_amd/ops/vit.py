@@ -286,7 +286,8 @@ class _GeluLinear16(torch.autograd.Function):
         dw2 = wgrad_splitk(gz2, h.reshape(-1, n_in), ctx.w_dtype) if ctx.needs_input_grad[2] else None
         gu = db1 = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            gu, part = native().linear_dgrad_dgelu(gz2, _transpose16(w16), u2, b1.float().contiguous())
+            bk = b1 if b1.dtype in (u.dtype, torch.float32) else b1.float()    # 16-bit: read as is
+            gu, part = native().linear_dgrad_dgelu(gz2, _transpose16(w16), u2, bk.contiguous())
             gu = gu.view(u.shape)
             if ctx.needs_input_grad[1]:
                 db1 = native().colsum_rows(part, _PKIND[b1.dtype])     # sum over tiles + cast, one pass

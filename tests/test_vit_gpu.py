@@ -267,3 +267,18 @@ def test_colsum_rows_matches_fp64(cuda, n, D, dt):
     out = native().colsum_rows(part, kind)
     assert out.dtype == dt and out.shape == (D,)
     torch.testing.assert_close(out, part.double().sum(0).float().to(dt), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_linear_dgrad_dgelu_16bit_bias_same_bits(cuda, dt):
+    """A bias in the operands' 16-bit type (read in the epilogue) == the same values as fp32."""
+    from distributed_pytorch_training_amd.ops import native
+    torch.manual_seed(5)
+    T, n_in, n_out = 300, 3072, 768
+    u = torch.randn(T, n_in, device=cuda).to(dt)
+    b16 = (torch.randn(n_in, device=cuda) * 0.5).to(dt)
+    wt = (torch.randn(n_in, n_out, device=cuda) / n_out ** 0.5).to(dt)
+    dz = torch.randn(T, n_out, device=cuda).to(dt)
+    gu16, p16 = native().linear_dgrad_dgelu(dz, wt, u, b16)
+    gu32, p32 = native().linear_dgrad_dgelu(dz, wt, u, b16.float())
+    assert torch.equal(gu16, gu32) and torch.equal(p16, p32)
