@@ -92,8 +92,24 @@ __device__ __forceinline__ float load_param(const void* p, int kind, int64_t i) 
 }
 
 // ---- LayerNorm forward (+ residual add + branch bias) ----------------------------------------
+// gamma / beta / bias are re-read per row (L1/L2 hits) instead of living in 36 registers per lane:
+// 64 VGPRs instead of 82 puts 8 waves on a SIMD (the whole 2,048-block grid resident at once)
+// instead of 5 (1,280 blocks, then a 60 %-full second round).
+__device__ __forceinline__ void load4_param(const void* p, int kind, int64_t c0, float v[4]) {
+  if (p == nullptr) {
+    v[0] = v[1] = v[2] = v[3] = 0.f;
+  } else if (kind == 0) {
+    const float4 q = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + c0);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else if (kind == 1) {
+    load4h<1>(static_cast<const uint16_t*>(p) + c0, v);
+  } else {
+    load4h<2>(static_cast<const uint16_t*>(p) + c0, v);
+  }
+}
+
 template <int VPL, int KIND, bool ADD>
-__global__ __launch_bounds__(kBlock) void ln_fwd_kernel(const float* __restrict__ x,
+__global__ __launch_bounds__(kBlock, 8) void ln_fwd_kernel(const float* __restrict__ x,
                                                         const uint16_t* __restrict__ a,
                                                         const void* __restrict__ bias, int bias_kind,
                                                         const float* __restrict__ gamma,
@@ -103,16 +119,6 @@ __global__ __launch_bounds__(kBlock) void ln_fwd_kernel(const float* __restrict_
                                                         float* __restrict__ rstd_out, int64_t T, float eps) {
   constexpr int D = VPL * 256;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float gm[VPL][4], bt[VPL][4], bs[VPL][4];
-#pragma unroll
-  for (int i = 0; i < VPL; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = (i * 64 + lane) * 4 + j;
-      gm[i][j] = gamma ? gamma[c] : 1.f;
-      bt[i][j] = beta ? beta[c] : 0.f;
-      bs[i][j] = ADD ? load_param(bias, bias_kind, c) : 0.f;
-    }
   for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < T; row += (int64_t)gridDim.x * 4) {
     const int64_t base = row * D;
     float v[VPL][4];
@@ -124,10 +130,11 @@ __global__ __launch_bounds__(kBlock) void ln_fwd_kernel(const float* __restrict_
     if (ADD) {
 #pragma unroll
       for (int i = 0; i < VPL; ++i) {
-        float w[4];
+        float w[4], bs[4];
         load4h<KIND>(a + base + (i * 64 + lane) * 4, w);
+        load4_param(bias, bias_kind, (i * 64 + lane) * 4, bs);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[i][j] += w[j] + bs[i][j];
+        for (int j = 0; j < 4; ++j) v[i][j] += w[j] + bs[j];
       }
     }
     float sum = 0.f;
@@ -147,11 +154,15 @@ __global__ __launch_bounds__(kBlock) void ln_fwd_kernel(const float* __restrict_
     const float rstd = rsqrtf(wave_sum(sq) * (1.f / D) + eps);
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
-      const int64_t off = base + (i * 64 + lane) * 4;
+      const int c0 = (i * 64 + lane) * 4;
+      const int64_t off = base + c0;
       if (ADD) *reinterpret_cast<float4*>(s_out + off) = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
+      float gm[4] = {1.f, 1.f, 1.f, 1.f}, bt[4] = {0.f, 0.f, 0.f, 0.f};
+      if (gamma) load4_param(gamma, 0, c0, gm);
+      if (beta) load4_param(beta, 0, c0, bt);
       float o[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * gm[i][j] + bt[i][j];
+      for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * gm[j] + bt[j];
       store4h<KIND>(h_out + off, o);
     }
     if (lane == 0) {
