@@ -73,7 +73,18 @@ class SelfAttention(nn.Module):
         """(out_proj(context) without its bias, the bias) - the fused path adds the bias in
         the following add+LayerNorm kernel."""
         y = self._context(x)
-        return linear16(y, shadow_param(self.out_proj, "weight", y)), shadow_param(self.out_proj, "bias", y)
+        return linear16(y, shadow_param(self.out_proj, "weight", y)), _bias16(self.out_proj, "bias", y)
+
+
+def _bias16(mod: nn.Module, name: str, like: torch.Tensor) -> torch.Tensor:
+    """A bias the fused kernels add to a 16-bit GEMM output: the bf16 weight shadow, or (no
+    shadows) the fp32 master rounded the way autocast's cast of nn.Linear's bias rounds it - the
+    two engines then compute the same values (tests/test_engine_gpu.py weight-shadow test)."""
+    b = shadow_param(mod, name, like)
+    if (b.dtype != like.dtype and like.dtype in (torch.bfloat16, torch.float16)
+            and torch.is_autocast_enabled(like.device.type)):
+        b = b.to(like.dtype)
+    return b
 
 
 class MLPBlock(nn.Sequential):
@@ -146,8 +157,8 @@ class Encoder(nn.Module):
             x, h2 = add_bias_layer_norm16(x, a, ab, blk.ln_2)
             fc1, fc2 = blk.mlp[0], blk.mlp[3]
             u = linear16(h2, shadow_param(fc1, "weight", h2))
-            z = gelu_linear16(u, shadow_param(fc1, "bias", h2), shadow_param(fc2, "weight", h2))
-            pending = (z, shadow_param(fc2, "bias", h2))
+            z = gelu_linear16(u, _bias16(fc1, "bias", h2), shadow_param(fc2, "weight", h2))
+            pending = (z, _bias16(fc2, "bias", h2))
         return add_bias_layer_norm16(x, pending[0], pending[1], self.ln)[1]
 
 

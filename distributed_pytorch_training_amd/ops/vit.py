@@ -230,6 +230,10 @@ def wgrad_splitk(dy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype) -> t
     return part.sum(0).to(out_dtype)
 
 
+def _to(t: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    return t if t.dtype == dtype else t.to(dtype)
+
+
 class _Linear16(torch.autograd.Function):
     """y = x W^T (+ b) on 16-bit operands; backward computes dW as a split-K batched GEMM
     (hipBLASLt's single-GEMM choice leaves most CUs idle on these long-K shapes)."""
@@ -250,13 +254,15 @@ class _Linear16(torch.autograd.Function):
         x2 = x.reshape(-1, shp[-1]).contiguous()
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         dx = (dy2 @ w16).view(shp) if ctx.needs_input_grad[0] else None
-        dw = wgrad_splitk(dy2, x2, ctx.w_dtype) if ctx.needs_input_grad[1] else None
+        # autocast semantics for fp32 masters (no weight shadows): the gradient of the 16-bit
+        # weight / bias copy, rounded once, then cast back - what F.linear on autocast's casts gives
+        dw = _to(wgrad_splitk(dy2, x2, w16.dtype), ctx.w_dtype) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.b_dtype is not None and ctx.needs_input_grad[2]:
             if dy2.shape[1] % 8 == 0 and dy2.dtype in _KIND:
-                db = native().bias_grad16(dy2, _PKIND[ctx.b_dtype])
+                db = _to(native().bias_grad16(dy2, _PKIND[dy2.dtype]), ctx.b_dtype)
             else:
-                db = dy2.sum(0, dtype=torch.float32).to(ctx.b_dtype)
+                db = dy2.sum(0, dtype=torch.float32).to(dy2.dtype).to(ctx.b_dtype)
         return dx, dw, db
 
 
@@ -283,14 +289,15 @@ class _GeluLinear16(torch.autograd.Function):
         n_in, n_out = u.shape[-1], gz.shape[-1]
         gz2 = gz.reshape(-1, n_out).contiguous()
         u2 = u.reshape(-1, n_in)
-        dw2 = wgrad_splitk(gz2, h.reshape(-1, n_in), ctx.w_dtype) if ctx.needs_input_grad[2] else None
+        dw2 = _to(wgrad_splitk(gz2, h.reshape(-1, n_in), w16.dtype), ctx.w_dtype) if ctx.needs_input_grad[2] else None
         gu = db1 = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             bk = b1 if b1.dtype in (u.dtype, torch.float32) else b1.float()    # 16-bit: read as is
             gu, part = native().linear_dgrad_dgelu(gz2, _transpose16(w16), u2, bk.contiguous())
             gu = gu.view(u.shape)
             if ctx.needs_input_grad[1]:
-                db1 = native().colsum_rows(part, _PKIND[b1.dtype])     # sum over tiles + cast, one pass
+                # sum over tiles + cast in one pass (16-bit like autocast's bias copy, then b1's dtype)
+                db1 = _to(native().colsum_rows(part, _PKIND[u.dtype]), b1.dtype)
         return gu, db1, dw2
 
 

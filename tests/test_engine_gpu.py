@@ -283,6 +283,8 @@ def test_weight_shadow_matches_autocast_casts(cuda, model_name, opt):
         # GEMM-algorithm rounding noise moves that weight by up to 2*lr per step.  Bound the worst
         # element by that and require the bulk to agree.
         d = (sh.ddp.arena.param_flat - no.ddp.arena.param_flat).abs()
+        print(f"shadow vs autocast casts: max {d.max().item():.3g} mean {d.mean().item():.3g} "
+              f"frac>1e-4 {(d > 1e-4).float().mean().item():.4f}")
         assert d.max().item() <= 2 * 1e-3 * 4 + 1e-4
         assert d.mean().item() < 2e-4
         assert (d > 1e-4).float().mean().item() < 0.1

@@ -197,8 +197,9 @@ def test_linear16_splitk_wgrad(cuda, n_out, n_in, bias):
     assert w.grad.dtype == torch.bfloat16
     _close(w.grad, wr.grad, 1e-2, 1e-1, "dW")
     _close(x.grad, xr.grad, 1e-2, 1e-2, "dx")
-    if bias:
-        _close(b.grad, br.grad, 1e-3, 1e-1, "db")
+    if bias:   # autocast semantics: the bf16 copy's gradient, rounded once (<= 1 ulp = 2^-8 relative)
+        assert b.grad.dtype == torch.float32
+        _close(b.grad, br.grad, 1e-2, 1e-1, "db")
 
 
 @pytest.mark.parametrize("T,dt", [(2 * 197, torch.bfloat16), (1000, torch.bfloat16), (2 * 197, torch.float16)])
