@@ -279,15 +279,16 @@ def test_weight_shadow_matches_autocast_casts(cuda, model_name, opt):
     if opt == "sgd":
         torch.testing.assert_close(sh.ddp.arena.param_flat, no.ddp.arena.param_flat, rtol=1e-4, atol=1e-5)
     else:
-        # Adam's update is ~lr*sign(m/sqrt(v)) per step: a near-zero gradient whose sign flips on
-        # GEMM-algorithm rounding noise moves that weight by up to 2*lr per step.  Bound the worst
-        # element by that and require the bulk to agree.
+        # Both runs now round like autocast (models/vit.py _bias16, ops/vit.py linear16) and were
+        # bitwise equal when measured (max 0, late round 5).  Adam's update is ~lr*sign(m/sqrt(v))
+        # per step, so any GEMM rounding noise would move a near-zero-gradient weight by up to
+        # 2*lr per step: bound the worst element by that and require the bulk to agree exactly.
         d = (sh.ddp.arena.param_flat - no.ddp.arena.param_flat).abs()
         print(f"shadow vs autocast casts: max {d.max().item():.3g} mean {d.mean().item():.3g} "
               f"frac>1e-4 {(d > 1e-4).float().mean().item():.4f}")
         assert d.max().item() <= 2 * 1e-3 * 4 + 1e-4
-        assert d.mean().item() < 2e-4
-        assert (d > 1e-4).float().mean().item() < 0.1
+        assert d.mean().item() < 2e-5
+        assert (d > 1e-4).float().mean().item() < 0.01
     assert sh.scaler.get_scale() == no.scaler.get_scale()
     # checkpoint-style reload refreshes the shadows
     with torch.no_grad():
