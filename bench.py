@@ -123,6 +123,11 @@ def parse(argv=None):
     ap.add_argument("--extra-budget", type=float, default=300.0,
                     help="seconds all extra-window child jobs together may take (later windows are "
                          "skipped and recorded as such once it is spent)")
+    ap.add_argument("--deadline", type=float, default=480.0,
+                    help="seconds from the start of the job by which rank 0 has printed the record: the "
+                         "same-box stock job and the extra windows only get the time that is left (each "
+                         "child job runs in its own process group and is killed whole at its limit), so a "
+                         "hung child can never cost the headline line")
     ap.add_argument("--vit-buckets", default="25,400,100",
                     help="bucket caps (MB) of the 8-GPU ViT-B/16 extra windows")
     ap.add_argument("--extra-rccl-channels", default="8,16",
@@ -135,11 +140,76 @@ def parse(argv=None):
 ENV_PREFIXES = ("DPT_", "NCCL_", "RCCL_", "MIOPEN_", "HIP_", "HSA_", "AMD_", "GPU_MAX_HW_QUEUES",
                 "PYTORCH_TUNABLEOP", "TORCH_NCCL", "OMP_NUM_THREADS")
 CHILD_MARK = "DPT_BENCH_LAUNCHER"
+DEADLINE_MARK = "DPT_BENCH_DEADLINE_AT"   # absolute epoch deadline, handed from a launcher to its ranks
+CHILD_JOB_MARK = "DPT_BENCH_CHILD_JOB"     # set in the stock / extra-window child jobs
+T_START = time.time()
 rccl_log = None  # distributed_pytorch_training_amd.utils.rccl_log, imported by the ranks only
 
 
 def env_in_effect() -> dict:
-    return {k: v for k, v in sorted(os.environ.items()) if k.startswith(ENV_PREFIXES) and k != CHILD_MARK}
+    return {k: v for k, v in sorted(os.environ.items())
+            if k.startswith(ENV_PREFIXES) and k not in (CHILD_MARK, DEADLINE_MARK, CHILD_JOB_MARK)}
+
+
+def _sig(v: float, digits: int = 6) -> float:
+    """Round to significant figures (a fixed number of decimals loses all precision on a slow
+    CPU run: 0.107 img/s -> 0.11)."""
+    return float(f"{v:.{digits}g}")
+
+
+def deadline_at(a) -> float:
+    """Absolute deadline of this job: a launcher's (inherited by its ranks) or start + --deadline."""
+    v = os.environ.get(DEADLINE_MARK)
+    return float(v) if v else T_START + a.deadline
+
+
+def _kill_group(p: subprocess.Popen, grace: float = 5.0) -> None:
+    """SIGTERM the whole process group of ``p`` (a child job started with start_new_session: its
+    self-launched ranks are in that group too), then SIGKILL whatever is left after ``grace``."""
+    pgid = p.pid          # start_new_session: the child leads its own process group
+    for sig in (signal.SIGTERM, signal.SIGKILL):
+        try:
+            os.killpg(pgid, sig)
+        except OSError:
+            break         # nothing left in the group
+        t_end = time.time() + grace
+        while time.time() < t_end:
+            p.poll()      # reap the leader (a zombie still counts as a group member)
+            try:
+                os.killpg(pgid, 0)
+            except OSError:
+                return
+            time.sleep(0.1)
+    p.poll()
+
+
+_LIVE_CHILDREN = []   # child-job Popen objects of this process, for the signal handler
+
+
+def run_group(cmd: list, env: dict, timeout: float):
+    """Run ``cmd`` as a child job in its own session / process group; on timeout kill the whole
+    group (its ranks included) and raise ``subprocess.TimeoutExpired``.  Returns (rc, stderr)."""
+    import tempfile
+    with tempfile.TemporaryFile(mode="w+") as err:
+        p = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=err, text=True,
+                             start_new_session=True)
+        _LIVE_CHILDREN.append(p)
+        try:
+            try:
+                rc = p.wait(timeout=max(1.0, timeout))
+            except subprocess.TimeoutExpired:
+                _kill_group(p)
+                raise
+            # the launcher exited; anything left in its group is an orphaned rank: end it
+            try:
+                os.killpg(p.pid, 0)
+                _kill_group(p)
+            except OSError:
+                pass
+        finally:
+            _LIVE_CHILDREN.remove(p)
+        err.seek(0)
+        return rc, err.read()
 
 
 def _free_port() -> int:
@@ -159,7 +229,7 @@ def _visible_gpus() -> int:
     CUDA_VISIBLE_DEVICES`` list is the fallback."""
     try:
         r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
-                           capture_output=True, text=True, timeout=600)
+                           capture_output=True, text=True, timeout=180)
         if r.returncode == 0 and r.stdout.strip():
             return int(r.stdout.strip().splitlines()[-1])
     except (subprocess.SubprocessError, ValueError, OSError):
@@ -194,8 +264,11 @@ def launch_ranks(a, argv, grace_s: float = 30.0) -> int:
     Nothing here touches the GPU: the children are fresh interpreters.  Returns the worst
     child exit status; when one rank fails, the survivors get ``grace_s`` to finish (they
     normally error out of their collective) and are then terminated, so a dead peer can not
-    leave the node hanging."""
+    leave the node hanging.  The ranks stay in this process's group (a ``killpg`` of the job
+    reaches them) and inherit the job's absolute deadline; a SIGTERM/SIGINT to this launcher is
+    passed on to them, and ranks still alive 60 s past the deadline are ended."""
     n = a.gpus
+    t_dead = deadline_at(a)
     ngpu = _visible_gpus()
     if a.rehearse_shared_gpu:
         if ngpu < 1:
@@ -214,9 +287,25 @@ def launch_ranks(a, argv, grace_s: float = 30.0) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", ROLE_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         env[CHILD_MARK] = "self"
+        env[DEADLINE_MARK] = repr(t_dead)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable, script, *argv], env=env))
     rcs = [None] * n
+
+    def _forward(signum, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+        t_end = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        os._exit(128 + signum)
+
+    old = {s: signal.signal(s, _forward) for s in (signal.SIGTERM,)}
     failed_at = None
     try:
         while any(rc is None for rc in rcs):
@@ -226,6 +315,9 @@ def launch_ranks(a, argv, grace_s: float = 30.0) -> int:
                     if rcs[i] not in (None, 0) and failed_at is None:
                         failed_at = time.time()
                         print(f"bench: rank {i} exited with status {rcs[i]}", file=sys.stderr)
+            if failed_at is None and time.time() > t_dead + 60:
+                failed_at = time.time() - grace_s - 1   # end them now
+                print("bench: ranks still running 60 s past the deadline; terminating them", file=sys.stderr)
             if failed_at is not None and time.time() - failed_at > grace_s:
                 for i, p in enumerate(procs):
                     if rcs[i] is None:
@@ -247,6 +339,10 @@ def launch_ranks(a, argv, grace_s: float = 30.0) -> int:
         for p in procs:
             p.wait()
         return 130
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    rcs = [124 if rc is None else rc for rc in rcs]
     bad = [rc for rc in rcs if rc != 0]
     if not bad:
         return 0
@@ -337,43 +433,53 @@ def _rank_devices(device, ws):
     return [mine]
 
 
-def _stock_argv(a, json_out: str) -> list:
+def _stock_argv(a, _unused=None) -> list:
     """The same benchmark on the stock engine: same model, per-GPU batch, dtype, layout, steps."""
     argv = ["--gpus", str(a.gpus), "--impl", "torch", "--steps", str(a.steps), "--warmup", str(a.warmup),
             "--model", a.model, "--batch-size", str(a.batch_size), "--image-size", str(a.image_size),
             "--num-classes", str(a.num_classes), "--amp-dtype", a.amp_dtype, "--optimizer", a.optimizer,
             "--bucket-cap-mb", str(a.bucket_cap_mb), "--profile-steps", "0", "--stock-baseline", "off",
-            "--json-out", json_out]
+            "--extra-windows", "off"]
     for flag in ("no_amp", "no_channels_last", "find"):
         if getattr(a, flag):
             argv.append("--" + flag.replace("_", "-"))
     return argv
 
 
+def _child_env() -> dict:
+    """This job's environment minus its launcher variables (a child picks its own rendezvous and
+    self-launches its ranks), marked as a child job."""
+    drop = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
+            "MASTER_PORT", "GROUP_WORLD_SIZE", "ROLE_WORLD_SIZE", CHILD_MARK, DEADLINE_MARK, "NCCL_DEBUG",
+            "NCCL_DEBUG_FILE", "NCCL_DEBUG_SUBSYS")
+    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
+    env[CHILD_JOB_MARK] = "1"
+    return env
+
+
 def _run_child(argv: list, timeout: float) -> dict:
-    """A fresh child ``bench.py`` job (new interpreter, launcher variables stripped so it picks its
-    own rendezvous and self-launches its ranks); returns its JSON record or the reason there is
-    none."""
+    """A fresh child ``bench.py`` job (new interpreter in its own process group, launcher
+    variables stripped); returns its JSON record or the reason there is none.  At ``timeout``
+    the whole group - the child's ranks included - is killed."""
     import tempfile
     fd, out = tempfile.mkstemp(prefix="dpt_child_", suffix=".json")
     os.close(fd)
-    drop = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
-            "MASTER_PORT", "GROUP_WORLD_SIZE", "ROLE_WORLD_SIZE", CHILD_MARK, "NCCL_DEBUG", "NCCL_DEBUG_FILE",
-            "NCCL_DEBUG_SUBSYS")
-    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
-    cmd = [sys.executable, os.path.abspath(__file__), *argv, "--json-out", out]
+    # the child's own deadline: its record must be written before this job gives up on it
+    cmd = [sys.executable, os.path.abspath(__file__), *argv, "--json-out", out,
+           "--deadline", f"{max(10.0, timeout - 5):.0f}"]
     t0 = time.time()
     try:
-        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+        rc, err = run_group(cmd, _child_env(), timeout)
         with open(out) as f:
             lines = [json.loads(l) for l in f if l.startswith("{")]
-        if r.returncode != 0 or not lines:
-            return {"error": f"child job exited {r.returncode}: {r.stderr[-400:]}", "wall_s": round(time.time() - t0, 1)}
+        if rc != 0 or not lines:
+            return {"error": f"child job exited {rc}: {err[-400:]}", "wall_s": round(time.time() - t0, 1)}
         rec = lines[-1]
         rec["wall_s"] = round(time.time() - t0, 1)
         return rec
     except subprocess.TimeoutExpired:
-        return {"error": f"child job exceeded {timeout:.0f} s"}
+        return {"error": f"child job exceeded {timeout:.0f} s (process group killed)",
+                "wall_s": round(time.time() - t0, 1)}
     except (OSError, ValueError) as e:
         return {"error": repr(e)[:400]}
     finally:
@@ -422,41 +528,21 @@ def extra_windows_plan(a, ws: int, forced: bool = False) -> list:
     return plan
 
 
-def run_stock_baseline(a) -> dict:
+def run_stock_baseline(a, timeout: float) -> dict:
     """Stock PyTorch-ROCm on the same box ("same MI355X box ... same harness"), in a
     fresh child job started AFTER this job's GPU work is done and its memory released: a new
-    interpreter (this process keeps running; nothing is exec'd over a process that touched the
-    GPU) that self-launches ``--gpus`` ranks of ``--impl torch``.  Launcher variables of this
-    job are stripped so the child picks its own rendezvous.  Returns its record's numbers or
-    the reason there are none."""
-    import tempfile
-    fd, out = tempfile.mkstemp(prefix="dpt_stock_", suffix=".json")
-    os.close(fd)
-    drop = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
-            "MASTER_PORT", "GROUP_WORLD_SIZE", "ROLE_WORLD_SIZE", CHILD_MARK, "NCCL_DEBUG", "NCCL_DEBUG_FILE",
-            "NCCL_DEBUG_SUBSYS")
-    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
-    cmd = [sys.executable, os.path.abspath(__file__), *_stock_argv(a, out)]
-    t0 = time.time()
+    interpreter in its own process group (this process keeps running; nothing is exec'd over a
+    process that touched the GPU) that self-launches ``--gpus`` ranks of ``--impl torch``.
+    Returns its record's numbers or the reason there are none."""
+    rec = _run_child(_stock_argv(a, None), timeout)
+    if "error" in rec:
+        return rec
     try:
-        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.stock_timeout)
-        with open(out) as f:
-            lines = [json.loads(l) for l in f if l.startswith("{")]
-        if r.returncode != 0 or not lines:
-            return {"error": f"stock job exited {r.returncode}: {r.stderr[-400:]}", "wall_s": round(time.time() - t0, 1)}
-        rec = lines[-1]
         return {"img_s": rec["value"], "ms_per_step": rec["ms_per_step"], "n_gpus": rec["n_gpus"],
                 "steps": rec["steps"], "warmup": rec["warmup"], "impl": rec["config"]["impl"],
-                "wall_s": round(time.time() - t0, 1), "cmd": "bench.py " + " ".join(_stock_argv(a, "<tmp>"))}
-    except subprocess.TimeoutExpired:
-        return {"error": f"stock job exceeded --stock-timeout {a.stock_timeout:.0f} s"}
-    except (OSError, ValueError, KeyError) as e:
+                "wall_s": rec["wall_s"], "cmd": "bench.py " + " ".join(_stock_argv(a, None))}
+    except KeyError as e:
         return {"error": repr(e)[:400]}
-    finally:
-        try:
-            os.remove(out)
-        except OSError:
-            pass
 
 
 def train_args(a):
@@ -500,6 +586,9 @@ def main(argv=None) -> int:
     elif int(env_ws) != a.gpus:
         print(f"error: --gpus {a.gpus} but the launcher started WORLD_SIZE={env_ws} ranks", file=sys.stderr)
         return 2
+    if os.environ.get(CHILD_JOB_MARK) and os.environ.get("DPT_TEST_HANG_CHILD"):
+        while True:         # testing: a child job whose ranks never finish (bench deadline test)
+            time.sleep(3600)
     global rccl_log
     from distributed_pytorch_training_amd.utils import rccl_log
     launcher = ("fake" if a.fake_pg else os.environ.get(CHILD_MARK) or
@@ -615,14 +704,14 @@ def main(argv=None) -> int:
             pdt = float(t.item())
         prof = trainer.timeline.summary(skip=0)
         prof_window = {"steps": a.profile_steps, "ms_per_step": round(1e3 * pdt / a.profile_steps, 3),
-                       "value": round(a.batch_size * ws * a.profile_steps / pdt, 2)}
+                       "value": _sig(a.batch_size * ws * a.profile_steps / pdt)}
 
     const = STOCK_TORCH_1GPU.get(a.batch_size) if (args.model == "resnet50" and args.amp and
                                                    args.amp_dtype == "bf16" and args.image_size == 224) else None
     rec = {
         "metric": "images/sec (whole node) ResNet-50 bf16 training" if args.model == "resnet50"
                   else f"images/sec (whole node) {args.model} training",
-        "value": round(value, 2), "unit": "images/s", "n_gpus": ws, "steps": a.steps,
+        "value": _sig(value), "unit": "images/s", "n_gpus": ws, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(value / (const * ws), 4) if const else None,   # replaced below when the
@@ -691,7 +780,36 @@ def main(argv=None) -> int:
                                             and not a.fake_pg and a.model == "resnet50" and not a.no_amp
                                             and ws in (4, 8))
     extra_plan = extra_windows_plan(a, ws, forced=a.extra_windows == "on") if extra_on else []
+    t_dead = deadline_at(a)
+    printed = []
+
+    def emit():
+        """Print rank 0's ONE JSON line (and append it to --json-out) exactly once."""
+        if rank != 0 or printed:
+            return
+        printed.append(True)
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "a") as f:
+                f.write(line + "\n")
+
     if stock_on or extra_plan:
+        if rank == 0:
+            # the headline is measured: whatever happens to the child jobs from here on, a SIGTERM
+            # (the driver's time limit) kills their process groups and still prints the record
+            def _on_term(signum, _frame):
+                for p in list(_LIVE_CHILDREN):
+                    _kill_group(p, grace=2.0)
+                if stock_on and "stock_same_box" not in rec["baseline"]:
+                    rec["baseline"]["stock_same_box"] = {"error": f"not measured: signal {signum} first"}
+                emit()
+                os._exit(0 if (verify is None or verify["ok"] is not False) else 3)
+
+            signal.signal(signal.SIGTERM, _on_term)
+            print("bench: headline measured (provisional record, before the child jobs): "
+                  + json.dumps({k: rec[k] for k in ("value", "ms_per_step", "n_gpus", "steps", "warmup")}),
+                  file=sys.stderr, flush=True)
         # free this job's GPU memory, then rank 0 runs the child jobs on the same GPUs while the
         # other ranks wait on the TCPStore (host side: no collective kernel spinning on a GPU)
         del trainer, model, batches, loader, ddp, comm
@@ -702,25 +820,35 @@ def main(argv=None) -> int:
             torch.cuda.empty_cache()
         if ws > 1:
             dist.barrier()
-        stock = run_stock_baseline(a) if rank == 0 and stock_on else None
+        reserve = 15.0      # seconds kept back for printing the record before the deadline
+
+        def left() -> float:
+            return t_dead - reserve - time.time()
+
+        stock = None
+        if rank == 0 and stock_on:
+            if left() >= 20:
+                stock = run_stock_baseline(a, min(a.stock_timeout, left()))
+            else:
+                stock = {"error": f"skipped: {max(0.0, left() + reserve):.0f} s left before the --deadline"}
         extra = {}
         if rank == 0:
             t_extra = time.time()
             for name, argv in extra_plan:
-                left = a.extra_budget - (time.time() - t_extra)
-                if left < 30:
-                    extra[name] = {"error": f"skipped: --extra-budget {a.extra_budget:.0f} s spent",
-                                   "cmd": "bench.py " + " ".join(argv)}
+                budget = min(a.extra_budget - (time.time() - t_extra), left())
+                if budget < 30:
+                    why = ("--extra-budget spent" if a.extra_budget - (time.time() - t_extra) < 30
+                           else "the --deadline is near")
+                    extra[name] = {"error": f"skipped: {why}", "cmd": "bench.py " + " ".join(argv)}
                     continue
-                extra[name] = _window(_run_child(argv, min(a.extra_timeout, left)), argv)
+                extra[name] = _window(_run_child(argv, min(a.extra_timeout, budget)), argv)
         if ws > 1:
             store = dist.distributed_c10d._get_default_store()
             key = "dpt_bench_stock_done"
             if rank == 0:
                 store.set(key, "1")
             else:
-                wait_s = (a.stock_timeout if stock_on else 0) + (a.extra_budget if extra_plan else 0) + 120
-                store.wait([key], datetime.timedelta(seconds=wait_s))
+                store.wait([key], datetime.timedelta(seconds=max(60.0, t_dead - time.time() + 60)))
         if rank == 0 and extra_plan:
             rec["extra_windows"] = extra
         if rank == 0 and stock_on:
@@ -729,12 +857,7 @@ def main(argv=None) -> int:
                 rec["baseline"]["stock_same_box_img_s"] = stock["img_s"]
                 rec["baseline"]["vs_baseline_source"] = "stock_same_box (fresh child job, --impl torch)"
                 rec["vs_baseline"] = round(value / stock["img_s"], 4)
-    if rank == 0:
-        line = json.dumps(rec)
-        print(line, flush=True)
-        if a.json_out:
-            with open(a.json_out, "a") as f:
-                f.write(line + "\n")
+    emit()
     if ws > 1:
         dist.barrier()
         dist.destroy_process_group()

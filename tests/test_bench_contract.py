@@ -304,3 +304,49 @@ def test_bench_extra_window_record(tmp_path):
     assert "error" not in w, w
     assert w["dtype"] == "fp32" and w["n_gpus"] == 1 and w["value"] > 0 and w["steps"] == 2
     assert rec["dtype"] == "bf16"
+
+
+def _tagged_procs(tag: str):
+    """Live processes (zombies excluded) whose environment carries DPT_TEST_TAG=tag."""
+    import psutil
+    out = []
+    for p in psutil.process_iter(["pid"]):
+        try:
+            if p.status() == psutil.STATUS_ZOMBIE:
+                continue
+            if p.environ().get("DPT_TEST_TAG") == tag:
+                out.append((p.pid, " ".join(p.cmdline())[:200]))
+        except (psutil.NoSuchProcess, psutil.AccessDenied, psutil.ZombieProcess):
+            continue
+    return out
+
+
+def test_bench_deadline_survives_hung_child_jobs(tmp_path):
+    """child jobs (stock run, extra windows) whose ranks hang can neither cost
+    the headline record nor leave rank processes behind.  With every child job hanging
+    (DPT_TEST_HANG_CHILD), a 2-rank job with a 90 s --deadline still prints its one record in
+    time, records the stock run and the extra window as errors, and no process of the job
+    (launchers, ranks, child jobs or their ranks) is alive after it exits."""
+    import time
+    import uuid
+    tag = uuid.uuid4().hex
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(DPT_TEST_HANG_CHILD="1", DPT_TEST_TAG=tag)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--stock-baseline", "on",
+                        "--extra-windows", "on", "--extra-steps", "2", "--deadline", "90", *TINY],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=600, env=env)
+    wall = time.time() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    rec = lines[0]
+    _check(rec, 2)
+    assert "error" in rec["baseline"]["stock_same_box"], rec["baseline"]
+    assert rec["baseline"]["vs_baseline_source"] == "stock_reference_constant"
+    w = rec["extra_windows"]["resnet50_fp32"]
+    assert "error" in w and "cmd" in w, w
+    assert wall < 90 + 30, wall            # deadline + process start-up slack
+    time.sleep(1.0)
+    left = _tagged_procs(tag)
+    assert not left, left
