@@ -142,7 +142,18 @@ ENV_PREFIXES = ("DPT_", "NCCL_", "RCCL_", "MIOPEN_", "HIP_", "HSA_", "AMD_", "GP
 CHILD_MARK = "DPT_BENCH_LAUNCHER"
 DEADLINE_MARK = "DPT_BENCH_DEADLINE_AT"   # absolute epoch deadline, handed from a launcher to its ranks
 CHILD_JOB_MARK = "DPT_BENCH_CHILD_JOB"     # set in the stock / extra-window child jobs
-T_START = time.time()
+
+
+def _process_start() -> float:
+    """Creation time of this process (the --deadline clock starts before the torch import)."""
+    try:
+        import psutil
+        return float(psutil.Process().create_time())
+    except Exception:
+        return time.time()
+
+
+T_START = _process_start()
 rccl_log = None  # distributed_pytorch_training_amd.utils.rccl_log, imported by the ranks only
 
 

@@ -67,6 +67,11 @@ def main(argv=None):
     step_ns = (int(rows[-1]["End_Timestamp"]) - int(rows[0]["Start_Timestamp"])) / a.steps
     agg = defaultdict(lambda: {"n": 0, "ns": 0.0, "lost": 0.0})
     total = lost = 0.0
+    # split of the estimate (4.63 vs 0.96 ms): grids of at least one full wave of
+    # block slots lose their last wave's empty slots as tail time; a grid smaller than one wave
+    # has no tail at all - its "empty slots" only mean fewer co-resident blocks, each of which
+    # then gets a larger share of the CU, so that part of the estimate is an upper bound
+    split = {"multi": [0.0, 0.0], "sub": [0.0, 0.0]}
     for r in rows:
         dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         total += dur
@@ -83,10 +88,20 @@ def main(argv=None):
         e["eff"] = eff
         e["lost"] += dur * (1 - eff)
         lost += dur * (1 - eff)
+        sp = split["multi" if tiles >= slots else "sub"]
+        sp[0] += dur
+        sp[1] += dur * (1 - eff)
     print(f"# Grid fill over {a.steps} timed steps: `{a.trace}`\n")
     print(f"step (first dispatch start -> last end) {step_ns / 1e6:.3f} ms; kernel time {total / a.steps / 1e6:.3f} ms/step; "
           f"estimated last-wave idle time {lost / a.steps / 1e6:.3f} ms/step "
           f"({100 * lost / max(total, 1):.1f} % of kernel time)\n")
+    print("| grids | kernel ms/step | estimated idle ms/step | what the estimate means |")
+    print("|---|---|---|---|")
+    print(f"| >= 1 wave of block slots | {split['multi'][0] / a.steps / 1e6:.3f} | {split['multi'][1] / a.steps / 1e6:.3f} | "
+          "last-wave tail: slots really empty while the last blocks finish |")
+    print(f"| < 1 wave (one partial wave) | {split['sub'][0] / a.steps / 1e6:.3f} | {split['sub'][1] / a.steps / 1e6:.3f} | "
+          "upper bound: no tail; fewer co-resident blocks, each with a larger share of its CU |")
+    print()
     print("| kernel | tiles | blocks/CU | LDS B | VGPR+AGPR | waves | wave eff | calls/step | ms/step | lost ms/step |")
     print("|---|---|---|---|---|---|---|---|---|---|")
     items = sorted(agg.items(), key=lambda kv: -kv[1]["lost"])

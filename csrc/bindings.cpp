@@ -1285,6 +1285,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eager_min_k"), py::arg("target"), "split-K thresholds (A/B knob; <= 0 keeps a value)");
   m.def("conv_set_big", &dpt::conv_set_big, py::arg("on"));
   m.def("conv_set_halo", &dpt::conv_set_halo, py::arg("on"));
+  m.def("conv_set_breg", &dpt::conv_set_breg, py::arg("mode"));
+  m.def("conv_get_breg", &dpt::conv_get_breg);
   m.def("conv_set_streamk", &dpt::conv_set_streamk, py::arg("mode"), py::arg("eff") = 0.0);
   m.def("conv_get_streamk", &dpt::conv_get_streamk);
   m.def("conv_sk_prepare", &dpt::conv_sk_prepare);
@@ -1371,6 +1373,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("exit_grace_s") = 30.0)
       .def_property_readonly("watchdog_tripped", &dpt::RcclComm::watchdog_tripped)
       .def_property_readonly("watchdog_outstanding", &dpt::RcclComm::watchdog_outstanding)
+      .def_property_readonly("watchdog_tracked", &dpt::RcclComm::watchdog_tracked)
       .def("async_error", &dpt::RcclComm::async_error);
 
   py::class_<dpt::HostBridgeComm, dpt::Collective, std::shared_ptr<dpt::HostBridgeComm>>(m, "HostBridgeComm")

@@ -216,15 +216,21 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero16[4];
 template <int BMT, int BN, int STAGES, bool LDSEPI, bool BKN, bool STATS = true, bool BNB = false,
           bool BNR = false, bool REMAP = false, bool ZSIB = false, bool BNR2 = false, bool F16 = false,
           int NT = conv::kThreads, bool SPLIT = false, bool HALO = false, int HB = 1, bool SK = false,
-          bool DGELU = false>
-__global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p) {
+          bool DGELU = false, bool BREG = false>
+__global__ __launch_bounds__(NT, (SK || BREG) ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p) {
   using namespace conv;
   constexpr int BM = BMT;
   constexpr int NW = NT / 64;         // waves
-  constexpr int WN = BN / 64;         // waves along N (each wave owns 64 output channels)
+  // BREG: the B operand (weights) never touches LDS - every wave loads its own 32 output
+  // channels' fragments straight from L2 into VGPRs (one 16-byte buffer load per lane and
+  // k-slice, refilled right after the MFMAs that consumed it), and the LDS holds only A, double
+  // buffered: the next A tile (1x1: the next K-step; HALO: the next halo strip, one per three
+  // taps) streams in while this one is multiplied, in the same LDS as the single-stage tile's A + B
+  constexpr int WCOL = BREG ? 32 : 64;  // output channels per wave
+  constexpr int WN = BN / WCOL;       // waves along N
   constexpr int WM = NW / WN;         // waves along M
   constexpr int MI = BM / (WM * 32);  // 32-row MFMA tiles per wave
-  constexpr int NI = 2;               // 32-col MFMA tiles per wave
+  constexpr int NI = WCOL / 32;       // 32-col MFMA tiles per wave
   static_assert(WM * WN == NW && MI >= 1 && MI * WM * 32 == BM, "conv_fwd_kernel: bad wave tiling");
   constexpr int A_PER_T = BM * 8 / NT;  // glds instructions per wave per K-step (A)
   constexpr int B_PER_T = BN * 8 / NT;  // (B)
@@ -234,18 +240,21 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
   // with u = bnx (the fc1 GEMM output before its bias) and b = bn_mean (fp32 bias); bp1 gets the
   // per-tile column sums of gu (fc1's bias gradient), bp2 is not written
   static_assert(!DGELU || (BNB && !BNR && !STATS && !REMAP && LDSEPI && !SK), "DGELU config");
+  static_assert(!BREG || (BMT == 128 && STAGES == 1 && LDSEPI && !BKN && !SPLIT && !SK && HB == 1 &&
+                          NT == conv::kThreads && (BN == 128 || BN == 64)), "BREG config");
   constexpr int HROWS = 136;  // halo strip rows: 128 + 2, rounded up to whole 8-row glds instructions
   // HB (HALO): B taps staged per load phase - 1: one per K-step; 3: all three taps of the row
   // with the halo strip, one wait per three K-steps (more LDS: fewer resident blocks)
   static_assert(HB == 1 || (HALO && HB == 3), "HB");
   constexpr int A_BYTES = (HALO ? HROWS : BM) * kRowBytes, B_BYTES = BN * kRowBytes;
-  constexpr int STAGE = A_BYTES + HB * B_BYTES;
+  constexpr int STAGE = A_BYTES + (BREG ? 0 : HB * B_BYTES);
+  constexpr int NSTAGE = BREG ? 2 : STAGES;  // LDS operand buffers
   constexpr int C_STRIDE = BN * 2 + 16;  // epilogue image row stride (bytes), padded
   constexpr int RED = 2 * WM * BN * 4;   // BN-statistics cross-wave scratch
   // HALO: one zeroed 128-byte row after the K-loop buffers - a fragment row in the padding
   // reads it instead of being zeroed in registers (4 v_cndmask per fragment and K-step)
-  constexpr int ZROW = STAGES * STAGE;
-  constexpr int LDS_MAIN = STAGES * STAGE + (HALO ? kRowBytes : 0);
+  constexpr int ZROW = NSTAGE * STAGE;
+  constexpr int LDS_MAIN = NSTAGE * STAGE + (HALO ? kRowBytes : 0);
   // HALF: the 128-row, 4-wave LDS epilogue stages its output image 64 rows at a time, so the
   // epilogue (17 KiB + statistics scratch) fits under the 32 KiB K-loop buffer of a 128 x 128
   // tile: 5 resident blocks per CU instead of 4 (36 KiB), i.e. 25 % more bytes in flight for a
@@ -390,9 +399,9 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         if (BKN) {
-          fb[j] = wg_frag<RBK>(b, kk * 16, wn * 64 + j * 32, lane);
+          fb[j] = wg_frag<RBK>(b, kk * 16, wn * WCOL + j * 32, lane);
         } else {
-          const int row = wn * 64 + j * 32 + lr;
+          const int row = wn * WCOL + j * 32 + lr;
           fb[j] = *reinterpret_cast<const bf16x8_t*>(b + row * kRowBytes + conv::swz(row, ch) * 16);
         }
       }
@@ -404,7 +413,138 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
     }
   };
 
-  if constexpr (HALO) {
+  if constexpr (BREG) {
+    static_assert(NI == 1 && WM * MI * 32 == BM, "BREG: one 32-column B fragment per wave and k-slice");
+    typedef unsigned breg_u32x4 __attribute__((ext_vector_type(4)));
+    // this lane's B column is output channel n0 + wn*32 + lr; its 8 k of k-slice kk are the
+    // K-step's elements [16kk + 8lh, +8): 16 contiguous bytes of the KRSC weight row
+    const uint32_t bvoff = (uint32_t)((int64_t)(n0 + wn * WCOL + lr) * Kg + 8 * lh) * 2u;
+    auto load_b = [&](int kbase, int kk) -> bf16x8_t {  // kbase: first k of the K-step (uniform)
+      const breg_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rw, bvoff + (uint32_t)kk * 32u,
+                                                                 (uint32_t)kbase * 2u, 0);
+      return __builtin_bit_cast(bf16x8_t, v);
+    };
+    bf16x8_t fb[BK / 16];
+    if constexpr (HALO) {
+      int fho[MI], fwo[MI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int64_t m = m0 + wm * (MI * 32) + i * 32 + lr;
+        if (m < p.M) {
+          const int rem = (int)(m % HoWo);
+          fho[i] = rem / p.Wo;
+          fwo[i] = rem - fho[i] * p.Wo;
+        } else {
+          fho[i] = -(1 << 28);
+          fwo[i] = 0;
+        }
+      }
+      if (tid < kRowBytes / 16) *reinterpret_cast<uint4*>(lds + ZROW + tid * 16) = uint4{0u, 0u, 0u, 0u};
+      const int64_t npix = (int64_t)p.N * p.H * p.W;
+      auto stage_halo = [&](int r, int cb, int buf) {
+        const int64_t q0 = m0 + (int64_t)(r - 1) * p.W - 1;
+        unsigned char* hb = lds + buf * STAGE;
+        for (int gi = wid; gi < HROWS / 8; gi += NW) {
+          const int j = gi * 8 + (lane >> 3);
+          const int chunk = (lane & 7) ^ ((j >> 1) & 7);
+          const int64_t q = q0 + j;
+          const bool ok = q >= 0 && q < npix;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rx, (__attribute__((address_space(3))) void*)(hb + gi * 1024), 16,
+              ok ? (uint32_t)((int)q * p.C + cb * BK + chunk * 8) * 2u : kOOB, 0, 0, 0);
+        }
+      };
+      auto kb = [&](int r, int sx, int cb) { return (r * 3 + sx) * p.C + cb * BK; };
+      // tap (r, sx) of the strip in `buf` with the B fragments in fb; kn >= 0: refill fb with
+      // the K-step at k = kn, one k-slice at a time right after its MFMAs
+      auto mma_h = [&](int buf, int r, int sx, int kn) {
+        const unsigned char* hb = lds + buf * STAGE;
+        int abase[MI];
+        const int hrow0 = wm * (MI * 32) + lr + sx;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const bool ok = ((unsigned)(fho[i] + r - 1) < (unsigned)p.H) & ((unsigned)(fwo[i] + sx - 1) < (unsigned)p.W);
+          abase[i] = ok ? buf * STAGE + (hrow0 + i * 32) * kRowBytes : ZROW;
+        }
+        (void)hb;
+#pragma unroll
+        for (int kk = 0; kk < BK / 16; ++kk) {
+          const int coff = conv::swz(hrow0, kk * 2 + lh) * 16;
+          bf16x8_t fa[MI];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8_t*>(lds + (abase[i] | coff));
+#pragma unroll
+          for (int i = 0; i < MI; ++i) acc[i][0] = cmfma<F16>(fa[i], fb[kk], acc[i][0]);
+          if (kn >= 0) fb[kk] = load_b(kn, kk);
+        }
+      };
+      const int T = 3 * cblocks;
+      stage_halo(0, 0, 0);
+#pragma unroll
+      for (int kk = 0; kk < BK / 16; ++kk) fb[kk] = load_b(kb(0, 0, 0), kk);
+      for (int t = 0; t < T; ++t) {
+        const int r = t / cblocks, cb = t - r * cblocks, buf = t & 1;
+        const int rn = (t + 1) / cblocks, cbn = (t + 1) - rn * cblocks;
+        vmcnt_wait<0>();   // this strip and tap 0's B fragments
+        __syncthreads();   // every wave's part of the strip is in; strip t-1's buffer is free
+        mma_h(buf, r, 0, kb(r, 1, cb));
+        vmcnt_wait<0>();   // tap 1's B fragments
+        mma_h(buf, r, 1, kb(r, 2, cb));
+        if (t + 1 < T) stage_halo(rn, cbn, buf ^ 1);  // lands while tap 2 is multiplied
+        // tap 2's B fragments were issued before the strip: wait for them only
+        if (t + 1 < T) {
+          if (wid < (HROWS / 8) % NW) vmcnt_wait<(HROWS / 8 + NW - 1) / NW>();
+          else vmcnt_wait<(HROWS / 8) / NW>();
+        } else {
+          vmcnt_wait<0>();
+        }
+        mma_h(buf, r, 2, t + 1 < T ? kb(rn, 0, cbn) : -1);
+      }
+      __syncthreads();  // the epilogue reuses the LDS
+    } else {
+      auto stage_a = [&](int ks, int buf) {
+        const int rs = (ks / cblocks) * tps, cb = ks - (ks / cblocks) * cblocks;
+        const int r = rs / p.S, s = rs - r * p.S;
+        const int koff = (r * p.W + s) * p.C + cb * BK;
+        unsigned char* a = lds + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < A_PER_T; ++i) {
+          const int hi = hi0[i] + r, wi = wi0[i] + s;
+          const bool ok = ((unsigned)hi < (unsigned)p.H) & ((unsigned)wi < (unsigned)p.W);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(a + (wid * A_PER_T + i) * 1024),
+                                                   16, ok ? (uint32_t)(aoff[i] + koff) * 2u : kOOB, 0, 0, 0);
+        }
+      };
+      auto mma_r = [&](int buf, int kn) {
+        const unsigned char* a = lds + buf * STAGE;
+#pragma unroll
+        for (int kk = 0; kk < BK / 16; ++kk) {
+          const int ch = kk * 2 + lh;
+          bf16x8_t fa[MI];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const int row = wm * (MI * 32) + i * 32 + lr;
+            fa[i] = *reinterpret_cast<const bf16x8_t*>(a + row * kRowBytes + conv::swz(row, ch) * 16);
+          }
+#pragma unroll
+          for (int i = 0; i < MI; ++i) acc[i][0] = cmfma<F16>(fa[i], fb[kk], acc[i][0]);
+          if (kn >= 0) fb[kk] = load_b(kn, kk);
+        }
+      };
+      stage_a(ks0, 0);
+#pragma unroll
+      for (int kk = 0; kk < BK / 16; ++kk) fb[kk] = load_b(ks0 * BK, kk);
+      for (int ks = ks0; ks < ks1; ++ks) {
+        const int cur = (ks - ks0) & 1;
+        vmcnt_wait<0>();   // A tile ks (LDS) and its B fragments (VGPRs)
+        __syncthreads();   // every wave's part of A is in; the other buffer is free
+        const bool more = ks + 1 < ks1;
+        if (more) stage_a(ks + 1, cur ^ 1);
+        mma_r(cur, more ? (ks + 1) * BK : -1);
+      }
+      __syncthreads();  // the epilogue reuses the LDS
+    }
+  } else if constexpr (HALO) {
     // per-lane fragment rows: output pixel coordinates, fixed for the whole loop
     int fho[MI], fwo[MI];
 #pragma unroll
@@ -463,7 +603,7 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
         const unsigned char* bs = bb + (HB == 3 ? sx * B_BYTES : 0);
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          const int row = wn * 64 + j * 32 + lr;
+          const int row = wn * WCOL + j * 32 + lr;
           fb[j] = *reinterpret_cast<const bf16x8_t*>(bs + row * kRowBytes + conv::swz(row, ch) * 16);
         }
 #pragma unroll
@@ -556,7 +696,7 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int col = n0 + wn * 64 + j * 32 + lr2;
+        const int col = n0 + wn * WCOL + j * 32 + lr2;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int64_t m = m0 + wm * (MI * 32) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh2;
@@ -574,25 +714,40 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
     // one VGPR offset per thread and slot; the float4 index q rides in the SGPR offset
     const __amdgpu_buffer_rsrc_t rp =
         __builtin_amdgcn_make_buffer_rsrc((void*)p.sk.part, 0, (int)p.sk.part_bytes, 0x00020000);
+    // a consumer that gave up on a contributor poisons its tile with NaN: the step's non-finite
+    // check then sees it, and the trainer fails loudly on the give-up counter (conv_sk_errors) at
+    // its host touch points - a late publish can leave a flag set for a later launch
+    __shared__ int sk_gave_up;
     if (sk_role == 2) {
       // consume: wave 0 polls each contributor's flag (relaxed, with sleeps, bounded), resets it for
       // the next launch, ONE agent-scope acquire, then every wave reads the partials
       if (wid == 0) {
+        int gave_up = 0;
         for (int b = sk_c0; b <= sk_c1; b += 8) {
           unsigned spins = 0;
           while (__hip_atomic_load((gu32*)(p.sk.flags + b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
             __builtin_amdgcn_s_sleep(2);
             if (++spins > (1u << 20)) {  // ~1 s: a contributor that never publishes - give up, count it
               if (lane == 0) __hip_atomic_fetch_add((gu32*)p.sk.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              gave_up = 1;
               break;
             }
           }
           if (lane == 0) __hip_atomic_store((gu32*)(p.sk.flags + b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        if (lane == 0) sk_gave_up = gave_up;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
+      if (sk_gave_up) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = __builtin_nanf("");
+      }
     }
     if (sk_role != 0) {
       // one pass over the accumulators, a float4 at a time, for both roles (keeps them in place:
@@ -645,7 +800,7 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      const int col = wn * 64 + j * 32 + lr;
+      const int col = wn * WCOL + j * 32 + lr;
       const int rbase = wm * (MI * 32) + i * 32 + 4 * lh;
 #pragma unroll
       for (int e = 0; e < 16; e += 2) {
@@ -677,7 +832,7 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
       cs[j] += __shfl_xor(cs[j], 32, 64);
       cq[j] += __shfl_xor(cq[j], 32, 64);
       if (lh == 0) {
-        const int col = wn * 64 + j * 32 + lr;
+        const int col = wn * WCOL + j * 32 + lr;
         red[wm * BN + col] = cs[j];
         red[WM * BN + wm * BN + col] = cq[j];
       }
@@ -741,7 +896,7 @@ __global__ __launch_bounds__(NT, SK ? 4 : 2) void conv_fwd_kernel(ConvFwdArgs p)
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NI; ++j) {
-            const int col = wn * 64 + j * 32 + lr;
+            const int col = wn * WCOL + j * 32 + lr;
             const int rbase = wm * (MI * 32) + i * 32 + 4 * lh - half * 64;
 #pragma unroll
             for (int e = 0; e < 16; e += 2) {
@@ -2084,6 +2239,11 @@ static int take_attached_reduce(ConvFwdArgs& a) { return take_attached_reduce(a.
 // 0.064 ms; a 1024-tile cut-off measured slower) - else one B tap per phase (HB = 1; HB = 3
 // everywhere lost 1.2 % in the step), 2 / 3 = force HB
 static int g_conv_halo = 1;
+// B operand straight into VGPRs (conv_fwd_kernel BREG): bit 0 = 3x3 HALO convs, bit 1 = the
+// other single-stage 128-row convs (1x1, strided, stem); conv_set_breg (A/B)
+static int g_conv_breg = 0;
+void conv_set_breg(int mode) { g_conv_breg = mode; }
+int conv_get_breg() { return g_conv_breg; }
 static int halo_hb(const ConvFwdArgs& a, int bn) {
   if (g_conv_halo == 2) return 1;
   if (g_conv_halo == 3) return 3;
@@ -2185,7 +2345,27 @@ static void fwd_launch(dim3 grid, dim3 /*block*/, hipStream_t s, const ConvFwdAr
   if constexpr (NT == conv::kThreads) grid.x += (unsigned)take_attached_reduce(a);
   conv_check_offsets(a, BKN);
   if constexpr (BMT == 128 && STAGES == 1 && LDSEPI && !BKN && !REMAP && NT == conv::kThreads) {
-    if (halo_ok(a)) {
+    // B operand in registers (conv_set_breg: bit 0 the 3x3 HALO convs, bit 1 the others)
+    const bool halo = halo_ok(a);
+    if ((g_conv_breg & (halo ? 1 : 2)) && a.n_tiles * BN == a.Cout) {
+      if (halo) {
+        if (a.f16)
+          hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, 1, true, false, STATS, BNB, BNR, false, ZSIB, BNR2, true,
+                                              conv::kThreads, false, true, 1, false, false, true>), grid, block, 0, s, a);
+        else
+          hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, 1, true, false, STATS, BNB, BNR, false, ZSIB, BNR2, false,
+                                              conv::kThreads, false, true, 1, false, false, true>), grid, block, 0, s, a);
+      } else {
+        if (a.f16)
+          hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, 1, true, false, STATS, BNB, BNR, false, ZSIB, BNR2, true,
+                                              conv::kThreads, false, false, 1, false, false, true>), grid, block, 0, s, a);
+        else
+          hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, 1, true, false, STATS, BNB, BNR, false, ZSIB, BNR2, false,
+                                              conv::kThreads, false, false, 1, false, false, true>), grid, block, 0, s, a);
+      }
+      return;
+    }
+    if (halo) {
       if (halo_hb(a, BN) == 3) {  // all three B taps with the halo strip
         if (a.f16)
           hipLaunchKernelGGL((conv_fwd_kernel<BMT, BN, 1, true, false, STATS, BNB, BNR, false, ZSIB, BNR2, true,

@@ -66,6 +66,7 @@ class RcclComm : public Collective {
   void enable_watchdog(double timeout_s, double poll_s, double exit_grace_s);
   bool watchdog_tripped() const { return watchdog_ && watchdog_->tripped(); }
   size_t watchdog_outstanding() const { return watchdog_ ? watchdog_->outstanding() : 0; }
+  uint64_t watchdog_tracked() const { return watchdog_ ? watchdog_->tracked() : 0; }
   std::string async_error() const;
   // Test hook: make async_error() report `msg` (exercises the watchdog's async-error branch
   // without a broken peer).  Empty string clears it.

@@ -92,6 +92,11 @@ size_t StreamWatchdog::outstanding() const {
   return core_.outstanding();
 }
 
+uint64_t StreamWatchdog::tracked() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return next_seq_;
+}
+
 void StreamWatchdog::loop() {
   double tripped_at = -1.0;
   std::unique_lock<std::mutex> lk(mu_);

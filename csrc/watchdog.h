@@ -72,6 +72,8 @@ class StreamWatchdog {
   bool tripped() const { return tripped_.load(); }
   std::string reason() const;
   size_t outstanding() const;
+  // Completion markers handed to the watchdog so far (retired = tracked - outstanding).
+  uint64_t tracked() const;
 
  private:
   void loop();

@@ -136,6 +136,10 @@ def build_parser() -> argparse.ArgumentParser:
                         "(RCCL through torch's default process group), host (gloo through pinned host "
                         "staging - lets several ranks share one GPU; debug only); host-async enqueues "
                         "the host collective on the comm stream like RCCL, so backward overlaps it")
+    g.add_argument("--rehearse-shared-gpu", action="store_true",
+                   help="testing: every rank runs on cuda:0 with a gloo process group (needs --comm host or "
+                        "host-async) - the N > 1 GPU code path (bucketed collectives, hipGraph capture, "
+                        "consistency checks) on a one-GPU box; timings are not xGMI's")
     g.add_argument("--rccl-channels", default=0, type=int,
                    help="RCCL channels (CTAs) of the framework's gradient communicator, set per "
                         "communicator through ncclConfig_t minCTAs/maxCTAs (0 = RCCL's topology default; "

@@ -129,13 +129,24 @@ def _has_randomness(module) -> bool:
     return any(isinstance(m, torch.nn.modules.dropout._DropoutNd) and m.p > 0 for m in module.modules())
 
 
-def auto_enabled(args, device, world_size: int = 1) -> bool:
-    """The ``--cuda-graph`` default: replay when the step is launch-bound."""
+# communicators whose collectives a hipGraph can hold: the framework's RCCL communicator (captured
+# ncclAllReduce on its comm stream, tests/test_graph_rccl_gpu.py) and the asynchronous host bridge
+# (host-function nodes).  The synchronous bridge blocks on the stream; torch's c10d communicator
+# is not captured by default.
+GRAPH_COMMS = ("rccl", "host-async")
+
+
+def auto_enabled(args, device, world_size: int = 1, comm_kind: str | None = None) -> bool:
+    """The ``--cuda-graph`` default: replay when the step is launch-bound - at any world size
+    whose communicator can be captured (``comm_kind``: the communicator actually created, else
+    ``--comm``).  At N > 1 the capture outcome is MIN-agreed over the ranks and the first replay
+    is validated against eager steps on every rank (``GraphedStep``), so a rank whose capture or
+    replay disagrees puts every rank back on eager steps."""
     if torch.device(device).type != "cuda" or getattr(args, "impl", "native") != "native":
         return False
     if getattr(args, "profile_sync", False) or getattr(args, "grad_accum", 1) != 1:
         return False
-    if world_size > 1:
+    if world_size > 1 and (comm_kind or getattr(args, "comm", "rccl")) not in GRAPH_COMMS:
         return False
     return int(args.batch_size) * int(args.image_size) ** 2 <= AUTO_GRAPH_MAX_PIXELS
 
@@ -329,7 +340,17 @@ class GraphedStep:
                 warnings.warn("hipGraph capture failed on another rank: every rank runs eagerly")
             ok = False
         if not ok:
+            # every failure path (this rank's capture raised, or another rank's did): drop what
+            # was captured and the host-bridge jobs / pinned staging it kept alive
             self.failed = True
+            try:
+                g.reset()
+            except Exception:       # nothing was captured
+                pass
+            torch.cuda.synchronize()
+            release = getattr(comm, "release_graph_resources", None)
+            if release is not None:
+                release()
             return
         self.graph, self.out, self.loss = g, out, loss
 

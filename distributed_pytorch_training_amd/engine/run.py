@@ -37,7 +37,10 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     args = parse_args(argv)
     Path(args.output_dir).mkdir(parents=True, exist_ok=True)
     setup_miopen_env()
-    info = init_distributed(args.backend, args.dist_timeout)
+    shared = bool(getattr(args, "rehearse_shared_gpu", False))
+    if shared and args.comm not in ("host", "host-async"):
+        raise SystemExit("--rehearse-shared-gpu needs --comm host or --comm host-async (RCCL needs one GPU per rank)")
+    info = init_distributed(args.backend, args.dist_timeout, shared_gpu=shared)
     rank, world_size, device = info.rank, info.world_size, info.device
     if args.impl == "native" and device.type == "cuda":
         setup_tunableop()
@@ -94,6 +97,13 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         sys.stdout.flush()
         sys.stderr.flush()
         os._exit(1)
+    g = trainer.graphed
+    if g is not None:   # stderr: the reference's stdout lines stay byte-identical
+        import sys
+        v = g.validation or {}
+        print(f"[dpt] rank {rank}: hipGraph captured={g.graph is not None} failed={g.failed} replays={g.replays} "
+              f"validation_ok={v.get('ok')} replay_vs_eager={v.get('replay_vs_eager')} "
+              f"param_checksum={trainer.ddp.arena.param_flat.double().sum().item():.17g}", file=sys.stderr, flush=True)
     trainer.close()
     cleanup_distributed()
     return 0

@@ -93,9 +93,6 @@ class Trainer:
         from ..parallel.ddp import NativeDDP
 
         args = self.args
-        if getattr(args, "native_conv_fp32", False):
-            from ..ops import conv_f32
-            conv_f32.ENABLED = True          # process-wide: fp32 convs on the MFMA kernels
         from ..models.vit import set_native as vit_set_native
         vit_set_native(model, self.device.type == "cuda")   # fused ViT encoder (no-op for other models)
         gpu_cl = self.device.type == "cuda" and bool(getattr(args, "channels_last", False))
@@ -105,16 +102,28 @@ class Trainer:
             from .. import ops
             sk = {"off": 0, "auto": 1, "all": 2}[getattr(args, "conv_streamk", "off")]
             ops.native().conv_set_streamk(sk)   # process-wide, like the other conv policies
+            self._streamk = bool(sk)
             if sk:
                 ops.native().conv_sk_prepare()  # workspace before any graph capture
         # every supported conv runs native: small tile grids split their K loop (split-K,
         # conv_kernels.hip), which made the MFMA path faster than MIOpen on ResNet-18 / 32x32
         # under hipGraph too; DPT_CONV_MIN_PIXELS still routes tiny convs to MIOpen
         min_px = None
+        # --native-conv-fp32: this model's fp32 convs on the fp32 MFMA kernels (routing stored per
+        # conv module, never process-wide: ADVICE r5)
+        f32 = True if getattr(args, "native_conv_fp32", False) else None
+        if f32 and not use_native_conv:
+            import warnings
+            warnings.warn("--native-conv-fp32 has no effect: the MFMA conv kernels need a GPU, channels_last "
+                          "activations and native convs (no --no-native-conv)")
+        if f32 and self.amp:
+            import warnings
+            warnings.warn("--native-conv-fp32 only affects fp32 convolutions; under --amp the 16-bit MFMA "
+                          "kernels run")
         if getattr(args, "fused_bn", True) and gpu_cl:
-            fuse_native_layers(model, native_conv=use_native_conv, min_pixels=min_px)
+            fuse_native_layers(model, native_conv=use_native_conv, min_pixels=min_px, native_f32=f32)
         else:
-            set_conv_routing(model, use_native_conv, min_px)
+            set_conv_routing(model, use_native_conv, min_px, f32)
         # per-step flip cache of the stride-1 backward-data weights (ops/conv.py)
         self._native_conv_cache = use_native_conv
         params_in_order = [p for p in model.parameters() if p.requires_grad]
@@ -144,7 +153,8 @@ class Trainer:
         from .graph import GraphedStep, auto_enabled
         cg = getattr(args, "cuda_graph", False)
         if cg is None:      # default: replay launch-bound steps (engine/graph.py)
-            cg = auto_enabled(args, self.device, self.world_size)
+            comm = self.ddp.comm
+            cg = auto_enabled(args, self.device, self.world_size, comm.kind if comm is not None else None)
         if cg and self.device.type == "cuda":
             self.graphed = GraphedStep(self)
 
@@ -276,9 +286,17 @@ class Trainer:
             self.ddp.verify_sequence()
 
     def _host_touch(self) -> None:
-        """Host touch point: surface a tripped communicator watchdog as an exception."""
+        """Host touch point: surface a tripped communicator watchdog, or a stream-K conv whose
+        consumer gave up waiting for a contributor (its tile was poisoned with NaN), as an
+        exception."""
         if self.ddp is not None:
             self.ddp.check_comm()
+        if getattr(self, "_streamk", False):
+            from .. import ops
+            n = ops.native().conv_sk_errors()
+            if n:
+                raise RuntimeError(f"stream-K convolution: {n} tile(s) gave up waiting for a contributing "
+                                   "block (results poisoned with NaN); rerun with --conv-streamk off")
 
     def train_one_epoch(self, epoch: int, loader, train_sampler=None) -> EpochStats:
         """One epoch with the reference's stdout contract (train_ddp.py:170-263).

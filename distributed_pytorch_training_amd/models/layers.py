@@ -173,19 +173,22 @@ class GemmConv1x1(nn.Conv2d):
         return y.permute(0, 3, 1, 2)
 
 
-def set_conv_routing(model: nn.Module, native_conv: bool = True, min_pixels=None) -> None:
+def set_conv_routing(model: nn.Module, native_conv: bool = True, min_pixels=None, native_f32=None) -> None:
     """Per-model conv routing: MFMA kernels (ops/conv.py, ops/conv_f32.py) or MIOpen, stored on
-    each conv; plain ``nn.Conv2d`` modules become ``NativeConv2d`` (same parameters)."""
+    each conv; plain ``nn.Conv2d`` modules become ``NativeConv2d`` (same parameters).
+    ``native_f32``: fp32 (no autocast) convs on the fp32 MFMA kernels for this model (None: the
+    process default, ops/conv_f32.py ``ENABLED``)."""
     for m in model.modules():
         if type(m) is nn.Conv2d:
             m.__class__ = NativeConv2d
         if isinstance(m, nn.Conv2d):
             m.dpt_native_conv = bool(native_conv)
             m.dpt_min_pixels = min_pixels
+            m.dpt_native_conv_f32 = None if native_f32 is None else bool(native_f32)
 
 
 def fuse_native_layers(model: nn.Module, gemm_1x1: bool = False, native_conv: bool = True,
-                       min_pixels=None) -> int:
+                       min_pixels=None, native_f32=None) -> int:
     """Install the gfx950 fused layers: BatchNorm2d -> FusedBatchNorm2d (fused with ReLU /
     residual add by the model's ``bn_act`` calls) and MaxPool2d -> FusedMaxPool2d.  Modules
     keep their parameters/buffers, so state dicts and checkpoints are unchanged.
@@ -193,7 +196,7 @@ def fuse_native_layers(model: nn.Module, gemm_1x1: bool = False, native_conv: bo
     ``native_conv`` / ``min_pixels``: this model's conv routing (MFMA kernels or MIOpen; convs
     with fewer output pixels than ``min_pixels`` stay on MIOpen), stored on each conv module so
     two models in one process never share it."""
-    set_conv_routing(model, native_conv, min_pixels)
+    set_conv_routing(model, native_conv, min_pixels, native_f32)
     n = fuse_batchnorm(model)
     for parent in model.modules():
         for name, child in list(parent.named_children()):

@@ -46,8 +46,10 @@ def _in_scope(r: int, s: int, stride: int) -> bool:
     return True
 
 
-def supported(x: torch.Tensor, w: torch.Tensor, bias, stride, padding, dilation, groups) -> bool:
-    if not (ENABLED and x.is_cuda and native_available() and x.dtype == torch.float32 and w.dtype == torch.float32
+def supported(x: torch.Tensor, w: torch.Tensor, bias, stride, padding, dilation, groups,
+              enabled: bool | None = None) -> bool:
+    """``enabled``: the conv module's own routing (``dpt_native_conv_f32``); None = ``ENABLED``."""
+    if not ((ENABLED if enabled is None else enabled) and x.is_cuda and native_available() and x.dtype == torch.float32 and w.dtype == torch.float32
             and x.dim() == 4 and groups == 1 and bias is None):
         return False
     if torch.is_autocast_enabled("cuda"):
@@ -97,16 +99,17 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Ten
 
 class NativeConv2d(nn.Conv2d):
     """``nn.Conv2d`` whose fp32 (no autocast) channels_last forward runs the fp32 MFMA kernels
-    when the model's routing allows it (``dpt_native_conv``, set by models/layers.py
-    ``set_conv_routing``); anything else is ``nn.Conv2d``'s own path.  Under autocast the shadow
+    when the model's routing allows it (``dpt_native_conv`` and ``dpt_native_conv_f32``, set per
+    model by models/layers.py ``set_conv_routing``); anything else is ``nn.Conv2d``'s own path.  Under autocast the shadow
     subclass (parallel/shadow.py ``ShadowConv2d``) takes the bf16 / fp16 MFMA kernels instead.
     Parameters and state-dict keys are the Conv2d's."""
 
     dpt_native_conv = True
     dpt_min_pixels = None
+    dpt_native_conv_f32 = None    # per-model fp32 routing (set_conv_routing); None = ENABLED (env)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.dpt_native_conv and supported(x, self.weight, self.bias, self.stride, self.padding,
-                                              self.dilation, self.groups):
+                                              self.dilation, self.groups, self.dpt_native_conv_f32):
             return conv2d(x, self.weight, self.stride[0], self.padding[0])
         return super().forward(x)

@@ -66,7 +66,18 @@ def setup_distributed(backend: str = "auto", timeout_s: int = 1800) -> Tuple[int
     return info.rank, info.world_size, info.local_rank
 
 
-def init_distributed(backend: str = "auto", timeout_s: int = 1800) -> DistInfo:
+def init_distributed(backend: str = "auto", timeout_s: int = 1800, shared_gpu: bool = False) -> DistInfo:
+    """``shared_gpu`` (testing, ``--rehearse-shared-gpu``): every rank on cuda:0 over a gloo group."""
+    if shared_gpu and is_distributed():
+        if not gpu_available():
+            raise RuntimeError("--rehearse-shared-gpu needs a visible GPU")
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        if not dist.is_initialized():
+            dist.init_process_group(backend="gloo", init_method="env://",
+                                    timeout=datetime.timedelta(seconds=timeout_s))
+        return DistInfo(int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]),
+                        int(os.environ.get("LOCAL_RANK", "0")), "gloo", dev)
     if not is_distributed():
         dev = torch.device("cuda:0") if gpu_available() else torch.device("cpu")
         if dev.type == "cuda":

@@ -346,7 +346,7 @@ def test_bench_deadline_survives_hung_child_jobs(tmp_path):
     assert rec["baseline"]["vs_baseline_source"] == "stock_reference_constant"
     w = rec["extra_windows"]["resnet50_fp32"]
     assert "error" in w and "cmd" in w, w
-    assert wall < 90 + 30, wall            # deadline + process start-up slack
+    assert wall < 90 + 20, wall            # the deadline counts from process creation; + teardown
     time.sleep(1.0)
     left = _tagged_procs(tag)
     assert not left, left

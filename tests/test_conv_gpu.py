@@ -933,3 +933,49 @@ def test_fwd_shape_policy_matches_fp32(cuda, shape, bits):
     yf = y.float()
     torch.testing.assert_close(ps.sum(1), yf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(pq.sum(1), (yf * yf).sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+
+
+BREG_SHAPES = SHAPES + [(s[0], s[1], s[2], s[3], s[4], 3, 1, 1) for s in HALO_SHAPES] + [
+    (8, 1024, 14, 14, 256, 1, 1, 0),   # the deep reducing 1x1 of ResNet-50 layer 3 (16 K-steps)
+    (2, 256, 14, 14, 256, 3, 1, 1),    # layer-3 3x3 (HALO, 4 channel blocks)
+]
+
+
+@pytest.mark.parametrize("shape", BREG_SHAPES)
+def test_breg_b_operand_in_registers_matches_lds_path(cuda, shape):
+    """conv_set_breg (B operand straight from L2 into VGPRs, A double-buffered in LDS; bit 0 the
+    3x3 HALO loop, bit 1 every other single-stage conv) against the default LDS-fed kernels: the
+    same K-steps and k-slices in the same order, so the conv outputs are bitwise identical; the
+    BatchNorm partials are summed over a different wave split (close, not equal).  Forward with
+    statistics and, for stride 1, backward-data with the BN+ReLU statistics epilogue."""
+    N, C, H, W, Cout, k, s, p = shape
+    C_ = ops.native()
+    x, w = _operands(cuda, N, C, H, W, Cout, k, seed=31)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    g = torch.Generator(device=cuda).manual_seed(32)
+    gy = torch.randn(N, Cout, Ho, Wo, device=cuda, generator=g).to(torch.bfloat16).contiguous(memory_format=CL)
+    bn_x = torch.randn(x.shape, device=cuda, generator=g).to(torch.bfloat16).contiguous(memory_format=CL)
+    bn_mean = torch.randn(C, device=cuda, generator=g)
+    bn_coef = torch.randn(2 * C, device=cuda, generator=g)
+    out = {}
+    try:
+        for mode in (0, 3):
+            C_.conv_set_breg(mode)
+            y, ps, pq = C_.conv_fwd(x, w, s, p, True)
+            res = [y, ps, pq]
+            if s == 1:
+                dx, p1, p2, _ = C_.conv_dgrad_bnstats(gy, w, p, bn_x, bn_mean, bn_coef)
+                res += [dx, p1, p2]
+            torch.cuda.synchronize()
+            out[mode] = res
+    finally:
+        C_.conv_set_breg(0)
+    ref = F.conv2d(x.float(), w.float(), stride=s, padding=p)
+    torch.testing.assert_close(out[3][0].float(), ref, rtol=1e-2, atol=1e-2)
+    assert torch.equal(out[3][0].view(torch.int16), out[0][0].view(torch.int16))
+    for a, b in zip(out[3][1:3], out[0][1:3]):
+        torch.testing.assert_close(a.sum(1), b.sum(1), rtol=1e-5, atol=1e-4)
+    if s == 1:
+        assert torch.equal(out[3][3].view(torch.int16), out[0][3].view(torch.int16))
+        for a, b in zip(out[3][4:], out[0][4:]):
+            torch.testing.assert_close(a.sum(1), b.sum(1), rtol=1e-5, atol=1e-4)
