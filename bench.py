@@ -112,10 +112,11 @@ def parse(argv=None):
                     help="seconds the stock child job may take before it is killed (then no same-box number)")
     ap.add_argument("--extra-windows", default="auto", choices=["auto", "on", "off"],
                     help="after the headline (and the stock job), fresh child jobs on the same GPUs for "
-                         "BASELINE.json configs 4 and 5: at 4 GPUs the fp32 ResNet-50 run (AMP vs FP32 with "
-                         "the sync profile), at 8 GPUs ViT-B/16 bf16 AdamW at several bucket caps; recorded "
-                         "under extra_windows, never part of the headline (auto: on for the native ResNet-50 "
-                         "bf16 engine on 4 or 8 GPUs)")
+                         "BASELINE.json configs 4 and 5: at 1 GPU the ViT-B/16 bf16 AdamW step and the fp32 "
+                         "ResNet-50 step, at 4 GPUs the fp32 ResNet-50 run (AMP vs FP32 with the sync "
+                         "profile), at 8 GPUs ViT-B/16 at several bucket caps; recorded under extra_windows, "
+                         "never part of the headline (auto: on for the native ResNet-50 bf16 engine on 1, 4 "
+                         "or 8 GPUs)")
     ap.add_argument("--extra-timeout", type=float, default=240.0,
                     help="seconds each extra-window child job may take")
     ap.add_argument("--extra-steps", type=int, default=10,
@@ -507,7 +508,7 @@ def _window(rec: dict, argv: list) -> dict:
     cfg = rec.get("config", {})
     return {"value": rec.get("value"), "unit": rec.get("unit"), "ms_per_step": rec.get("ms_per_step"),
             "n_gpus": rec.get("n_gpus"), "steps": rec.get("steps"), "dtype": rec.get("dtype"),
-            "model": cfg.get("model"), "per_gpu_batch": cfg.get("per_gpu_batch"),
+            "model": cfg.get("model"), "impl": cfg.get("impl"), "per_gpu_batch": cfg.get("per_gpu_batch"),
             "bucket_cap_mb": cfg.get("bucket_cap_mb"), "optimizer": cfg.get("optimizer"),
             "pct_step_allreduce": rec.get("pct_step_allreduce"),
             "pct_step_exposed_comm": rec.get("pct_step_exposed_comm"),
@@ -524,7 +525,14 @@ def extra_windows_plan(a, ws: int, forced: bool = False) -> list:
     steps = ["--steps", str(a.extra_steps), "--warmup", "3", "--profile-steps", "6"]
     r50_shape = ["--model", a.model, "--batch-size", str(a.batch_size), "--image-size", str(a.image_size)]
     plan = []
-    if (ws == 4 or forced) and not a.no_amp:
+    vit1 = ("vit_b16_bucket25mb", common[:-1] + ["25", "--model", "vit_b_16", "--batch-size", "128",
+                                                 "--optimizer", "adamw"] + steps)
+    if ws == 1 and not a.no_amp:
+        # one GPU: the ViT-B/16 step (BASELINE.json config 5's model, native and stock engines) and
+        # the fp32 ResNet-50 step (config 4's AMP-vs-FP32 pair) measured under the headline's record
+        plan.append(vit1)
+        plan.append(("vit_b16_stock", vit1[1] + ["--impl", "torch"]))
+    if (ws in (1, 4) or forced) and not a.no_amp:
         plan.append(("resnet50_fp32", common + r50_shape + ["--no-amp"] + steps))
     if ws == 8:
         vit = [(f"vit_b16_bucket{float(cap):g}mb",
@@ -789,7 +797,7 @@ def main(argv=None) -> int:
     extra_on = a.extra_windows == "on" or (a.extra_windows == "auto" and a.impl == "native"
                                             and device.type == "cuda" and not a.rehearse_shared_gpu
                                             and not a.fake_pg and a.model == "resnet50" and not a.no_amp
-                                            and ws in (4, 8))
+                                            and ws in (1, 4, 8))
     extra_plan = extra_windows_plan(a, ws, forced=a.extra_windows == "on") if extra_on else []
     t_dead = deadline_at(a)
     printed = []

@@ -37,6 +37,12 @@ def granule(v: int, g: int = 8) -> int:
     return (v + g - 1) // g * g
 
 
+# rocprofv3's VGPR_Count on gfx950 decodes the kernel descriptor's register granules as 4 VGPRs
+# where gfx950 allocates 8: a kernel the compiler reports at 118-123 VGPRs
+# (-Rpass-analysis=kernel-resource-usage) shows up as 64.  Scale it back.
+TRACE_VGPR_SCALE = 2
+
+
 def blocks_per_cu(lds: int, vgpr: int, agpr: int, wg_threads: int) -> int:
     waves_per_block = max(1, (wg_threads + 63) // 64)
     waves_per_simd_per_block = max(1, math.ceil(waves_per_block / 4))
@@ -77,11 +83,12 @@ def main(argv=None):
         total += dur
         wg = int(r["Workgroup_Size_X"]) * int(r["Workgroup_Size_Y"]) * int(r["Workgroup_Size_Z"])
         tiles = (int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])) // max(wg, 1)
-        bpc = blocks_per_cu(int(r["LDS_Block_Size"]), int(r["VGPR_Count"]), int(r["Accum_VGPR_Count"]), wg)
+        bpc = blocks_per_cu(int(r["LDS_Block_Size"]), TRACE_VGPR_SCALE * int(r["VGPR_Count"]),
+                            TRACE_VGPR_SCALE * int(r["Accum_VGPR_Count"]), wg)
         slots = CUS * max(bpc, 1)
         eff = tiles / (math.ceil(tiles / slots) * slots) if tiles else 1.0
         key = (short(r["Kernel_Name"]), tiles, bpc, int(r["LDS_Block_Size"]),
-               granule(int(r["VGPR_Count"])) + granule(int(r["Accum_VGPR_Count"])))
+               granule(TRACE_VGPR_SCALE * int(r["VGPR_Count"])) + granule(TRACE_VGPR_SCALE * int(r["Accum_VGPR_Count"])))
         e = agg[key]
         e["n"] += 1
         e["ns"] += dur

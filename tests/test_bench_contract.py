@@ -269,6 +269,10 @@ def test_extra_windows_plan():
         else:
             assert argv[argv.index("--rccl-channels") + 1] == name[len("resnet50_rccl_channels"):]
     assert bench.extra_windows_plan(bench.parse(["--gpus", "2"]), 2) == []
+    plan1 = dict(bench.extra_windows_plan(bench.parse([]), 1))
+    assert list(plan1) == ["vit_b16_bucket25mb", "vit_b16_stock", "resnet50_fp32"]
+    assert plan1["vit_b16_stock"][-2:] == ["--impl", "torch"]
+    assert plan1["vit_b16_bucket25mb"][plan1["vit_b16_bucket25mb"].index("--model") + 1] == "vit_b_16"
     assert bench.extra_windows_plan(bench.parse(["--gpus", "4", "--no-amp"]), 4) == []
 
 
