@@ -12,7 +12,8 @@ on by default (launch-bound step).  Two checks (bench/graph_parity.py):
   work would be off by ~1);
 * free-running: 300 steps replayed vs 300 eager from the same init on the learnable synthetic
   task (class prototypes + fresh noise, ``--synthetic-task prototypes``); the windowed loss curves
-  must stay within a band after the first 50 steps (the lr 0.1 transient, only bounded).  (On the default 4-batch random-label pool the run is a memorisation
+  must stay within a band after the first 150 steps (the lr 0.1 transient, only bounded) and both
+  runs must learn the task.  (On the default 4-batch random-label pool the run is a memorisation
   race whose speed differs between two EAGER runs of this configuration by as much as between
   replay and eager - MIOpen's find-mode algorithms are not deterministic - so that task cannot
   tell replay from eager; profiles/graph_vs_eager_r4.md has both.)
@@ -58,12 +59,20 @@ def test_replayed_run_tracks_eager_run(benchmark_mode):
     curves = graph_parity.free(300, [], task="prototypes")
     g, e = curves["--cuda-graph"], curves["--no-cuda-graph"]
     w = 50
-    # steps 0-49 are lr 0.1's violent transient (25-step means 2.0-2.5 against ln 10 = 2.3): its
-    # path is chaotic, and whichever run leaves it first has differed between full-suite runs in
-    # both directions (1.04 vs 1.29 and 1.37 vs 1.06), so it is only checked to stay bounded there
+    # steps 0-149 are lr 0.1's violent transient (25-step means 2.0-3.1 against ln 10 = 2.3): its
+    # path is chaotic, and which run leaves it first - and whether a second spike follows, as late
+    # as steps 50-99 (0.46 / 0.34 in one eager run against 0.08 / 0.05 replayed, full-suite run of
+    # round 6) - has differed between runs in both directions, so it is only checked to stay bounded
+    # there; a replay that dropped or repeated work would not leave ln 10 at all
     a0, b0 = sum(g[:w]) / w, sum(e[:w]) / w
-    assert a0 < 3.0 and b0 < 3.0 and max(a0, b0) <= 1.6 * min(a0, b0), (a0, b0)
-    for i in range(w, 300, w):
+    assert a0 < 3.5 and b0 < 3.5 and max(a0, b0) <= 1.6 * min(a0, b0), (a0, b0)
+    for i in range(w, 150, w):
+        a = sum(g[i:i + w]) / w
+        b = sum(e[i:i + w]) / w
+        assert a < 1.0 and b < 1.0, (i, a, b)
+    # settled: the two runs learn the task to the same loss
+    for i in range(150, 300, w):
         a = sum(g[i:i + w]) / w
         b = sum(e[i:i + w]) / w
         assert abs(a - b) <= 0.1 * max(b, 0.5) + 0.05, (i, a, b)
+    assert sum(g[-w:]) / w < 0.2 and sum(e[-w:]) / w < 0.2
