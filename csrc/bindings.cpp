@@ -1286,6 +1286,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_set_big", &dpt::conv_set_big, py::arg("on"));
   m.def("conv_set_halo", &dpt::conv_set_halo, py::arg("on"));
   m.def("conv_set_breg", &dpt::conv_set_breg, py::arg("mode"));
+  m.def("conv_set_wgrad_stages", &dpt::conv_set_wgrad_stages, py::arg("mode"));
   m.def("conv_get_breg", &dpt::conv_get_breg);
   m.def("conv_set_streamk", &dpt::conv_set_streamk, py::arg("mode"), py::arg("eff") = 0.0);
   m.def("conv_get_streamk", &dpt::conv_get_streamk);

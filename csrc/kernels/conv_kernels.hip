@@ -2918,6 +2918,7 @@ void launch_conv_dgrad_s2(const uint16_t* dy, const uint16_t* w, uint16_t* dx, i
 static int g_wgrad_halo = 5;
 static int wgrad_halo_mode(int C = 0) {
   if (g_wgrad_halo == 5) return C == 64 ? 3 : 0;
+  if (g_wgrad_halo == 6) return C == 64 ? 4 : 0;  // A/B: the double-buffered strip on the same convs
   return g_wgrad_halo;
 }
 void conv_set_wgrad_halo(int on) { g_wgrad_halo = on; }
@@ -2943,6 +2944,12 @@ static FastDiv make_fastdiv(uint32_t d) {
 // conv_set_wgrad_target(n > 0): n blocks for every shape (the sweep); 0: this policy.
 static int g_wgrad_target = 0;
 void conv_set_wgrad_target(int blocks) { g_wgrad_target = blocks; }
+// backward-weight K loop depth (A/B, conv_set_wgrad_stages): 0 = the single-stage tile (4 blocks
+// per CU); 1 = the double-buffered tile (2 blocks per CU) for grids of at most one wave at 2
+// blocks per CU - there residency is set by the grid, not by LDS, so the deeper pipeline costs
+// no resident block; 2 = double-buffered everywhere
+static int g_wgrad_stages = 0;
+void conv_set_wgrad_stages(int mode) { g_wgrad_stages = mode; }
 static int wgrad_target(int R, int S, int stride, int steps) {
   if (g_wgrad_target > 0) return g_wgrad_target;
   if (R * S == 1 && stride == 1) return 512;
@@ -3060,7 +3067,8 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* part, void*
   } else if (pl.bmw == 256) {  // conv_wgrad_plan chose the 8-wave 256 x 256 tile
     if (a.f16) throw std::runtime_error("conv_wgrad: the 256 x 256 variant is bf16 only");
     hipLaunchKernelGGL((conv_wgrad_kernel<256, 256, 2, false, 512>), grid, dim3(512), 0, st, a);
-  } else if ((v == 1 || v == 2) && pl.bnw <= 128) {
+  } else if ((v == 1 || v == 2 || (!a.f16 && (g_wgrad_stages == 2 ||
+                                             (g_wgrad_stages == 1 && grid.x <= 2u * 256u)))) && pl.bnw <= 128) {
     if (pl.bmw == 128 && pl.bnw == 128) wgrad_launch<128, 128, 2>(grid, block, st, a);
     else if (pl.bmw == 128) wgrad_launch<128, 64, 2>(grid, block, st, a);
     else if (pl.bnw == 128) wgrad_launch<64, 128, 2>(grid, block, st, a);

@@ -155,6 +155,7 @@ bool conv_supported_narrow(int C, int Cout, int S);  // C = 16/32 with S % (64/C
 int conv_m_tiles(int64_t M);
 void conv_set_variant(int v);
 void conv_set_big(int on);  // 8-wave 256-row tiles where conv_big_auto picks them (default off)
+void conv_set_wgrad_stages(int mode);  // backward-weight 2-stage K loop: 1 = one-wave grids, 2 = all (A/B)
 void conv_set_breg(int mode);  // B operand in VGPRs: bit 0 HALO 3x3, bit 1 other convs (A/B)
 int conv_get_breg();
 void conv_set_halo(int on);  // 3x3 / stride-1 halo K loop (default on, DPT_CONV_HALO)

@@ -979,3 +979,30 @@ def test_breg_b_operand_in_registers_matches_lds_path(cuda, shape):
         assert torch.equal(out[3][3].view(torch.int16), out[0][3].view(torch.int16))
         for a, b in zip(out[3][4:], out[0][4:]):
             torch.testing.assert_close(a.sum(1), b.sum(1), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape", SHAPES + [(8, 1024, 14, 14, 256, 1, 1, 0), (4, 256, 14, 14, 256, 3, 1, 1)])
+def test_wgrad_stage_policy_matches_single_stage(cuda, shape):
+    """conv_set_wgrad_stages (the double-buffered backward-weight K loop for one-wave grids, 1, or
+    everywhere, 2) against the single-stage tile: same tiles, splits and K order - equal results;
+    and both against an fp32 reference."""
+    N, C, H, W, Cout, k, s, p = shape
+    C_ = ops.native()
+    x, w = _operands(cuda, N, C, H, W, Cout, k, seed=41)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    g = torch.Generator(device=cuda).manual_seed(42)
+    gy = torch.randn(N, Cout, Ho, Wo, device=cuda, generator=g).to(torch.bfloat16).contiguous(memory_format=CL)
+    out = {}
+    try:
+        for mode in (0, 1, 2):
+            C_.conv_set_wgrad_stages(mode)
+            out[mode] = C_.conv_wgrad(gy, x, list(w.shape), s, p, True)
+            torch.cuda.synchronize()
+    finally:
+        C_.conv_set_wgrad_stages(0)
+    ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, gy.float(), stride=s, padding=p)
+    scale = ref.abs().max().item()
+    for mode in (0, 2):
+        torch.testing.assert_close(out[mode], ref, rtol=1e-2, atol=1e-3 * scale + 1e-3)
+    for mode in (1, 2):
+        torch.testing.assert_close(out[mode], out[0], rtol=1e-5, atol=1e-5 * scale)
