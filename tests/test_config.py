@@ -48,3 +48,24 @@ def test_types_and_overrides():
     assert a.backend == "rccl" and a.betas == (0.8, 0.9)
     with pytest.raises(SystemExit):
         parse_args(["--epochs", "x"])
+
+
+def test_rehearse_shared_gpu_needs_a_host_bridge(monkeypatch, tmp_path):
+    """--rehearse-shared-gpu (testing: N ranks on one GPU) is off by default and refuses a
+    communicator that needs one GPU per rank before touching the process group."""
+    from distributed_pytorch_training_amd.engine import run
+    assert parse_args([]).rehearse_shared_gpu is False
+    for k, v in {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"}.items():
+        monkeypatch.setenv(k, v)
+    with pytest.raises(SystemExit, match="host-async"):
+        run.main(["--dataset", "synthetic", "--rehearse-shared-gpu", "--comm", "rccl",
+                  "--output-dir", str(tmp_path)])
+
+
+def test_shared_gpu_bootstrap_needs_a_gpu(monkeypatch):
+    from distributed_pytorch_training_amd.utils import dist as udist
+    for k, v in {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"}.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setattr(udist, "gpu_available", lambda: False)
+    with pytest.raises(RuntimeError, match="visible GPU"):
+        udist.init_distributed("auto", 30, shared_gpu=True)
