@@ -2627,6 +2627,7 @@ static bool conv_fwd_big(int v, ConvFwdArgs& a, hipStream_t s) {
 //      0.106 without; bench/conv_variant_sweep.py, profiles/conv_variant_sweep_r4.md);
 //   2: the 3x3 stride-2 256->256 conv (K = 2304, M >= 32768) -> the 8-wave 256x256 tile (variant
 //      9): 0.081 -> 0.069 ms, 1.05-1.08x MIOpen.
+//   16: the s2d stem's 4x4 conv (C = 16) on the 2-stage K loop (variant 1).
 //   4 / 8: 1x1 stride-1 convs with the statistics epilogue on grids under 1,024 tiles (the deep
 //      reducing convs at 14x14 / 7x7, latency-bound with ~3 resident blocks per CU:
 //      profiles/step_pmc_r5.md) -> the BK = 32 pipelined K loop, 2 stages (variant 14, 4 blocks
@@ -2643,6 +2644,9 @@ static int fwd_shape_variant(const ConvFwdArgs& a, bool stats) {
   if ((g_fwd_shape_policy & 12) && stats && a.R == 1 && a.S == 1 && a.stride == 1 && a.C % 32 == 0 &&
       (int64_t)a.m_tiles * a.n_tiles < 1024)
     return (g_fwd_shape_policy & 4) ? 14 : 7;
+  // 16: the 16-channel space-to-depth stem (4 K-steps, 6 resident blocks per CU, latency-bound)
+  // on the double-buffered K loop (variant 1)
+  if ((g_fwd_shape_policy & 16) && a.C == 16) return 1;
   return 0;
 }
 
