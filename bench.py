@@ -142,6 +142,7 @@ ENV_PREFIXES = ("DPT_", "NCCL_", "RCCL_", "MIOPEN_", "HIP_", "HSA_", "AMD_", "GP
                 "PYTORCH_TUNABLEOP", "TORCH_NCCL", "OMP_NUM_THREADS")
 CHILD_MARK = "DPT_BENCH_LAUNCHER"
 DEADLINE_MARK = "DPT_BENCH_DEADLINE_AT"   # absolute epoch deadline, handed from a launcher to its ranks
+RECORD_MARK = "DPT_BENCH_RECORD_FILE"     # a file rank 0 creates once its record is written (launcher)
 CHILD_JOB_MARK = "DPT_BENCH_CHILD_JOB"     # set in the stock / extra-window child jobs
 
 
@@ -160,7 +161,7 @@ rccl_log = None  # distributed_pytorch_training_amd.utils.rccl_log, imported by 
 
 def env_in_effect() -> dict:
     return {k: v for k, v in sorted(os.environ.items())
-            if k.startswith(ENV_PREFIXES) and k not in (CHILD_MARK, DEADLINE_MARK, CHILD_JOB_MARK)}
+            if k.startswith(ENV_PREFIXES) and k not in (CHILD_MARK, DEADLINE_MARK, CHILD_JOB_MARK, RECORD_MARK)}
 
 
 def _sig(v: float, digits: int = 6) -> float:
@@ -277,10 +278,16 @@ def launch_ranks(a, argv, grace_s: float = 30.0) -> int:
     child exit status; when one rank fails, the survivors get ``grace_s`` to finish (they
     normally error out of their collective) and are then terminated, so a dead peer can not
     leave the node hanging.  The ranks stay in this process's group (a ``killpg`` of the job
-    reaches them) and inherit the job's absolute deadline; a SIGTERM/SIGINT to this launcher is
-    passed on to them, and ranks still alive 60 s past the deadline are ended."""
+    reaches them) and inherit the job's absolute deadline; a SIGTERM to this launcher is passed on
+    to them, and once rank 0 has written its record, ranks still alive 60 s past the deadline (a
+    teardown that hangs: 60 s after the record and past the deadline) are ended - a headline window
+    still being measured is never cut."""
+    import tempfile
     n = a.gpus
     t_dead = deadline_at(a)
+    fd, mark = tempfile.mkstemp(prefix="dpt_bench_record_")
+    os.close(fd)
+    os.remove(mark)
     ngpu = _visible_gpus()
     if a.rehearse_shared_gpu:
         if ngpu < 1:
@@ -300,6 +307,7 @@ def launch_ranks(a, argv, grace_s: float = 30.0) -> int:
                    GROUP_RANK="0", ROLE_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         env[CHILD_MARK] = "self"
         env[DEADLINE_MARK] = repr(t_dead)
+        env[RECORD_MARK] = mark
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable, script, *argv], env=env))
     rcs = [None] * n
@@ -327,9 +335,11 @@ def launch_ranks(a, argv, grace_s: float = 30.0) -> int:
                     if rcs[i] not in (None, 0) and failed_at is None:
                         failed_at = time.time()
                         print(f"bench: rank {i} exited with status {rcs[i]}", file=sys.stderr)
-            if failed_at is None and time.time() > t_dead + 60:
+            if failed_at is None and time.time() > t_dead + 60 and os.path.exists(mark) and \
+                    time.time() > os.path.getmtime(mark) + 60:
                 failed_at = time.time() - grace_s - 1   # end them now
-                print("bench: ranks still running 60 s past the deadline; terminating them", file=sys.stderr)
+                print("bench: ranks still running 60 s after the record, past the deadline; terminating them",
+                      file=sys.stderr)
             if failed_at is not None and time.time() - failed_at > grace_s:
                 for i, p in enumerate(procs):
                     if rcs[i] is None:
@@ -354,6 +364,10 @@ def launch_ranks(a, argv, grace_s: float = 30.0) -> int:
     finally:
         for s, h in old.items():
             signal.signal(s, h)
+        try:
+            os.remove(mark)
+        except OSError:
+            pass
     rcs = [124 if rc is None else rc for rc in rcs]
     bad = [rc for rc in rcs if rc != 0]
     if not bad:
@@ -462,7 +476,7 @@ def _child_env() -> dict:
     """This job's environment minus its launcher variables (a child picks its own rendezvous and
     self-launches its ranks), marked as a child job."""
     drop = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
-            "MASTER_PORT", "GROUP_WORLD_SIZE", "ROLE_WORLD_SIZE", CHILD_MARK, DEADLINE_MARK, "NCCL_DEBUG",
+            "MASTER_PORT", "GROUP_WORLD_SIZE", "ROLE_WORLD_SIZE", CHILD_MARK, DEADLINE_MARK, RECORD_MARK, "NCCL_DEBUG",
             "NCCL_DEBUG_FILE", "NCCL_DEBUG_SUBSYS")
     env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
     env[CHILD_JOB_MARK] = "1"
@@ -527,9 +541,9 @@ def extra_windows_plan(a, ws: int, forced: bool = False) -> list:
     plan = []
     vit1 = ("vit_b16_bucket25mb", common[:-1] + ["25", "--model", "vit_b_16", "--batch-size", "128",
                                                  "--optimizer", "adamw"] + steps)
-    if ws == 1 and not a.no_amp:
-        # one GPU: the ViT-B/16 step (BASELINE.json config 5's model, native and stock engines) and
-        # the fp32 ResNet-50 step (config 4's AMP-vs-FP32 pair) measured under the headline's record
+    if ws == 1 and not a.no_amp and a.model == "resnet50" and a.image_size == 224:
+        # one GPU, headline config: the ViT-B/16 step (BASELINE.json config 5's model, native and
+        # stock engines) beside the fp32 ResNet-50 step (config 4's AMP-vs-FP32 pair)
         plan.append(vit1)
         plan.append(("vit_b16_stock", vit1[1] + ["--impl", "torch"]))
     if (ws in (1, 4) or forced) and not a.no_amp:
@@ -801,17 +815,27 @@ def main(argv=None) -> int:
     extra_plan = extra_windows_plan(a, ws, forced=a.extra_windows == "on") if extra_on else []
     t_dead = deadline_at(a)
     printed = []
+    t_headline = time.time()
 
     def emit():
         """Print rank 0's ONE JSON line (and append it to --json-out) exactly once."""
         if rank != 0 or printed:
             return
         printed.append(True)
+        # wall-clock bookkeeping of the job (epoch seconds): when the headline window was done,
+        # the --deadline, and when this record was written
+        rec["timing"] = {"process_start": round(T_START, 3), "headline_done": round(t_headline, 3),
+                         "deadline": round(t_dead, 3), "record": round(time.time(), 3)}
         line = json.dumps(rec)
         print(line, flush=True)
         if a.json_out:
             with open(a.json_out, "a") as f:
                 f.write(line + "\n")
+        if os.environ.get(RECORD_MARK):
+            try:
+                open(os.environ[RECORD_MARK], "w").close()
+            except OSError:
+                pass
 
     if stock_on or extra_plan:
         if rank == 0:

@@ -350,7 +350,13 @@ def test_bench_deadline_survives_hung_child_jobs(tmp_path):
     assert rec["baseline"]["vs_baseline_source"] == "stock_reference_constant"
     w = rec["extra_windows"]["resnet50_fp32"]
     assert "error" in w and "cmd" in w, w
-    assert wall < 90 + 20, wall            # the deadline counts from process creation; + teardown
+    # the record is written by the deadline (or, when the headline window itself ran past it on a
+    # loaded CPU, right after the window: no child job is started then), plus the kill grace of a
+    # timed-out child job; the job then exits promptly
+    tm = rec["timing"]
+    assert tm["deadline"] - t0 <= 90 + 5, tm
+    assert tm["record"] <= max(tm["deadline"], tm["headline_done"]) + 12, tm
+    assert t0 + wall - tm["record"] < 30, (tm, t0, wall)
     time.sleep(1.0)
     left = _tagged_procs(tag)
     assert not left, left
