@@ -111,3 +111,53 @@ def test_rocprof_rows_reads_sqlite_and_csv(tmp_path):
     _write_trace(str(tmp_path / "kt"), [1.0] * len(KERNELS))
     rows = rocprof_rows.load_rows(str(tmp_path / "kt" / "run_kernel_trace.csv"))
     assert [r["Kernel_Name"] for r in rows] == KERNELS
+
+
+def _write_full_trace(path, rows):
+    cols = ["Kernel_Name", "Start_Timestamp", "End_Timestamp", "LDS_Block_Size", "VGPR_Count", "Accum_VGPR_Count",
+            "Workgroup_Size_X", "Workgroup_Size_Y", "Workgroup_Size_Z", "Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"]
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=cols)
+        w.writeheader()
+        t = 1000
+        for name, us, blocks, vgpr_trace, lds in rows:
+            w.writerow({"Kernel_Name": name, "Start_Timestamp": t, "End_Timestamp": t + int(us * 1000),
+                        "LDS_Block_Size": lds, "VGPR_Count": vgpr_trace, "Accum_VGPR_Count": 0,
+                        "Workgroup_Size_X": 256, "Workgroup_Size_Y": 1, "Workgroup_Size_Z": 1,
+                        "Grid_Size_X": 256 * blocks, "Grid_Size_Y": 1, "Grid_Size_Z": 1})
+            t += int(us * 1000) + 500
+
+
+def test_wave_efficiency_splits_tail_from_sub_wave_grids(tmp_path, capsys):
+    """Round 6: the idle estimate is split into the last-wave tail of grids of >= 1 wave and the
+    upper bound from grids smaller than one wave, and the trace's VGPR_Count (half the compiler's
+    count on gfx950) is scaled back before the resident-block model."""
+    # 64 in the trace = 128 VGPRs -> 4 blocks per CU -> 1024 slots
+    rows = [("void dpt::conv_fwd_kernel<1>(x)", 100.0, 1536, 64, 0),    # 1.5 waves: eff 0.75
+            ("void dpt::conv_wgrad_kernel<1>(x)", 100.0, 512, 64, 0),   # 0.5 wave: eff 0.5
+            ("void dpt::sgd_kernel<2>(float*)", 10.0, 256, 16, 0)] * 2
+    p = str(tmp_path / "kt.csv")
+    _write_full_trace(p, rows)
+    wave_efficiency.main([p, "--steps", "1"])
+    out = capsys.readouterr().out
+    multi = next(l for l in out.splitlines() if l.startswith("| >= 1 wave"))
+    sub = next(l for l in out.splitlines() if l.startswith("| < 1 wave"))
+    # last step only: conv 100 us x (1 - 0.75) = 25 us tail; wgrad 100 x 0.5 = 50 us upper bound
+    assert [c.strip() for c in multi.split("|")][3] == "0.025"
+    assert [c.strip() for c in sub.split("|")][3] == "0.050"
+    conv = next(l for l in out.splitlines() if "conv_fwd_kernel" in l)
+    assert [c.strip() for c in conv.split("|")][3] == "4" and [c.strip() for c in conv.split("|")][5] == "128"
+
+
+def test_selfcheck_acceptance_rule():
+    from distributed_pytorch_training_amd.engine import selfcheck
+    ok = {"loss": {"fp32": 6.9, "stock": 7.0, "native": 6.95},
+          "update_rel_vs_fp32": {"stock": 1.3, "native": 1.35},
+          "fc_update_rel_vs_fp32": {"stock": 0.32, "native": 0.31}, "moved": {"native": 1.0}}
+    assert selfcheck.check(ok) == []
+    bad = dict(ok, update_rel_vs_fp32={"stock": 1.0, "native": 2.0})        # a wrong engine's update
+    assert any("update_rel_vs_fp32" in b for b in selfcheck.check(bad))
+    bad = dict(ok, loss={"fp32": 6.9, "stock": 7.0, "native": 8.0})
+    assert any("native loss" in b for b in selfcheck.check(bad))
+    bad = dict(ok, moved={"native": 0.0})
+    assert any("did not move" in b for b in selfcheck.check(bad))
