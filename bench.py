@@ -868,13 +868,23 @@ def main(argv=None) -> int:
         def left() -> float:
             return t_dead - reserve - time.time()
 
-        stock = None
+        def take_stock(stock):
+            """Put the stock job's result into the record (as soon as it exists: a SIGTERM later
+            still prints it)."""
+            rec["baseline"]["stock_same_box"] = stock
+            if stock.get("img_s"):
+                rec["baseline"]["stock_same_box_img_s"] = stock["img_s"]
+                rec["baseline"]["vs_baseline_source"] = "stock_same_box (fresh child job, --impl torch)"
+                rec["vs_baseline"] = round(value / stock["img_s"], 4)
+
         if rank == 0 and stock_on:
             if left() >= 20:
-                stock = run_stock_baseline(a, min(a.stock_timeout, left()))
+                take_stock(run_stock_baseline(a, min(a.stock_timeout, left())))
             else:
-                stock = {"error": f"skipped: {max(0.0, left() + reserve):.0f} s left before the --deadline"}
+                take_stock({"error": f"skipped: {max(0.0, left() + reserve):.0f} s left before the --deadline"})
         extra = {}
+        if rank == 0 and extra_plan:
+            rec["extra_windows"] = extra    # filled window by window (a SIGTERM prints what is done)
         if rank == 0:
             t_extra = time.time()
             for name, argv in extra_plan:
@@ -892,14 +902,6 @@ def main(argv=None) -> int:
                 store.set(key, "1")
             else:
                 store.wait([key], datetime.timedelta(seconds=max(60.0, t_dead - time.time() + 60)))
-        if rank == 0 and extra_plan:
-            rec["extra_windows"] = extra
-        if rank == 0 and stock_on:
-            rec["baseline"]["stock_same_box"] = stock
-            if stock.get("img_s"):
-                rec["baseline"]["stock_same_box_img_s"] = stock["img_s"]
-                rec["baseline"]["vs_baseline_source"] = "stock_same_box (fresh child job, --impl torch)"
-                rec["vs_baseline"] = round(value / stock["img_s"], 4)
     emit()
     if ws > 1:
         dist.barrier()

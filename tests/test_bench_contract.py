@@ -360,3 +360,39 @@ def test_bench_deadline_survives_hung_child_jobs(tmp_path):
     time.sleep(1.0)
     left = _tagged_procs(tag)
     assert not left, left
+
+
+def test_bench_sigterm_during_child_jobs_still_prints_the_record(tmp_path):
+    """The driver's time limit arriving while a child job runs: SIGTERM to the self-launching
+    parent is forwarded to the ranks, rank 0 kills the child job's process group and prints its
+    one record (the stock run marked as not measured), and nothing of the job is left running."""
+    import signal
+    import time
+    import uuid
+    tag = uuid.uuid4().hex
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(DPT_TEST_HANG_CHILD="1", DPT_TEST_TAG=tag)
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--stock-baseline", "on",
+                          "--deadline", "600", *TINY], cwd=tmp_path, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True, env=env)
+    t0 = time.time()
+    seen = False
+    while time.time() - t0 < 500:
+        line = p.stderr.readline()
+        if not line:
+            break
+        if "headline measured" in line:
+            seen = True
+            break
+    assert seen, "no provisional record on stderr"
+    time.sleep(5.0)                     # the (hanging) stock child job is running now
+    p.send_signal(signal.SIGTERM)
+    out, err = p.communicate(timeout=120)
+    lines = _json_lines(out)
+    assert len(lines) == 1, (out, err[-2000:])
+    rec = lines[0]
+    _check(rec, 2)
+    assert "not measured: signal" in rec["baseline"]["stock_same_box"]["error"], rec["baseline"]
+    time.sleep(1.0)
+    left = _tagged_procs(tag)
+    assert not left, left
